@@ -1,0 +1,134 @@
+/*
+ * tfhe_hip.h — C ABI of libtfhe_hip.so, the MI355X-native TFHE programmable-bootstrap engine.
+ *
+ * This is the drop-in boundary for the reference's PBS path.  In the reference, JS callers reach
+ * the TFHE core through packages/wasm (tfhe-rs 0.8.7 compiled to WASM/N-API, an empty submodule
+ * here: .gitmodules:4, packages/pnpm-lock.yaml:1988-1995) and through the FHE server's
+ * /evaluate endpoint (e2e/test/fhe.test.ts:105-175).  Each entry point below names the reference
+ * interface it replaces.  Plain C: pointers + sizes, no torch / HIP types in signatures
+ * (streams are passed as void*).
+ *
+ * Conventions
+ *   - LWE ciphertexts: u64[dim + 1] = (a_0 .. a_{dim-1}, b), native torus Z_{2^64}.
+ *   - GLWE / BSK values: Z_p, p = 2^64 - 2^32 + 1, canonical in [0, p).
+ *   - BSK (standard domain): u64[n][(k+1)*l][k+1][N]; row index = c*l + lvl (c = component that
+ *     carries s_i * 2^(64 - base_log*(lvl+1))), column = GLWE component (0..k-1 mask, k body).
+ *   - KSK: u64[k*N][ks_level][n + 1], KSK[j][r] = LWE_s(s'_j * 2^(64 - ks_base_log*(r+1))).
+ *   - LUT ("accumulator"): u64[N] in Z_p (see tfhe_hip_lut_*).
+ *   - Every function returns 0 on success or a negative TFHE_HIP_E* code; it never aborts.
+ *     tfhe_hip_last_error() returns the message of the last failure on the calling thread.
+ *   - Ownership: the caller owns every host buffer; calls read/write them synchronously (the
+ *     *_async variants take DEVICE pointers and enqueue on the given HIP stream).  The library
+ *     owns device keys and workspaces (freed by tfhe_hip_destroy).
+ *   - Threading: a ctx is not re-entrant; calls on one ctx are serialized by an internal mutex.
+ */
+#ifndef TFHE_HIP_H
+#define TFHE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TFHE_HIP_OK 0
+#define TFHE_HIP_EINVAL (-1)      /* bad argument / size mismatch */
+#define TFHE_HIP_ENOMEM (-2)      /* host or device allocation failed */
+#define TFHE_HIP_EDEVICE (-3)     /* HIP runtime error */
+#define TFHE_HIP_ENOKEYS (-4)     /* keys not loaded */
+#define TFHE_HIP_EUNSUPPORTED (-5) /* parameter set not supported by the device kernels */
+
+#define TFHE_HIP_PRESET_GATE 0   /* n=630 k=1 N=1024, PBS 7x3, KS 2x8 (TFHE 128-bit default) */
+#define TFHE_HIP_PRESET_FHEVM 1  /* n=918 k=1 N=2048, PBS 23x1, KS 4x4 (PARAM_MESSAGE_2_CARRY_2_KS_PBS) */
+
+typedef struct tfhe_params {
+  uint32_t n, k, N;
+  uint32_t pbs_base_log, pbs_level;
+  uint32_t ks_base_log, ks_level;
+  int32_t lwe_noise_log2;  /* stddev as log2 of a torus fraction */
+  int32_t glwe_noise_log2;
+  uint32_t order;          /* 0 = PBS then KS (ciphertexts under the small key), 1 = KS then PBS */
+} tfhe_params;
+
+typedef struct tfhe_ctx tfhe_ctx;
+
+/* ---- parameters & sizes ------------------------------------------------------------------
+ * Replaces the tfhe-rs parameter constants selected by name in sdk/relayer/src/tfhe.ts:14-19. */
+int tfhe_hip_params_preset(int preset, tfhe_params* out);
+size_t tfhe_hip_bsk_len(const tfhe_params* p);
+size_t tfhe_hip_ksk_len(const tfhe_params* p);
+/* LWE dimension of PBS inputs/outputs (n for order 0, k*N for order 1). */
+uint32_t tfhe_hip_io_dim(const tfhe_params* p);
+
+/* ---- client-side key material (host) ------------------------------------------------------
+ * Replaces TfheClientKey.generate / ServerKey generation (sdk/relayer/src/tfhe.ts:20-28,
+ * generateKeys.js:20-31) for the deterministic seeded keys this engine consumes.
+ * Streams: LWE key 1, GLWE key 2, BSK_i 0x1000+i, KSK_j 0x100000+j (ChaCha20). */
+int tfhe_hip_keygen(const tfhe_params* p, uint64_t seed, uint64_t* lwe_key, uint64_t* glwe_key,
+                    uint64_t* bsk /* nullable */, uint64_t* ksk /* nullable */);
+/* Encrypt count torus messages; ciphertext q uses ChaCha stream (stream0 + q).
+ * Replaces the encrypt path of packages/luxfhejs/src/index.ts:127-141 (server-side /encrypt). */
+int tfhe_hip_lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, uint64_t seed,
+                         uint64_t stream0, const uint64_t* msgs, size_t count, uint64_t* out);
+/* phase = b - <a, s> (decryption before decoding); replaces /decrypt
+ * (packages/hardhat-plugin/src/index.ts:71-75). */
+int tfhe_hip_lwe_phase(uint32_t dim, const uint64_t* key, const uint64_t* ct, size_t count, uint64_t* out);
+/* LUT builders.  Replaces ServerKey::generate_accumulator (ml/biometrics/notebooks/main.rs:65-68). */
+int tfhe_hip_lut_constant(uint32_t N, uint64_t torus_value, uint64_t* lut);
+int tfhe_hip_lut_from_table(uint32_t N, uint32_t msg_modulus, const uint64_t* table, uint64_t delta_out,
+                            uint64_t* lut);
+
+/* ---- device engine ------------------------------------------------------------------------ */
+int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out);
+void tfhe_hip_destroy(tfhe_ctx* ctx);
+const char* tfhe_hip_last_error(void);
+int tfhe_hip_device(const tfhe_ctx* ctx);
+
+/* Upload standard-domain BSK and KSK (host memory) and convert the BSK to the device NTT layout.
+ * Replaces the packages/kms key-loader role (pinned-HBM key residency). */
+int tfhe_hip_load_keys(tfhe_ctx* ctx, const uint64_t* bsk, size_t bsk_len, const uint64_t* ksk, size_t ksk_len);
+/* Same, from DEVICE buffers on this ctx's device (e.g. after an RCCL broadcast of the keys). */
+int tfhe_hip_load_keys_device(tfhe_ctx* ctx, const uint64_t* d_bsk, size_t bsk_len, const uint64_t* d_ksk,
+                              size_t ksk_len);
+
+/* Full PBS of B ciphertexts: order 0 = blind-rotate -> sample-extract -> keyswitch.
+ * luts: n_lut LUTs of N values; lut_index (nullable, B entries) picks the LUT per ciphertext.
+ * Replaces ServerKey::keyswitch_programmable_bootstrap (ml/biometrics/notebooks/main.rs:71) and
+ * the compute behind POST /evaluate (e2e/test/fhe.test.ts:141-157).  Host buffers, synchronous. */
+int tfhe_hip_pbs(tfhe_ctx* ctx, const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
+                 const uint32_t* lut_index, uint64_t* lwe_out);
+/* Device buffers, enqueued on `stream` (hipStream_t; NULL = the ctx stream).  Inputs resident in HBM. */
+int tfhe_hip_pbs_async(tfhe_ctx* ctx, const uint64_t* d_lwe_in, size_t B, const uint64_t* d_luts, size_t n_lut,
+                       const uint32_t* d_lut_index, uint64_t* d_lwe_out, void* stream);
+
+/* Stage-level entry points (host buffers) used by the parity tests. */
+/* acc_out: B x (k+1) x N values in Z_p (coefficient domain) after the CMUX loop. */
+int tfhe_hip_blind_rotate(tfhe_ctx* ctx, const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
+                          const uint32_t* lut_index, uint64_t* acc_out);
+/* acc (Z_p, B x (k+1)N) -> LWE under the GLWE key, converted to 2^64: B x (kN + 1). */
+int tfhe_hip_sample_extract(tfhe_ctx* ctx, const uint64_t* acc, size_t B, uint64_t* lwe_big_out);
+/* B x (kN+1) -> B x (n+1). */
+int tfhe_hip_keyswitch(tfhe_ctx* ctx, const uint64_t* lwe_big, size_t B, uint64_t* lwe_small_out);
+/* Negacyclic NTT over Z_p of count polynomials of size N, in place, natural order:
+ * A[j] = a(psi^(2j+1)), psi the primitive 2N-th root with psi^(2N/64) = 8.  ntt_inv includes 1/N. */
+int tfhe_hip_ntt_fwd(tfhe_ctx* ctx, uint64_t* polys, size_t count);
+int tfhe_hip_ntt_inv(tfhe_ctx* ctx, uint64_t* polys, size_t count);
+
+/* Gate bootstrapping (FheBool NAND): out = PBS((0, 1/8) - c1 - c2, LUT == 1/8), B gates. */
+int tfhe_hip_nand(tfhe_ctx* ctx, const uint64_t* c1, const uint64_t* c2, size_t B, uint64_t* out);
+
+/* Wait for all work on the ctx stream. */
+int tfhe_hip_sync(tfhe_ctx* ctx);
+/* Per-kernel device timing (HIP events recorded on the launch stream around every blind-rotate /
+ * keyswitch launch).  reset clears the record; stats waits for the recorded events and returns the
+ * summed milliseconds and the launch count.  which: 0 = blind rotate (+sample extract), 1 = keyswitch.
+ * Used by bench.py for the roofline figure. */
+int tfhe_hip_timing_enable(tfhe_ctx* ctx, int enable);
+int tfhe_hip_timing_reset(tfhe_ctx* ctx);
+int tfhe_hip_timing_stats(tfhe_ctx* ctx, int which, double* total_ms, int* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

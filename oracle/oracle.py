@@ -1,0 +1,240 @@
+"""ctypes binding for the CPU oracle (liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg — never by the product (tfhe_amd/, js/).  See tfhe_oracle.h for the
+reference file:line each function restates and the "parity unpinned" statement.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+P = 0xFFFFFFFF00000001
+U64P = ctypes.POINTER(ctypes.c_uint64)
+U32P = ctypes.POINTER(ctypes.c_uint32)
+I64P = ctypes.POINTER(ctypes.c_int64)
+
+
+class Params(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint32), ("k", ctypes.c_uint32), ("N", ctypes.c_uint32),
+        ("pbs_base_log", ctypes.c_uint32), ("pbs_level", ctypes.c_uint32),
+        ("ks_base_log", ctypes.c_uint32), ("ks_level", ctypes.c_uint32),
+        ("lwe_noise_log2", ctypes.c_int32), ("glwe_noise_log2", ctypes.c_int32),
+        ("order", ctypes.c_uint32),
+    ]
+
+
+def build() -> str:
+    """Compile liboracle.so with the committed Makefile (gcc)."""
+    import subprocess
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return os.path.join(_HERE, "liboracle.so")
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        L.or_rng_u64.restype = ctypes.c_uint64
+        L.or_rng_mod_p.restype = ctypes.c_uint64
+        L.or_rng_gauss.restype = ctypes.c_int64
+        L.or_add.restype = ctypes.c_uint64
+        L.or_sub.restype = ctypes.c_uint64
+        L.or_mul.restype = ctypes.c_uint64
+        L.or_mul.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        L.or_pow.restype = ctypes.c_uint64
+        L.or_pow.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        L.or_psi.restype = ctypes.c_uint64
+        L.or_tor_to_p.restype = ctypes.c_uint64
+        L.or_tor_to_p.argtypes = [ctypes.c_uint64]
+        L.or_p_to_tor.restype = ctypes.c_uint64
+        L.or_p_to_tor.argtypes = [ctypes.c_uint64]
+        L.or_mod_switch.restype = ctypes.c_uint32
+        L.or_mod_switch.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
+        L.or_bsk_len.restype = ctypes.c_size_t
+        L.or_ksk_len.restype = ctypes.c_size_t
+        _LIB = L
+    return _LIB
+
+
+def _p(a: np.ndarray, t=U64P):
+    return a.ctypes.data_as(t)
+
+
+def params(preset: int = 0) -> Params:
+    p = Params()
+    assert lib().or_params_preset(preset, ctypes.byref(p)) == 0
+    return p
+
+
+class Rng:
+    def __init__(self, seed: int, stream: int):
+        self.buf = (ctypes.c_uint8 * 128)()
+        lib().or_rng_init(self.buf, ctypes.c_uint64(seed), ctypes.c_uint64(stream))
+
+    def u64(self) -> int:
+        return lib().or_rng_u64(self.buf)
+
+
+def ntt_fwd(a: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(a, dtype=np.uint64).copy()
+    for row in x.reshape(-1, x.shape[-1]):
+        lib().or_ntt_fwd(_p(row), ctypes.c_uint32(x.shape[-1]))
+    return x
+
+
+def ntt_inv(a: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(a, dtype=np.uint64).copy()
+    for row in x.reshape(-1, x.shape[-1]):
+        lib().or_ntt_inv(_p(row), ctypes.c_uint32(x.shape[-1]))
+    return x
+
+
+def poly_mul_schoolbook(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    b = np.ascontiguousarray(b, dtype=np.uint64)
+    out = np.zeros_like(a)
+    lib().or_poly_mul_schoolbook(_p(out), _p(a), _p(b), ctypes.c_uint32(a.shape[0]))
+    return out
+
+
+def poly_mul_ntt(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    b = np.ascontiguousarray(b, dtype=np.uint64)
+    out = np.zeros_like(a)
+    lib().or_poly_mul_ntt(_p(out), _p(a), _p(b), ctypes.c_uint32(a.shape[0]))
+    return out
+
+
+def decompose(x: int, base_log: int, level: int) -> list[int]:
+    d = np.zeros(64, dtype=np.int64)
+    lib().or_decompose(ctypes.c_uint64(x), ctypes.c_uint32(base_log), ctypes.c_uint32(level), _p(d, I64P))
+    return [int(v) for v in d[:level]]
+
+
+def psi(N: int) -> int:
+    return lib().or_psi(ctypes.c_uint32(N))
+
+
+class Keys:
+    """Oracle key material generated from a seed (same ChaCha20 streams as the product keygen)."""
+
+    def __init__(self, prm: Params, seed: int, with_bsk: bool = True, with_ksk: bool = True):
+        L = lib()
+        self.prm = prm
+        self.seed = seed
+        self.lwe_key = np.zeros(prm.n, dtype=np.uint64)
+        self.glwe_key = np.zeros(prm.k * prm.N, dtype=np.uint64)
+        self.bsk = np.zeros(L.or_bsk_len(ctypes.byref(prm)), dtype=np.uint64) if with_bsk else None
+        self.ksk = np.zeros(L.or_ksk_len(ctypes.byref(prm)), dtype=np.uint64) if with_ksk else None
+        L.or_keygen(ctypes.byref(prm), ctypes.c_uint64(seed), _p(self.lwe_key), _p(self.glwe_key),
+                    _p(self.bsk) if with_bsk else None, _p(self.ksk) if with_ksk else None)
+        self._bsk_ntt = None
+
+    @property
+    def bsk_ntt(self) -> np.ndarray:
+        if self._bsk_ntt is None:
+            self._bsk_ntt = np.zeros_like(self.bsk)
+            lib().or_bsk_to_ntt(ctypes.byref(self.prm), _p(self.bsk), _p(self._bsk_ntt))
+        return self._bsk_ntt
+
+    # --- encryption under the input-side key (small key for PBS_KS order, big for KS_PBS) ---
+    def in_key(self):
+        return (self.lwe_key, self.prm.n) if self.prm.order == 0 else (self.glwe_key, self.prm.k * self.prm.N)
+
+    def out_key(self):
+        return self.in_key()
+
+    def encrypt(self, msgs_torus, seed: int, stream0: int = 0) -> np.ndarray:
+        key, dim = self.in_key()
+        noise = self.prm.lwe_noise_log2 if self.prm.order == 0 else self.prm.glwe_noise_log2
+        m = np.ascontiguousarray(np.asarray(msgs_torus, dtype=np.uint64))
+        out = np.zeros((m.shape[0], dim + 1), dtype=np.uint64)
+        lib().or_lwe_encrypt(ctypes.c_uint32(dim), _p(key), ctypes.c_int32(noise), ctypes.c_uint64(seed),
+                             ctypes.c_uint64(stream0), _p(m), ctypes.c_size_t(m.shape[0]), _p(out))
+        return out
+
+    def phase(self, cts: np.ndarray, key=None, dim=None) -> np.ndarray:
+        if key is None:
+            key, dim = self.out_key()
+        cts = np.ascontiguousarray(cts, dtype=np.uint64).reshape(-1, dim + 1)
+        out = np.zeros(cts.shape[0], dtype=np.uint64)
+        lib().or_lwe_phase(ctypes.c_uint32(dim), _p(key), _p(cts), ctypes.c_size_t(cts.shape[0]), _p(out))
+        return out
+
+
+def blind_rotate(prm: Params, keys: Keys, lwe_in: np.ndarray, lut: np.ndarray, schoolbook=False) -> np.ndarray:
+    acc = np.zeros((prm.k + 1) * prm.N, dtype=np.uint64)
+    bsk = keys.bsk if schoolbook else keys.bsk_ntt
+    lib().or_blind_rotate(ctypes.byref(prm), _p(bsk), ctypes.c_int(1 if schoolbook else 0),
+                          _p(np.ascontiguousarray(lwe_in, dtype=np.uint64)),
+                          _p(np.ascontiguousarray(lut, dtype=np.uint64)), _p(acc))
+    return acc
+
+
+def sample_extract(prm: Params, acc: np.ndarray) -> np.ndarray:
+    out = np.zeros(prm.k * prm.N + 1, dtype=np.uint64)
+    lib().or_sample_extract(ctypes.byref(prm), _p(np.ascontiguousarray(acc, dtype=np.uint64)), _p(out))
+    return out
+
+
+def keyswitch(prm: Params, keys: Keys, lwe_big: np.ndarray) -> np.ndarray:
+    out = np.zeros(prm.n + 1, dtype=np.uint64)
+    lib().or_keyswitch(ctypes.byref(prm), _p(keys.ksk), _p(np.ascontiguousarray(lwe_big, dtype=np.uint64)), _p(out))
+    return out
+
+
+def pbs_batch(prm: Params, keys: Keys, lwe_in: np.ndarray, luts: np.ndarray, lut_index=None,
+              threads: int = 0) -> np.ndarray:
+    lwe_in = np.ascontiguousarray(lwe_in, dtype=np.uint64)
+    luts = np.ascontiguousarray(luts, dtype=np.uint64).reshape(-1, prm.N)
+    B = lwe_in.shape[0]
+    dout = (prm.n if prm.order == 0 else prm.k * prm.N) + 1
+    out = np.zeros((B, dout), dtype=np.uint64)
+    li = None
+    if lut_index is not None:
+        li = np.ascontiguousarray(lut_index, dtype=np.uint32)
+    lib().or_pbs_batch(ctypes.byref(prm), _p(keys.bsk_ntt), _p(keys.ksk), _p(lwe_in), ctypes.c_size_t(B),
+                       _p(luts), ctypes.c_size_t(luts.shape[0]), _p(li, U32P) if li is not None else None,
+                       _p(out), ctypes.c_int(threads))
+    return out
+
+
+def lut_constant(N: int, torus_value: int) -> np.ndarray:
+    out = np.zeros(N, dtype=np.uint64)
+    lib().or_lut_constant(ctypes.c_uint32(N), ctypes.c_uint64(torus_value), _p(out))
+    return out
+
+
+def lut_from_table(N: int, msg_modulus: int, table, delta_out: int) -> np.ndarray:
+    t = np.ascontiguousarray(np.asarray(table, dtype=np.uint64))
+    out = np.zeros(N, dtype=np.uint64)
+    lib().or_lut_from_table(ctypes.c_uint32(N), ctypes.c_uint32(msg_modulus), _p(t), ctypes.c_uint64(delta_out), _p(out))
+    return out
+
+
+def nand(prm: Params, keys: Keys, c1: np.ndarray, c2: np.ndarray) -> np.ndarray:
+    out = np.zeros(prm.n + 1, dtype=np.uint64)
+    lib().or_nand(ctypes.byref(prm), _p(keys.bsk_ntt), _p(keys.ksk), _p(np.ascontiguousarray(c1, dtype=np.uint64)),
+                  _p(np.ascontiguousarray(c2, dtype=np.uint64)), _p(out))
+    return out
+
+
+MU = 1 << 61  # gate encoding: true = +1/8, false = -1/8 (2^64 torus)
+
+
+def encode_bit(b: int) -> int:
+    return MU if b else (1 << 64) - MU
+
+
+def decode_bit(phase: int) -> int:
+    return 1 if phase < (1 << 63) else 0

@@ -1,0 +1,130 @@
+/*
+ * tfhe_oracle.h — CPU restatement of the TFHE programmable bootstrap (PBS) path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (libtfhe_hip.so, tfhe_amd/, js/) links,
+ * imports or executes this code.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may call it, and only as the checker / the timed CPU baseline.
+ *
+ * What it restates.  The reference (luxfi/tfhe monorepo) reaches its PBS through tfhe-rs
+ * (npm `tfhe`/`node-tfhe` 0.8.7, packages/pnpm-lock.yaml:1988-1995; Rust git revs in
+ * ml/extensions/rust/Cargo.toml:40), which is NOT vendored under /root/reference.  This file
+ * restates the published CGGI/tfhe-rs algorithm with the conventions visible in the
+ * reference's own call sites:
+ *   - Delta encoding with one padding bit ........ ml/extensions/rust/src/encryption.rs:5-22
+ *   - SignedDecomposer / closest_representable ... ml/extensions/rust/src/encryption.rs:152-166,191-201
+ *   - exact negacyclic wrapping product .......... ml/extensions/rust/src/computations.rs:50-54,101-105
+ *   - sample extraction .......................... ml/extensions/rust/src/computations.rs:109-132
+ *   - LUT + keyswitch_programmable_bootstrap ..... ml/biometrics/notebooks/main.rs:65-77
+ *   - P-FHEVM parameters ......................... sdk/relayer/src/tfhe.ts:14-19 (decoded in SURVEY App. A)
+ *
+ * PARITY STATUS: "parity unpinned" at the raw-ciphertext level.  No file in the reference holds
+ * raw PBS input/output vectors (e2e/test/fhe.test.ts only asserts byteLength>0), and tfhe-rs
+ * itself uses an f64 FFT that is not bit-reproducible.  Parity is pinned at the MESSAGE level:
+ * decrypt(PBS(f)) == f(m) for every message (biometrics main.rs:77 pattern), the NAND truth
+ * table, and the fhEVM operator KATs (tests/fhevm-suite/e2e/test/fhevmOperations*.ts).
+ * The GPU path must match THIS oracle bit-for-bit on identical integer inputs and keys.
+ *
+ * Arithmetic design (SURVEY.md §7 option A):
+ *   LWE / KSK : native torus Z_{2^64}
+ *   GLWE / BSK: Z_p with p = 2^64 - 2^32 + 1 (Goldilocks), NTT-friendly, exact
+ *   q_p -> 2^64 after sample extraction: y = x + ((x + 2^31) >> 32)
+ */
+#ifndef TFHE_ORACLE_H
+#define TFHE_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OR_P 0xFFFFFFFF00000001ull
+
+typedef struct or_params {
+  uint32_t n, k, N;
+  uint32_t pbs_base_log, pbs_level;
+  uint32_t ks_base_log, ks_level;
+  int32_t lwe_noise_log2;   /* stddev = 2^x of the torus */
+  int32_t glwe_noise_log2;
+  uint32_t order;           /* 0 = PBS then KS (small key ciphertexts), 1 = KS then PBS */
+} or_params;
+
+/* preset 0 = P-GATE (n=630,k=1,N=1024, 7x3, 2x8), preset 1 = P-FHEVM (918,1,2048, 23x1, 4x4). */
+int or_params_preset(int preset, or_params* out);
+
+/* ---- PRNG (ChaCha20, RFC 8439 block function) -------------------------------------- */
+typedef struct or_rng { uint32_t key[8]; uint32_t ctr; uint32_t buf[16]; int pos; } or_rng;
+void or_rng_init(or_rng* r, uint64_t seed, uint64_t stream);
+uint64_t or_rng_u64(or_rng* r);
+uint64_t or_rng_mod_p(or_rng* r);
+int64_t or_rng_gauss(or_rng* r, int32_t log2_sigma); /* round(N(0,1) * 2^(64+log2_sigma)) */
+
+/* ---- Z_p arithmetic ----------------------------------------------------------------- */
+uint64_t or_add(uint64_t a, uint64_t b);
+uint64_t or_sub(uint64_t a, uint64_t b);
+uint64_t or_mul(uint64_t a, uint64_t b);
+uint64_t or_pow(uint64_t a, uint64_t e);
+uint64_t or_psi(uint32_t N);      /* canonical primitive 2N-th root: psi^(2N/64) == 8 */
+uint64_t or_tor_to_p(uint64_t v); /* torus 2^64 -> Z_p embedding used for LUT values */
+uint64_t or_p_to_tor(uint64_t x); /* Z_p -> torus 2^64: x + ((x + 2^31) >> 32) */
+
+/* ---- polynomials in Z_p[X]/(X^N+1) --------------------------------------------------- */
+void or_poly_mul_schoolbook(uint64_t* out, const uint64_t* a, const uint64_t* b, uint32_t N);
+void or_ntt_fwd(uint64_t* a, uint32_t N); /* natural order: A[j] = a(psi^(2j+1)) */
+void or_ntt_inv(uint64_t* a, uint32_t N); /* exact inverse, includes 1/N */
+void or_poly_mul_ntt(uint64_t* out, const uint64_t* a, const uint64_t* b, uint32_t N);
+void or_poly_monomial_mul(uint64_t* out, const uint64_t* in, uint32_t N, uint32_t t); /* X^t * in */
+
+/* ---- decomposition -------------------------------------------------------------------- */
+/* tfhe-rs SignedDecomposer: closest_representable to base_log*level bits, balanced digits.
+ * digits[0] is the MOST significant level (gadget 2^(64-base_log)). */
+void or_decompose(uint64_t x, uint32_t base_log, uint32_t level, int64_t* digits);
+uint32_t or_mod_switch(uint64_t x, uint32_t two_n); /* round(x * 2N / 2^64) mod 2N */
+
+/* ---- sizes -------------------------------------------------------------------------- */
+size_t or_bsk_len(const or_params* p); /* n*(k+1)l*(k+1)*N u64, layout [i][c*l+lvl][j][coef] */
+size_t or_ksk_len(const or_params* p); /* kN*l_ks*(n+1) u64, layout [j][r][0..n] (b last) */
+
+/* ---- keys & encryption --------------------------------------------------------------- */
+void or_keygen(const or_params* p, uint64_t seed, uint64_t* lwe_key /*n*/, uint64_t* glwe_key /*kN*/,
+               uint64_t* bsk /*nullable*/, uint64_t* ksk /*nullable*/);
+/* ct q of the batch uses ChaCha stream (stream0 + q). dim = LWE dimension of key. */
+void or_lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, uint64_t seed,
+                    uint64_t stream0, const uint64_t* msgs, size_t count, uint64_t* out);
+void or_lwe_phase(uint32_t dim, const uint64_t* key, const uint64_t* ct, size_t count, uint64_t* out);
+
+/* ---- bootstrap pieces ----------------------------------------------------------------- */
+/* NTT-domain copy of the BSK (natural order, pre-scaled by nothing) for the fast oracle path */
+void or_bsk_to_ntt(const or_params* p, const uint64_t* bsk, uint64_t* bsk_ntt);
+/* acc_out: (k+1)*N u64 in Z_p.  lwe_in: dim n+1.  lut: N values in Z_p. bsk_ntt from above.
+ * use_schoolbook != 0 uses the O(N^2) product against the standard-domain bsk instead. */
+void or_blind_rotate(const or_params* p, const uint64_t* bsk_any, int use_schoolbook,
+                     const uint64_t* lwe_in, const uint64_t* lut, uint64_t* acc_out);
+void or_sample_extract(const or_params* p, const uint64_t* acc, uint64_t* lwe_big_out /*kN+1*/);
+void or_keyswitch(const or_params* p, const uint64_t* ksk, const uint64_t* lwe_big /*kN+1*/,
+                  uint64_t* lwe_small_out /*n+1*/);
+/* Full PBS of one ciphertext (order from params). */
+void or_pbs(const or_params* p, const uint64_t* bsk_ntt, const uint64_t* ksk, const uint64_t* lwe_in,
+            const uint64_t* lut, uint64_t* lwe_out);
+/* Batch PBS over B ciphertexts with OpenMP (threads<=0: all cores). lut_index nullable. */
+void or_pbs_batch(const or_params* p, const uint64_t* bsk_ntt, const uint64_t* ksk, const uint64_t* lwe_in,
+                  size_t B, const uint64_t* luts, size_t n_lut, const uint32_t* lut_index,
+                  uint64_t* lwe_out, int threads);
+
+/* ---- LUT helpers --------------------------------------------------------------------- */
+void or_lut_constant(uint32_t N, uint64_t torus_value, uint64_t* lut); /* gate LUT: every coef = v */
+/* tfhe-rs generate_accumulator: box = N/msg_modulus, v[i] = f(i/box)*delta_out, half-box rotation.
+ * f_table has msg_modulus entries. */
+void or_lut_from_table(uint32_t N, uint32_t msg_modulus, const uint64_t* f_table, uint64_t delta_out,
+                       uint64_t* lut);
+
+/* ---- gate bootstrap (P-GATE) --------------------------------------------------------- */
+/* NAND: c = (0, 1/8) - c1 - c2 then PBS with LUT == 1/8.  Bits are +-1/8 (true = +1/8). */
+void or_nand(const or_params* p, const uint64_t* bsk_ntt, const uint64_t* ksk, const uint64_t* c1,
+             const uint64_t* c2, uint64_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,92 @@
+"""Host-side checks of the product library without a GPU: the C-ABI .so loads and exports every
+symbol include/tfhe_hip.h declares; client-side key material (keygen / encrypt / LUT builders in
+libtfhe_hip.so) is bit-identical to the oracle; device entry points fail cleanly (no abort)."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import KEY_SEED, ROOT
+
+import tfhe_amd
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "tfhe_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(tfhe_hip_\w+)\s*\(", src)))
+
+
+def test_abi_exports_every_declared_symbol():
+    L = tfhe_amd.lib()
+    declared = header_functions()
+    assert len(declared) >= 25
+    for name in declared:
+        assert hasattr(L, name), f"libtfhe_hip.so does not export {name}"
+    assert sorted(tfhe_amd.ABI_SYMBOLS) == declared
+
+
+def test_presets():
+    g = tfhe_amd.Params.preset(tfhe_amd.PRESET_GATE)
+    assert (g.n, g.k, g.N, g.pbs_base_log, g.pbs_level, g.ks_base_log, g.ks_level, g.order) == (630, 1, 1024, 7, 3, 2, 8, 0)
+    f = tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM)
+    assert (f.n, f.k, f.N, f.pbs_base_log, f.pbs_level, f.ks_base_log, f.ks_level, f.order) == (918, 1, 2048, 23, 1, 4, 4, 1)
+    L = tfhe_amd.lib()
+    import ctypes
+    assert L.tfhe_hip_bsk_len(ctypes.byref(g)) == 630 * 6 * 2 * 1024
+    assert L.tfhe_hip_ksk_len(ctypes.byref(g)) == 1024 * 8 * 631
+    with pytest.raises(tfhe_amd.TfheError):
+        tfhe_amd.Params.preset(7)
+
+
+def test_keygen_matches_oracle(product_keys, oracle_keys):
+    ck, sk = product_keys
+    assert np.array_equal(ck.lwe_key, oracle_keys.lwe_key)
+    assert np.array_equal(ck.glwe_key, oracle_keys.glwe_key)
+    assert np.array_equal(sk.bsk, oracle_keys.bsk)
+    assert np.array_equal(sk.ksk, oracle_keys.ksk)
+    assert int(sk.bsk.max()) < 0xFFFFFFFF00000001  # canonical Z_p
+
+
+def test_encrypt_phase_matches_oracle(product_keys, oracle_keys):
+    ck, _ = product_keys
+    msgs = np.array([1 << 61, (1 << 64) - (1 << 61), 0, 12345], dtype=np.uint64)
+    a = ck.encrypt_torus(msgs, seed=0xC0FFEE02, stream0=5)
+    b = oracle_keys.encrypt(msgs, seed=0xC0FFEE02, stream0=5)
+    assert np.array_equal(a, b)
+    assert np.array_equal(ck.phase(a), oracle_keys.phase(b))
+    err = (ck.phase(a) - msgs).astype(np.int64)
+    assert np.abs(err).max() < 2**56
+
+
+def test_lut_builders_match_oracle(oracle_mod):
+    O = oracle_mod
+    assert np.array_equal(tfhe_amd.lut_constant(1024, 1 << 61), O.lut_constant(1024, 1 << 61))
+    for mm in (2, 4, 8, 16):
+        tab = [(3 * m + 1) % mm for m in range(mm)]
+        assert np.array_equal(tfhe_amd.lut_from_table(1024, mm, tab, (1 << 63) // mm),
+                              O.lut_from_table(1024, mm, tab, (1 << 63) // mm))
+
+
+def test_bad_arguments_fail_cleanly():
+    with pytest.raises(tfhe_amd.TfheError) as e:
+        tfhe_amd.lut_from_table(1024, 3, [0, 1, 2], 1)
+    assert e.value.code == -1
+
+
+def test_engine_without_gpu_raises_not_aborts():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present: covered by the gpu tests")
+    except ImportError:
+        pass
+    with pytest.raises(tfhe_amd.TfheError):
+        tfhe_amd.Engine(tfhe_amd.Params.preset(tfhe_amd.PRESET_GATE), 0)
+
+
+def test_fhevm_params_unsupported_on_device_build():
+    # P-FHEVM (N=2048, KS->PBS) is a "next" row: the device path must refuse it loudly, not compute wrong.
+    with pytest.raises(tfhe_amd.TfheError):
+        tfhe_amd.Engine(tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM), 0)

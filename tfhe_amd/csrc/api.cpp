@@ -1,0 +1,518 @@
+// api.cpp — the C ABI of libtfhe_hip.so (include/tfhe_hip.h): device context, key residency,
+// launch sequencing, error reporting.  Host code; kernels live in pbs_kernels.hip.
+#include <hip/hip_runtime_api.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/tfhe_hip.h"
+#include "client.h"
+#include "gl64.h"
+#include "ntt32.h"
+#include "pbs_kernels.h"
+
+using tfhe::u64;
+using tfhe::u32;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess)                                                                      \
+      return fail(_e == hipErrorOutOfMemory ? TFHE_HIP_ENOMEM : TFHE_HIP_EDEVICE, "%s: %s (%s:%d)", #expr, \
+                  hipGetErrorString(_e), __FILE__, __LINE__);                                  \
+  } while (0)
+
+bool params_valid(const tfhe_params* p) {
+  return p && p->n > 0 && p->k > 0 && p->N >= 32 && (p->N & (p->N - 1)) == 0 && p->pbs_level > 0 &&
+         p->pbs_base_log > 0 && p->pbs_base_log * p->pbs_level < 64 && p->ks_level > 0 && p->ks_base_log > 0 &&
+         p->ks_base_log * p->ks_level < 64;
+}
+
+// The device kernels of this build: P-GATE shape (k=1, N=1024, PBS 7x3, KS 2x8, PBS then KS).
+bool params_on_device(const tfhe_params* p) {
+  return p->k == 1 && p->N == 1024 && p->pbs_base_log == 7 && p->pbs_level == 3 && p->ks_base_log == 2 &&
+         p->ks_level == 8 && p->order == 0;
+}
+
+// canonical psi: primitive 2N-th root of unity with psi^(2N/64) = 8 (generator 7)
+u64 canonical_psi(uint32_t N) {
+  using namespace tfhe;
+  const u64 w = gl_pow(7, (GL_P - 1) / (2ull * N));
+  const u64 r = gl_pow(w, 2ull * N / 64);
+  u64 k = 0, t = 1;
+  for (k = 0; k < 64; k++) {
+    if (t == r) break;
+    t = gl_mul(t, 8);
+  }
+  u64 m = 1;
+  while ((k * m) % 64 != 1) m += 2;
+  return gl_pow(w, m);
+}
+
+}  // namespace
+
+struct tfhe_ctx {
+  tfhe_params p{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  u64* d_bsk = nullptr;  // NTT layout, x N^-1
+  u64* d_ksk = nullptr;
+  u64* d_twf = nullptr;  // 1024 forward twiddles (R16 layout)
+  u64* d_twi = nullptr;
+  u64 ninv = 0;
+  bool keys = false;
+  // workspaces
+  u64* d_big = nullptr;
+  size_t big_cap = 0;  // u64 elements
+  void* d_stage = nullptr;
+  size_t stage_cap = 0;  // bytes
+  std::mutex mu;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev[2];  // start/stop pairs, flattened
+  std::vector<hipEvent_t> ev_pool;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int grow(void** ptr, size_t* cap, size_t bytes) {
+  if (*cap >= bytes) return 0;
+  if (*ptr) (void)hipFree(*ptr);
+  *ptr = nullptr;
+  *cap = 0;
+  HIP_TRY(hipMalloc(ptr, bytes));
+  *cap = bytes;
+  return 0;
+}
+
+hipEvent_t take_event(tfhe_ctx* c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+void timed_begin(tfhe_ctx* c, int which, hipStream_t s) {
+  if (!c->timing) return;
+  hipEvent_t e = take_event(c);
+  if (e) {
+    (void)hipEventRecord(e, s);
+    c->ev[which].push_back(e);
+  }
+}
+void timed_end(tfhe_ctx* c, int which, hipStream_t s) {
+  if (!c->timing) return;
+  if (c->ev[which].size() % 2 == 0) return;  // begin failed
+  hipEvent_t e = take_event(c);
+  if (e) {
+    (void)hipEventRecord(e, s);
+    c->ev[which].push_back(e);
+  } else {
+    c->ev_pool.push_back(c->ev[which].back());
+    c->ev[which].pop_back();
+  }
+}
+
+uint32_t io_dim(const tfhe_params& p) { return p.order == 0 ? p.n : p.k * p.N; }
+
+// PBS on device buffers (caller holds c->mu, device set).
+int pbs_device(tfhe_ctx* c, const u64* d_in, size_t B, const u64* d_luts, size_t n_lut, const u32* d_idx, u64* d_out,
+               hipStream_t s) {
+  const size_t big = (size_t)c->p.k * c->p.N + 1;
+  int rc = grow((void**)&c->d_big, &c->big_cap, B * big * sizeof(u64));
+  if (rc) return rc;
+  timed_begin(c, 0, s);
+  HIP_TRY(tfhe::launch_blind_rotate(d_in, B, (int)c->p.n, d_luts, d_idx, (int)n_lut, c->d_bsk, c->d_twf, c->d_twi,
+                                    c->d_big, nullptr, s));
+  timed_end(c, 0, s);
+  timed_begin(c, 1, s);
+  HIP_TRY(tfhe::launch_keyswitch(c->d_big, B, (int)(c->p.k * c->p.N), c->d_ksk, (int)c->p.n, d_out, s));
+  timed_end(c, 1, s);
+  return 0;
+}
+
+// Stage host buffers into one device allocation. Returns device pointers in order.
+int stage(tfhe_ctx* c, std::initializer_list<std::pair<const void*, size_t>> in, std::vector<void*>& dptr,
+          size_t extra_out_bytes) {
+  size_t total = 0;
+  std::vector<size_t> off;
+  for (auto& x : in) {
+    off.push_back(total);
+    total += (x.second + 255) & ~(size_t)255;
+  }
+  const size_t out_off = total;
+  total += (extra_out_bytes + 255) & ~(size_t)255;
+  int rc = grow(&c->d_stage, &c->stage_cap, total ? total : 256);
+  if (rc) return rc;
+  size_t i = 0;
+  dptr.clear();
+  for (auto& x : in) {
+    void* d = (char*)c->d_stage + off[i++];
+    if (x.first && x.second) HIP_TRY(hipMemcpyAsync(d, x.first, x.second, hipMemcpyHostToDevice, c->stream));
+    dptr.push_back(x.first ? d : nullptr);
+  }
+  dptr.push_back((char*)c->d_stage + out_off);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* tfhe_hip_last_error(void) { return g_err.c_str(); }
+
+int tfhe_hip_params_preset(int preset, tfhe_params* o) {
+  if (!o) return fail(TFHE_HIP_EINVAL, "null params");
+  memset(o, 0, sizeof(*o));
+  if (preset == TFHE_HIP_PRESET_GATE) {
+    *o = tfhe_params{630, 1, 1024, 7, 3, 2, 8, -15, -25, 0};
+    return 0;
+  }
+  if (preset == TFHE_HIP_PRESET_FHEVM) {
+    *o = tfhe_params{918, 1, 2048, 23, 1, 4, 4, -19, -47, 1};
+    return 0;
+  }
+  return fail(TFHE_HIP_EINVAL, "unknown preset %d", preset);
+}
+
+size_t tfhe_hip_bsk_len(const tfhe_params* p) { return p ? tfhe::client::bsk_len(*p) : 0; }
+size_t tfhe_hip_ksk_len(const tfhe_params* p) { return p ? tfhe::client::ksk_len(*p) : 0; }
+uint32_t tfhe_hip_io_dim(const tfhe_params* p) { return p ? io_dim(*p) : 0; }
+
+int tfhe_hip_keygen(const tfhe_params* p, uint64_t seed, uint64_t* lwe_key, uint64_t* glwe_key, uint64_t* bsk,
+                    uint64_t* ksk) {
+  if (!params_valid(p) || !lwe_key || !glwe_key) return fail(TFHE_HIP_EINVAL, "keygen: bad arguments");
+  tfhe::client::keygen(*p, seed, lwe_key, glwe_key, bsk, ksk);
+  return 0;
+}
+
+int tfhe_hip_lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, uint64_t seed, uint64_t stream0,
+                         const uint64_t* msgs, size_t count, uint64_t* out) {
+  if (!dim || !key || (count && (!msgs || !out))) return fail(TFHE_HIP_EINVAL, "lwe_encrypt: bad arguments");
+  if (noise_log2 >= 0 || noise_log2 < -63) return fail(TFHE_HIP_EINVAL, "lwe_encrypt: noise_log2 out of range");
+  tfhe::client::lwe_encrypt(dim, key, noise_log2, seed, stream0, msgs, count, out);
+  return 0;
+}
+
+int tfhe_hip_lwe_phase(uint32_t dim, const uint64_t* key, const uint64_t* ct, size_t count, uint64_t* out) {
+  if (!dim || !key || (count && (!ct || !out))) return fail(TFHE_HIP_EINVAL, "lwe_phase: bad arguments");
+  tfhe::client::lwe_phase(dim, key, ct, count, out);
+  return 0;
+}
+
+int tfhe_hip_lut_constant(uint32_t N, uint64_t v, uint64_t* lut) {
+  if (!N || !lut) return fail(TFHE_HIP_EINVAL, "lut_constant: bad arguments");
+  tfhe::client::lut_constant(N, v, lut);
+  return 0;
+}
+
+int tfhe_hip_lut_from_table(uint32_t N, uint32_t msg_modulus, const uint64_t* table, uint64_t delta_out,
+                            uint64_t* lut) {
+  if (!N || !msg_modulus || msg_modulus > N || (N % msg_modulus) || !table || !lut)
+    return fail(TFHE_HIP_EINVAL, "lut_from_table: bad arguments (N=%u, msg_modulus=%u)", N, msg_modulus);
+  tfhe::client::lut_from_table(N, msg_modulus, table, delta_out, lut);
+  return 0;
+}
+
+int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out) {
+  if (!out) return fail(TFHE_HIP_EINVAL, "create: null out");
+  *out = nullptr;
+  if (!params_valid(p)) return fail(TFHE_HIP_EINVAL, "create: invalid parameters");
+  if (!params_on_device(p))
+    return fail(TFHE_HIP_EUNSUPPORTED,
+                "create: device kernels of this build cover k=1, N=1024, PBS 7x3, KS 2x8, PBS->KS (P-GATE); got "
+                "k=%u N=%u pbs %ux%u ks %ux%u order %u",
+                p->k, p->N, p->pbs_base_log, p->pbs_level, p->ks_base_log, p->ks_level, p->order);
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(TFHE_HIP_EINVAL, "create: device %d of %d", device, ndev);
+  DeviceGuard g(device);
+  tfhe_ctx* c = new tfhe_ctx();
+  c->p = *p;
+  c->device = device;
+  auto cleanup = [&](int rc) {
+    tfhe_hip_destroy(c);
+    return rc;
+  };
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail(TFHE_HIP_EDEVICE, "create: hipStreamCreate failed"));
+  // twiddles, R16 layout: element (lane L, e) <-> m = 2e + (L >> 5), i2 = L & 31
+  using namespace tfhe;
+  const uint32_t N = p->N;
+  const u64 psi = canonical_psi(N), psi_inv = gl_pow(psi, GL_P - 2);
+  std::vector<u64> twf(N), twi(N);
+  for (int L = 0; L < 64; L++)
+    for (int e = 0; e < 16; e++) {
+      const int m = 2 * e + (L >> 5), i2 = L & 31;
+      const u64 ex = (u64)i2 * (2 * brv5(m) + 1);
+      twf[64 * e + L] = gl_pow(psi, ex);
+      twi[64 * e + L] = gl_pow(psi_inv, ex);
+    }
+  c->ninv = gl_pow(N, GL_P - 2);
+  if (hipMalloc(&c->d_twf, N * 8) != hipSuccess || hipMalloc(&c->d_twi, N * 8) != hipSuccess)
+    return cleanup(fail(TFHE_HIP_ENOMEM, "create: twiddle allocation failed"));
+  if (hipMemcpy(c->d_twf, twf.data(), N * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_twi, twi.data(), N * 8, hipMemcpyHostToDevice) != hipSuccess)
+    return cleanup(fail(TFHE_HIP_EDEVICE, "create: twiddle upload failed"));
+  *out = c;
+  return 0;
+}
+
+void tfhe_hip_destroy(tfhe_ctx* c) {
+  if (!c) return;
+  {
+    DeviceGuard g(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (int w = 0; w < 2; w++)
+      for (auto e : c->ev[w]) (void)hipEventDestroy(e);
+    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    (void)hipFree(c->d_bsk);
+    (void)hipFree(c->d_ksk);
+    (void)hipFree(c->d_twf);
+    (void)hipFree(c->d_twi);
+    (void)hipFree(c->d_big);
+    (void)hipFree(c->d_stage);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+  }
+  delete c;
+}
+
+int tfhe_hip_device(const tfhe_ctx* c) { return c ? c->device : -1; }
+
+static int load_keys_impl(tfhe_ctx* c, const uint64_t* bsk, size_t bsk_len, const uint64_t* ksk, size_t ksk_len,
+                          hipMemcpyKind kind) {
+  if (!c || !bsk || !ksk) return fail(TFHE_HIP_EINVAL, "load_keys: null argument");
+  if (bsk_len != tfhe::client::bsk_len(c->p) || ksk_len != tfhe::client::ksk_len(c->p))
+    return fail(TFHE_HIP_EINVAL, "load_keys: sizes %zu/%zu, expected %zu/%zu", bsk_len, ksk_len,
+                tfhe::client::bsk_len(c->p), tfhe::client::ksk_len(c->p));
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  c->keys = false;
+  if (!c->d_bsk) HIP_TRY(hipMalloc(&c->d_bsk, bsk_len * 8));
+  if (!c->d_ksk) HIP_TRY(hipMalloc(&c->d_ksk, ksk_len * 8));
+  HIP_TRY(hipMemcpyAsync(c->d_ksk, ksk, ksk_len * 8, kind, c->stream));
+  // standard-domain BSK staged in the workspace, converted in one launch
+  void* tmp = nullptr;
+  if (kind == hipMemcpyHostToDevice) {
+    int rc = grow(&c->d_stage, &c->stage_cap, bsk_len * 8);
+    if (rc) return rc;
+    tmp = c->d_stage;
+    HIP_TRY(hipMemcpyAsync(tmp, bsk, bsk_len * 8, kind, c->stream));
+  } else {
+    tmp = (void*)bsk;
+  }
+  const size_t polys = bsk_len / c->p.N;
+  HIP_TRY(tfhe::launch_bsk_to_ntt((const u64*)tmp, c->d_bsk, (int)(polys / 12), c->d_twf, c->ninv, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->keys = true;
+  return 0;
+}
+
+int tfhe_hip_load_keys(tfhe_ctx* c, const uint64_t* bsk, size_t bsk_len, const uint64_t* ksk, size_t ksk_len) {
+  return load_keys_impl(c, bsk, bsk_len, ksk, ksk_len, hipMemcpyHostToDevice);
+}
+
+int tfhe_hip_load_keys_device(tfhe_ctx* c, const uint64_t* d_bsk, size_t bsk_len, const uint64_t* d_ksk,
+                              size_t ksk_len) {
+  return load_keys_impl(c, d_bsk, bsk_len, d_ksk, ksk_len, hipMemcpyDeviceToDevice);
+}
+
+int tfhe_hip_pbs_async(tfhe_ctx* c, const uint64_t* d_in, size_t B, const uint64_t* d_luts, size_t n_lut,
+                       const uint32_t* d_idx, uint64_t* d_out, void* stream) {
+  if (!c) return fail(TFHE_HIP_EINVAL, "pbs: null ctx");
+  if (!c->keys) return fail(TFHE_HIP_ENOKEYS, "pbs: keys not loaded");
+  if (B == 0) return 0;
+  if (!d_in || !d_luts || !n_lut || !d_out) return fail(TFHE_HIP_EINVAL, "pbs: null buffer or n_lut == 0");
+  if (B > 0x7FFFFFFF) return fail(TFHE_HIP_EINVAL, "pbs: batch too large");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  return pbs_device(c, d_in, B, d_luts, n_lut, d_idx, d_out, stream ? (hipStream_t)stream : c->stream);
+}
+
+int tfhe_hip_pbs(tfhe_ctx* c, const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
+                 const uint32_t* lut_index, uint64_t* lwe_out) {
+  if (!c) return fail(TFHE_HIP_EINVAL, "pbs: null ctx");
+  if (!c->keys) return fail(TFHE_HIP_ENOKEYS, "pbs: keys not loaded");
+  if (B == 0) return 0;
+  if (!lwe_in || !luts || !n_lut || !lwe_out) return fail(TFHE_HIP_EINVAL, "pbs: null buffer or n_lut == 0");
+  if (lut_index)
+    for (size_t q = 0; q < B; q++)
+      if (lut_index[q] >= n_lut) return fail(TFHE_HIP_EINVAL, "pbs: lut_index[%zu] = %u >= n_lut %zu", q, lut_index[q], n_lut);
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  const size_t dim = io_dim(c->p) + 1;
+  std::vector<void*> d;
+  int rc = stage(c, {{lwe_in, B * dim * 8}, {luts, n_lut * c->p.N * 8}, {lut_index, lut_index ? B * 4 : 0}}, d,
+                 B * dim * 8);
+  if (rc) return rc;
+  rc = pbs_device(c, (const u64*)d[0], B, (const u64*)d[1], n_lut, (const u32*)d[2], (u64*)d[3], c->stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(lwe_out, d[3], B * dim * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int tfhe_hip_blind_rotate(tfhe_ctx* c, const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
+                          const uint32_t* lut_index, uint64_t* acc_out) {
+  if (!c) return fail(TFHE_HIP_EINVAL, "blind_rotate: null ctx");
+  if (!c->keys) return fail(TFHE_HIP_ENOKEYS, "blind_rotate: keys not loaded");
+  if (B == 0) return 0;
+  if (!lwe_in || !luts || !n_lut || !acc_out) return fail(TFHE_HIP_EINVAL, "blind_rotate: null buffer");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  const size_t din = (size_t)c->p.n + 1, acc_len = (size_t)(c->p.k + 1) * c->p.N;
+  std::vector<void*> d;
+  int rc = stage(c, {{lwe_in, B * din * 8}, {luts, n_lut * c->p.N * 8}, {lut_index, lut_index ? B * 4 : 0}}, d,
+                 B * acc_len * 8);
+  if (rc) return rc;
+  HIP_TRY(tfhe::launch_blind_rotate((const u64*)d[0], B, (int)c->p.n, (const u64*)d[1], (const u32*)d[2], (int)n_lut,
+                                    c->d_bsk, c->d_twf, c->d_twi, nullptr, (u64*)d[3], c->stream));
+  HIP_TRY(hipMemcpyAsync(acc_out, d[3], B * acc_len * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int tfhe_hip_sample_extract(tfhe_ctx* c, const uint64_t* acc, size_t B, uint64_t* out) {
+  if (!c || (B && (!acc || !out))) return fail(TFHE_HIP_EINVAL, "sample_extract: bad arguments");
+  if (B == 0) return 0;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  const size_t acc_len = (size_t)(c->p.k + 1) * c->p.N, big = (size_t)c->p.k * c->p.N + 1;
+  std::vector<void*> d;
+  int rc = stage(c, {{acc, B * acc_len * 8}}, d, B * big * 8);
+  if (rc) return rc;
+  HIP_TRY(tfhe::launch_sample_extract((const u64*)d[0], B, (u64*)d[1], c->stream));
+  HIP_TRY(hipMemcpyAsync(out, d[1], B * big * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int tfhe_hip_keyswitch(tfhe_ctx* c, const uint64_t* in, size_t B, uint64_t* out) {
+  if (!c || (B && (!in || !out))) return fail(TFHE_HIP_EINVAL, "keyswitch: bad arguments");
+  if (!c->keys) return fail(TFHE_HIP_ENOKEYS, "keyswitch: keys not loaded");
+  if (B == 0) return 0;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  const size_t big = (size_t)c->p.k * c->p.N + 1, small = (size_t)c->p.n + 1;
+  std::vector<void*> d;
+  int rc = stage(c, {{in, B * big * 8}}, d, B * small * 8);
+  if (rc) return rc;
+  HIP_TRY(tfhe::launch_keyswitch((const u64*)d[0], B, (int)(c->p.k * c->p.N), c->d_ksk, (int)c->p.n, (u64*)d[1],
+                                 c->stream));
+  HIP_TRY(hipMemcpyAsync(out, d[1], B * small * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+static int ntt_impl(tfhe_ctx* c, uint64_t* polys, size_t count, bool inverse) {
+  if (!c || (count && !polys)) return fail(TFHE_HIP_EINVAL, "ntt: bad arguments");
+  if (count == 0) return 0;
+  for (size_t i = 0; i < count * c->p.N; i++)
+    if (polys[i] >= tfhe::GL_P) return fail(TFHE_HIP_EINVAL, "ntt: value at %zu not reduced mod p", i);
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  const size_t bytes = count * c->p.N * 8;
+  std::vector<void*> d;
+  int rc = stage(c, {{polys, bytes}}, d, 0);
+  if (rc) return rc;
+  if (inverse) HIP_TRY(tfhe::launch_ntt_inv((u64*)d[0], count, c->d_twi, c->ninv, c->stream));
+  else HIP_TRY(tfhe::launch_ntt_fwd((u64*)d[0], count, c->d_twf, c->stream));
+  HIP_TRY(hipMemcpyAsync(polys, d[0], bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int tfhe_hip_ntt_fwd(tfhe_ctx* c, uint64_t* polys, size_t count) { return ntt_impl(c, polys, count, false); }
+int tfhe_hip_ntt_inv(tfhe_ctx* c, uint64_t* polys, size_t count) { return ntt_impl(c, polys, count, true); }
+
+int tfhe_hip_nand(tfhe_ctx* c, const uint64_t* c1, const uint64_t* c2, size_t B, uint64_t* out) {
+  if (!c || (B && (!c1 || !c2 || !out))) return fail(TFHE_HIP_EINVAL, "nand: bad arguments");
+  if (B == 0) return 0;
+  const size_t dim = (size_t)c->p.n + 1;
+  std::vector<u64> in(B * dim), lut(c->p.N);
+  const u64 mu = 1ull << 61;  // 1/8
+  for (size_t q = 0; q < B; q++) {
+    for (size_t i = 0; i + 1 < dim; i++) in[q * dim + i] = 0 - c1[q * dim + i] - c2[q * dim + i];
+    in[q * dim + dim - 1] = mu - c1[q * dim + dim - 1] - c2[q * dim + dim - 1];
+  }
+  tfhe::client::lut_constant(c->p.N, mu, lut.data());
+  return tfhe_hip_pbs(c, in.data(), B, lut.data(), 1, nullptr, out);
+}
+
+int tfhe_hip_sync(tfhe_ctx* c) {
+  if (!c) return fail(TFHE_HIP_EINVAL, "sync: null ctx");
+  DeviceGuard g(c->device);
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int tfhe_hip_timing_enable(tfhe_ctx* c, int enable) {
+  if (!c) return fail(TFHE_HIP_EINVAL, "timing: null ctx");
+  c->timing = enable != 0;
+  return 0;
+}
+
+int tfhe_hip_timing_reset(tfhe_ctx* c) {
+  if (!c) return fail(TFHE_HIP_EINVAL, "timing: null ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  for (int w = 0; w < 2; w++) {
+    for (auto e : c->ev[w]) c->ev_pool.push_back(e);
+    c->ev[w].clear();
+  }
+  return 0;
+}
+
+int tfhe_hip_timing_stats(tfhe_ctx* c, int which, double* total_ms, int* launches) {
+  if (!c || which < 0 || which > 1 || !total_ms || !launches) return fail(TFHE_HIP_EINVAL, "timing: bad arguments");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  double tot = 0;
+  int cnt = 0;
+  auto& v = c->ev[which];
+  for (size_t i = 0; i + 1 < v.size(); i += 2) {
+    HIP_TRY(hipEventSynchronize(v[i + 1]));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, v[i], v[i + 1]));
+    tot += ms;
+    cnt++;
+  }
+  *total_ms = tot;
+  *launches = cnt;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,246 @@
+// client.cpp — client-side key material for libtfhe_hip.so (host C++, std::thread).
+//
+// Replaces the key-generation / encryption role the reference delegates to tfhe-rs WASM
+// (sdk/relayer/src/tfhe.ts:20-28, generateKeys.js:20-31) and the server /encrypt + /decrypt
+// endpoints (packages/luxfhejs/src/index.ts:127-141, packages/hardhat-plugin/src/index.ts:71-75),
+// for the deterministic seeded key sets this engine consumes.  Compiled with -ffp-contract=off:
+// the Gaussian sampler uses only IEEE + - * / sqrt, so keys are bit-identical on every host.
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+#include "../../include/tfhe_hip.h"
+#include "client.h"
+
+namespace tfhe {
+namespace client {
+
+static constexpr uint64_t P = 0xFFFFFFFF00000001ull;
+
+// Static-partition parallel for over [0, count) on hardware threads (std::thread, no OpenMP runtime).
+template <class F>
+static void parallel_for(int64_t count, F&& f) {
+  unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const int64_t nt = std::min<int64_t>(std::min<int64_t>(hw, 32), count);
+  if (nt <= 1) {
+    for (int64_t i = 0; i < count; i++) f(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int64_t t = 0; t < nt; t++)
+    th.emplace_back([&, t] {
+      for (int64_t i = t; i < count; i += nt) f(i);
+    });
+  for (auto& x : th) x.join();
+}
+
+// ---------------------------------------------------------------- ChaCha20 (RFC 8439) stream
+struct ChaCha {
+  uint32_t key[8];
+  uint32_t ctr = 0;
+  uint32_t buf[16];
+  int pos = 16;
+
+  ChaCha(uint64_t seed, uint64_t stream) {
+    static const uint8_t tag[16] = {'t', 'f', 'h', 'e', '-', 'a', 'm', 'd', ' ', 'c', 'h', 'a', 'c', 'h', 'a', '!'};
+    key[0] = (uint32_t)seed;
+    key[1] = (uint32_t)(seed >> 32);
+    key[2] = (uint32_t)stream;
+    key[3] = (uint32_t)(stream >> 32);
+    for (int i = 0; i < 4; i++) memcpy(&key[4 + i], tag + 4 * i, 4);
+  }
+  static inline uint32_t rl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+  void refill() {
+    uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1], key[2], key[3],
+                      key[4],      key[5],      key[6],      key[7],      ctr++,  0,      0,      0};
+    uint32_t x[16];
+    memcpy(x, s, sizeof(x));
+    auto qr = [&](int a, int b, int c, int d) {
+      x[a] += x[b]; x[d] = rl(x[d] ^ x[a], 16);
+      x[c] += x[d]; x[b] = rl(x[b] ^ x[c], 12);
+      x[a] += x[b]; x[d] = rl(x[d] ^ x[a], 8);
+      x[c] += x[d]; x[b] = rl(x[b] ^ x[c], 7);
+    };
+    for (int r = 0; r < 10; r++) {
+      qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15);
+      qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14);
+    }
+    for (int i = 0; i < 16; i++) buf[i] = x[i] + s[i];
+    pos = 0;
+  }
+  uint64_t next() {
+    if (pos >= 16) refill();
+    uint64_t v = (uint64_t)buf[pos] | ((uint64_t)buf[pos + 1] << 32);
+    pos += 2;
+    return v;
+  }
+  uint64_t next_mod_p() {
+    for (;;) {
+      uint64_t v = next();
+      if (v < P) return v;
+    }
+  }
+  // Box-Muller (cosine branch) with series log / cos in plain IEEE double arithmetic.
+  static double dlog(double u) {
+    int ex;
+    double m = frexp(u, &ex);
+    if (m < 0.70710678118654752) { m *= 2.0; ex -= 1; }
+    const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+    double term = s, acc = 0.0;
+    for (int i = 1; i <= 23; i += 2) { acc += term / (double)i; term *= s2; }
+    return (double)ex * 6.93147180369123816490e-01 + ((double)ex * 1.90821492927058770002e-10 + 2.0 * acc);
+  }
+  static double dsin(double x) {
+    const double x2 = x * x;
+    double term = x, acc = 0.0;
+    for (int i = 1; i <= 21; i += 2) { acc += term; term = -term * x2 / (double)((i + 1) * (i + 2)); }
+    return acc;
+  }
+  static double dcos(double x) {
+    const double x2 = x * x;
+    double term = 1.0, acc = 0.0;
+    for (int i = 0; i <= 20; i += 2) { acc += term; term = -term * x2 / (double)((i + 1) * (i + 2)); }
+    return acc;
+  }
+  static double dcos2pi(double u) {
+    const double two_pi = 6.28318530717958647692;
+    double v = u <= 0.5 ? u : 1.0 - u, sg = 1.0;
+    if (v > 0.25) { sg = -1.0; v = 0.5 - v; }
+    if (v > 0.125) return sg * dsin(two_pi * (0.25 - v));
+    return sg * dcos(two_pi * v);
+  }
+  int64_t gauss(int32_t log2_sigma) {
+    const double u1 = (double)((next() >> 11) + 1) * 0x1.0p-53;
+    const double u2 = (double)(next() >> 11) * 0x1.0p-53;
+    const double z = sqrt(-2.0 * dlog(u1)) * dcos2pi(u2);
+    return (int64_t)llrint(ldexp(z, 64 + log2_sigma));
+  }
+};
+
+// ---------------------------------------------------------------- Z_p helpers (host)
+static inline uint64_t padd(uint64_t a, uint64_t b) {
+  uint64_t s = a + b;
+  return (s < a || s >= P) ? s + 0xFFFFFFFFull : s;
+}
+static inline uint64_t psub(uint64_t a, uint64_t b) { return a < b ? a - b + P : a - b; }
+static inline uint64_t pfrom(int64_t v) {
+  if (v >= 0) return (uint64_t)v;
+  uint64_t m = (0ull - (uint64_t)v) % P;
+  return m ? P - m : 0;
+}
+
+size_t bsk_len(const tfhe_params& p) { return (size_t)p.n * (p.k + 1) * p.pbs_level * (p.k + 1) * p.N; }
+size_t ksk_len(const tfhe_params& p) { return (size_t)p.k * p.N * p.ks_level * (p.n + 1); }
+
+// GLWE_S(0) over Z_p: masks uniform, body = sum_c A_c * S_c + E.  S is binary, so the product is
+// a signed sum of rotated masks.
+static void glwe_zero(const tfhe_params& p, const uint64_t* S, ChaCha& r, uint64_t* out) {
+  const uint32_t N = p.N, k = p.k;
+  for (uint32_t c = 0; c < k; c++)
+    for (uint32_t i = 0; i < N; i++) out[(size_t)c * N + i] = r.next_mod_p();
+  uint64_t* body = out + (size_t)k * N;
+  for (uint32_t i = 0; i < N; i++) body[i] = pfrom(r.gauss(p.glwe_noise_log2));
+  for (uint32_t c = 0; c < k; c++) {
+    const uint64_t* A = out + (size_t)c * N;
+    const uint64_t* Sc = S + (size_t)c * N;
+    for (uint32_t j = 0; j < N; j++) {
+      if (!Sc[j]) continue;
+      // body[d] += A[d - j] for d >= j ; body[d] -= A[d - j + N] for d < j
+      for (uint32_t d = 0; d < j; d++) body[d] = psub(body[d], A[d + N - j]);
+      for (uint32_t d = j; d < N; d++) body[d] = padd(body[d], A[d - j]);
+    }
+  }
+}
+
+static void lwe_one(uint32_t dim, const uint64_t* key, int32_t noise_log2, ChaCha& r, uint64_t m, uint64_t* out) {
+  uint64_t acc = 0;
+  for (uint32_t i = 0; i < dim; i++) {
+    out[i] = r.next();
+    acc += out[i] * key[i];
+  }
+  acc += (uint64_t)r.gauss(noise_log2);
+  out[dim] = acc + m;
+}
+
+void keygen(const tfhe_params& p, uint64_t seed, uint64_t* lwe_key, uint64_t* glwe_key, uint64_t* bsk,
+            uint64_t* ksk) {
+  {
+    ChaCha r(seed, 1);
+    for (uint32_t i = 0; i < p.n; i++) lwe_key[i] = r.next() & 1;
+  }
+  {
+    ChaCha r(seed, 2);
+    for (uint32_t i = 0; i < p.k * p.N; i++) glwe_key[i] = r.next() & 1;
+  }
+  if (bsk) {
+    const size_t row = (size_t)(p.k + 1) * p.N, per_i = (size_t)(p.k + 1) * p.pbs_level * row;
+    parallel_for((int64_t)p.n, [&](int64_t i) {
+      ChaCha r(seed, 0x1000 + (uint64_t)i);
+      for (uint32_t c = 0; c <= p.k; c++)
+        for (uint32_t l = 0; l < p.pbs_level; l++) {
+          uint64_t* out = bsk + per_i * i + row * (c * p.pbs_level + l);
+          glwe_zero(p, glwe_key, r, out);
+          if (lwe_key[i]) {
+            const uint64_t g = 1ull << (64 - p.pbs_base_log * (l + 1));
+            out[(size_t)c * p.N] = padd(out[(size_t)c * p.N], g);
+          }
+        }
+    });
+  }
+  if (ksk) {
+    const size_t per_j = (size_t)p.ks_level * (p.n + 1);
+    parallel_for((int64_t)(p.k * p.N), [&](int64_t j) {
+      ChaCha r(seed, 0x100000 + (uint64_t)j);
+      for (uint32_t l = 0; l < p.ks_level; l++)
+        lwe_one(p.n, lwe_key, p.lwe_noise_log2, r, glwe_key[j] << (64 - p.ks_base_log * (l + 1)),
+                ksk + per_j * j + (size_t)l * (p.n + 1));
+    });
+  }
+}
+
+void lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, uint64_t seed, uint64_t stream0,
+                 const uint64_t* msgs, size_t count, uint64_t* out) {
+  auto one = [&](int64_t q) {
+    ChaCha r(seed, stream0 + (uint64_t)q);
+    lwe_one(dim, key, noise_log2, r, msgs[q], out + (size_t)q * (dim + 1));
+  };
+  if (count > 256) parallel_for((int64_t)count, one);
+  else for (int64_t q = 0; q < (int64_t)count; q++) one(q);
+}
+
+void lwe_phase(uint32_t dim, const uint64_t* key, const uint64_t* ct, size_t count, uint64_t* out) {
+  for (size_t q = 0; q < count; q++) {
+    const uint64_t* c = ct + q * (dim + 1);
+    uint64_t s = 0;
+    for (uint32_t i = 0; i < dim; i++) s += c[i] * key[i];
+    out[q] = c[dim] - s;
+  }
+}
+
+static inline uint64_t tor_to_p(uint64_t v) { return v - ((v >> 32) + ((v >> 31) & 1)); }
+
+void lut_constant(uint32_t N, uint64_t v, uint64_t* lut) {
+  const uint64_t g = tor_to_p(v);
+  for (uint32_t i = 0; i < N; i++) lut[i] = g;
+}
+
+// tfhe-rs generate_accumulator layout: box = N / msg_modulus, v[i] = f(i / box) * delta,
+// then X^{-box/2} (half-box negacyclic rotation) so message m lands in the middle of its box.
+void lut_from_table(uint32_t N, uint32_t msg_modulus, const uint64_t* table, uint64_t delta, uint64_t* lut) {
+  const uint32_t box = N / msg_modulus, half = box / 2;
+  for (uint32_t i = 0; i < N; i++) {
+    const uint32_t src = i + half;  // lut[i] = (X^{-half} v)[i] = v[i + half], negated past N
+    if (src < N) lut[i] = tor_to_p(table[src / box] * delta);
+    else {
+      const uint64_t g = tor_to_p(table[(src - N) / box] * delta);
+      lut[i] = g ? P - g : 0;
+    }
+  }
+}
+
+}  // namespace client
+}  // namespace tfhe

@@ -1,0 +1,19 @@
+// client.h — host-side key material (see client.cpp).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/tfhe_hip.h"
+
+namespace tfhe {
+namespace client {
+size_t bsk_len(const tfhe_params& p);
+size_t ksk_len(const tfhe_params& p);
+void keygen(const tfhe_params& p, uint64_t seed, uint64_t* lwe_key, uint64_t* glwe_key, uint64_t* bsk, uint64_t* ksk);
+void lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, uint64_t seed, uint64_t stream0,
+                 const uint64_t* msgs, size_t count, uint64_t* out);
+void lwe_phase(uint32_t dim, const uint64_t* key, const uint64_t* ct, size_t count, uint64_t* out);
+void lut_constant(uint32_t N, uint64_t torus_value, uint64_t* lut);
+void lut_from_table(uint32_t N, uint32_t msg_modulus, const uint64_t* table, uint64_t delta, uint64_t* lut);
+}  // namespace client
+}  // namespace tfhe
