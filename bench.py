@@ -36,6 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import tfhe_amd  # noqa: E402  (imports torch first: one HIP runtime per process)
+from tfhe_amd.dist import broadcast_keys, rank_batch_seed  # noqa: E402
 
 METRIC = "PBS/sec at TFHE 128-bit default (N=1024), batch=4096; 1/2/4/8 MI355X"
 KEY_SEED = 0x7F4E0001
@@ -47,6 +48,20 @@ HBM_PEAK_GBS = 8000.0
 
 def log(msg: str) -> None:
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def pmc_traffic(B: int):
+    """HBM bytes per blind-rotate launch from the committed rocprofv3 PMC passes
+    (profiles/*_pmc_blind_rotate.json, produced by tools/pmc_summary.py for this same command), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_blind_rotate.json")))
+    if not files or B != 4096:
+        return None
+    d = json.load(open(files[-1]))
+    for k, v in d.items():
+        if "blind_rotate_kernel" in k:
+            return round(v["hbm_bytes_per_launch"])
+    return None
 
 
 def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int):
@@ -82,6 +97,9 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--cpu-sample", type=int, default=0, help="PBS in the CPU baseline sample (0 = auto)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on GPUs; gloo only for rehearsals")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank uses device 0 (with --dist-backend gloo)")
     args = ap.parse_args()
 
     import torch
@@ -89,13 +107,16 @@ def main() -> int:
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     params = tfhe_amd.Params.preset(tfhe_amd.PRESET_GATE)
     B = args.batch
@@ -116,18 +137,13 @@ def main() -> int:
     bcast_ms = 0.0
     if world > 1:
         dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        dist.broadcast(d_bsk, src=0)
-        dist.broadcast(d_ksk, src=0)
-        torch.cuda.synchronize()
-        bcast_ms = (time.perf_counter() - t0) * 1e3
+        bcast_ms = broadcast_keys(d_bsk, d_ksk, src=0)
     eng = tfhe_amd.Engine(params, local)
     eng.load_keys_device(d_bsk, d_ksk)
     del d_bsk, d_ksk
 
     # ---- inputs: this rank's batch, encrypted on the host, resident in HBM ----------------------
-    rng = np.random.default_rng(INPUT_SEED + rank)
+    rng = np.random.default_rng(rank_batch_seed(INPUT_SEED, rank))
     bits = rng.integers(0, 2, B).astype(bool)
     cts = ck.encrypt_bool(bits, seed=INPUT_SEED + 1, stream0=rank * B)
     d_in = torch.from_numpy(cts.view(np.int64)).to(dev)
@@ -188,7 +204,7 @@ def main() -> int:
             "data": "synthetic: ChaCha20-seeded LWE encryptions of uniform bits (key seed 0x7F4E0001), gate LUT",
             "config": {
                 "workload": "P-GATE PBS (blind rotate + sample extract + keyswitch), n=630 k=1 N=1024, "
-                            "PBS 2^7x3, KS 2^2x8, batch 4096 per GPU",
+                            f"PBS 2^7x3, KS 2^2x8, batch {B} per GPU",
                 "batch_per_gpu": B,
                 "params": params.as_dict(),
                 "parallelism": f"batch-sharded x{world}, BSK/KSK RCCL broadcast once",
@@ -200,7 +216,7 @@ def main() -> int:
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": pmc_traffic(B),
                 "bytes_per_launch": B * BR_BYTES_PER_PBS,
                 "kernel_ms": round(br_avg, 3),
                 "launches": br_n,

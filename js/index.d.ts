@@ -1,0 +1,73 @@
+// Type declarations for @luxfhe-amd/tfhe (js/index.js).  Mirrors the FheBool / FheUint* and
+// LuxFHEClient surfaces of the reference (packages/luxfhejs/src/index.ts, sdk/relayer/src/tfhe.ts).
+export interface TfheParams {
+  n: number; k: number; N: number; pbs_base_log: number; pbs_level: number;
+  ks_base_log: number; ks_level: number; lwe_noise_log2: number; glwe_noise_log2: number; order: number;
+}
+export const PRESET_GATE: 0;
+export const PRESET_FHEVM: 1;
+export const MU: bigint;
+export function paramsPreset(which?: number): TfheParams;
+
+export class ClientKey {
+  readonly params: TfheParams; readonly seed: bigint;
+  readonly lweKey: BigUint64Array; readonly glweKey: BigUint64Array;
+  static generate(params?: TfheParams, seed?: bigint): ClientKey;
+  encryptTorus(msgs: BigUint64Array | Iterable<bigint | number>, seed?: bigint, stream0?: bigint): BigUint64Array;
+  phase(cts: BigUint64Array): BigUint64Array;
+  encryptBool(bits: Iterable<boolean>, seed?: bigint, stream0?: bigint): BigUint64Array;
+  decryptBool(cts: BigUint64Array): boolean[];
+  encrypt(values: Iterable<number | bigint>, msgModulus: number, seed?: bigint, stream0?: bigint): BigUint64Array;
+  decrypt(cts: BigUint64Array, msgModulus: number): number[];
+}
+export class ServerKey { readonly params: TfheParams; readonly bsk: BigUint64Array; readonly ksk: BigUint64Array; }
+export function genKeys(params?: TfheParams, seed?: bigint): [ClientKey, ServerKey];
+
+export class Engine {
+  constructor(params?: TfheParams, device?: number);
+  loadKeys(sk: ServerKey): this;
+  destroy(): void;
+  gateLut(): BigUint64Array;
+  generateAccumulator(f: (m: number) => number | bigint, msgModulus?: number, deltaOut?: bigint | null): BigUint64Array;
+  pbs(cts: BigUint64Array, luts: BigUint64Array, lutIndex?: Uint32Array | null): Promise<BigUint64Array>;
+  keyswitchProgrammableBootstrap(ct: BigUint64Array, acc: BigUint64Array): Promise<BigUint64Array>;
+  nand(c1: BigUint64Array, c2: BigUint64Array): Promise<BigUint64Array>;
+}
+
+export class FheBool {
+  constructor(engine: Engine, ct: BigUint64Array);
+  readonly ct: BigUint64Array;
+  static encrypt(values: boolean | boolean[], ck: ClientKey, engine: Engine, seed?: bigint, stream0?: bigint): FheBool;
+  decrypt(ck: ClientKey): boolean[];
+  nand(o: FheBool): Promise<FheBool>;
+  and(o: FheBool): Promise<FheBool>;
+  or(o: FheBool): Promise<FheBool>;
+  xor(o: FheBool): Promise<FheBool>;
+  not(): FheBool;
+}
+declare class FheUintN {
+  constructor(engine: Engine, ct: BigUint64Array);
+  readonly ct: BigUint64Array;
+  static readonly bitWidth: number;
+  decrypt(ck: ClientKey): bigint[];
+  and(o: FheUintN): Promise<FheUintN>;
+  or(o: FheUintN): Promise<FheUintN>;
+  xor(o: FheUintN): Promise<FheUintN>;
+  not(): FheUintN;
+}
+export class FheUint8 extends FheUintN { static encrypt(v: number | bigint | Array<number | bigint>, ck: ClientKey, e: Engine, seed?: bigint, stream0?: bigint): FheUint8; }
+export class FheUint16 extends FheUintN { static encrypt(v: number | bigint | Array<number | bigint>, ck: ClientKey, e: Engine, seed?: bigint, stream0?: bigint): FheUint16; }
+export class FheUint32 extends FheUintN { static encrypt(v: number | bigint | Array<number | bigint>, ck: ClientKey, e: Engine, seed?: bigint, stream0?: bigint): FheUint32; }
+
+export interface EvaluateRequest { op: 'and' | 'or' | 'xor' | 'not'; left: Uint8Array; right?: Uint8Array; bitWidth: 8 | 16 | 32; }
+export class LuxFHELocalClient {
+  constructor(config?: { params?: TfheParams; seed?: bigint; device?: number });
+  initialize(): Promise<void>;
+  getPublicKey(): Promise<Uint8Array>;
+  encrypt_uint8(v: number): Promise<Uint8Array>;
+  encrypt_uint16(v: number): Promise<Uint8Array>;
+  encrypt_uint32(v: number): Promise<Uint8Array>;
+  evaluate(req: EvaluateRequest): Promise<Uint8Array>;
+  decrypt(ct: Uint8Array, bitWidth: 8 | 16 | 32): Promise<bigint>;
+  close(): void;
+}

@@ -1,0 +1,475 @@
+/*
+ * tfhe_napi.c — N-API binding of libtfhe_hip.so (include/tfhe_hip.h) for Node.
+ *
+ * Replaces the packages/wasm TFHE core that the JS SDKs reach (tfhe-rs WASM/N-API:
+ * packages/pnpm-lock.yaml:1988-1995; used through global.TFHE, sdk/relayer/src/node.ts:1-4) and the
+ * compute behind packages/luxfhejs' server calls (packages/luxfhejs/src/index.ts:127-141).
+ *
+ * Buffers cross as BigUint64Array / Uint32Array (zero-copy views of their backing stores).
+ * Device work (pbs, nand) runs in napi_create_async_work and resolves a Promise, so the event
+ * loop never blocks; argument buffers are referenced until the work completes.  A failing
+ * C-ABI call becomes a JS Error whose `code` is the TFHE_HIP_E* status.
+ */
+#include <node_api.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/tfhe_hip.h"
+
+#define NAPI_CALL(env, call)                                              \
+  do {                                                                    \
+    if ((call) != napi_ok) {                                              \
+      napi_throw_error((env), "EINTERNAL", "N-API call failed: " #call); \
+      return NULL;                                                        \
+    }                                                                     \
+  } while (0)
+
+static napi_value throw_tfhe(napi_env env, int rc) {
+  napi_value err, msg, code;
+  char cbuf[16];
+  const char* m = tfhe_hip_last_error();
+  napi_create_string_utf8(env, m && *m ? m : "tfhe_hip error", NAPI_AUTO_LENGTH, &msg);
+  snprintf(cbuf, sizeof(cbuf), "%d", rc);
+  napi_create_string_utf8(env, cbuf, NAPI_AUTO_LENGTH, &code);
+  napi_create_error(env, code, msg, &err);
+  napi_value num;
+  napi_create_int32(env, rc, &num);
+  napi_set_named_property(env, err, "status", num);
+  napi_throw(env, err);
+  return NULL;
+}
+
+/* typed-array argument -> data pointer + element count, checking the element type */
+static int get_typed(napi_env env, napi_value v, napi_typedarray_type want, void** data, size_t* len) {
+  bool is_ta = false;
+  if (napi_is_typedarray(env, v, &is_ta) != napi_ok || !is_ta) return 0;
+  napi_typedarray_type t;
+  napi_value ab;
+  size_t off;
+  if (napi_get_typedarray_info(env, v, &t, len, data, &ab, &off) != napi_ok) return 0;
+  return t == want;
+}
+
+static napi_value new_u64_array(napi_env env, size_t count, uint64_t** data) {
+  napi_value ab, ta;
+  void* p = NULL;
+  if (napi_create_arraybuffer(env, count * 8, &p, &ab) != napi_ok) return NULL;
+  memset(p, 0, count * 8);
+  if (napi_create_typedarray(env, napi_biguint64_array, count, ab, 0, &ta) != napi_ok) return NULL;
+  *data = (uint64_t*)p;
+  return ta;
+}
+
+static int get_u64(napi_env env, napi_value v, uint64_t* out) {
+  bool lossless;
+  napi_valuetype t;
+  napi_typeof(env, v, &t);
+  if (t == napi_bigint) return napi_get_value_bigint_uint64(env, v, out, &lossless) == napi_ok;
+  if (t == napi_number) {
+    double d;
+    napi_get_value_double(env, v, &d);
+    if (d < 0) return 0;
+    *out = (uint64_t)d;
+    return 1;
+  }
+  return 0;
+}
+
+static int get_params(napi_env env, napi_value v, tfhe_params* p) {
+  napi_valuetype t;
+  napi_typeof(env, v, &t);
+  if (t == napi_number) {
+    int32_t preset;
+    napi_get_value_int32(env, v, &preset);
+    return tfhe_hip_params_preset(preset, p) == 0;
+  }
+  if (t != napi_object) return 0;
+  const char* names[] = {"n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
+                         "lwe_noise_log2", "glwe_noise_log2", "order"};
+  int32_t vals[10];
+  for (int i = 0; i < 10; i++) {
+    napi_value f;
+    if (napi_get_named_property(env, v, names[i], &f) != napi_ok) return 0;
+    if (napi_get_value_int32(env, f, &vals[i]) != napi_ok) return 0;
+  }
+  p->n = vals[0]; p->k = vals[1]; p->N = vals[2]; p->pbs_base_log = vals[3]; p->pbs_level = vals[4];
+  p->ks_base_log = vals[5]; p->ks_level = vals[6]; p->lwe_noise_log2 = vals[7]; p->glwe_noise_log2 = vals[8];
+  p->order = vals[9];
+  return 1;
+}
+
+static napi_value params_to_js(napi_env env, const tfhe_params* p) {
+  napi_value o, x;
+  napi_create_object(env, &o);
+#define SETF(name, val) napi_create_int32(env, (int32_t)(val), &x); napi_set_named_property(env, o, name, x);
+  SETF("n", p->n) SETF("k", p->k) SETF("N", p->N) SETF("pbs_base_log", p->pbs_base_log)
+  SETF("pbs_level", p->pbs_level) SETF("ks_base_log", p->ks_base_log) SETF("ks_level", p->ks_level)
+  SETF("lwe_noise_log2", p->lwe_noise_log2) SETF("glwe_noise_log2", p->glwe_noise_log2) SETF("order", p->order)
+#undef SETF
+  return o;
+}
+
+/* paramsPreset(preset) -> {n, k, N, ...} */
+static napi_value js_params_preset(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  tfhe_params p;
+  int32_t preset = 0;
+  if (argc > 0) napi_get_value_int32(env, argv[0], &preset);
+  int rc = tfhe_hip_params_preset(preset, &p);
+  if (rc) return throw_tfhe(env, rc);
+  return params_to_js(env, &p);
+}
+
+/* keygen(params, seed[, withServerKey=true]) -> {lweKey, glweKey, bsk, ksk} */
+static napi_value js_keygen(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  tfhe_params p;
+  uint64_t seed = 0;
+  if (argc < 2 || !get_params(env, argv[0], &p) || !get_u64(env, argv[1], &seed)) {
+    napi_throw_type_error(env, "EINVAL", "keygen(params, seed[, withServerKey])");
+    return NULL;
+  }
+  bool with_sk = true;
+  if (argc > 2) napi_get_value_bool(env, argv[2], &with_sk);
+  uint64_t *lwe, *glwe, *bsk = NULL, *ksk = NULL;
+  napi_value o, a_lwe, a_glwe, a_bsk = NULL, a_ksk = NULL;
+  a_lwe = new_u64_array(env, p.n, &lwe);
+  a_glwe = new_u64_array(env, (size_t)p.k * p.N, &glwe);
+  if (!a_lwe || !a_glwe) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  if (with_sk) {
+    a_bsk = new_u64_array(env, tfhe_hip_bsk_len(&p), &bsk);
+    a_ksk = new_u64_array(env, tfhe_hip_ksk_len(&p), &ksk);
+    if (!a_bsk || !a_ksk) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  }
+  int rc = tfhe_hip_keygen(&p, seed, lwe, glwe, bsk, ksk);
+  if (rc) return throw_tfhe(env, rc);
+  napi_create_object(env, &o);
+  napi_set_named_property(env, o, "lweKey", a_lwe);
+  napi_set_named_property(env, o, "glweKey", a_glwe);
+  if (with_sk) {
+    napi_set_named_property(env, o, "bsk", a_bsk);
+    napi_set_named_property(env, o, "ksk", a_ksk);
+  }
+  napi_set_named_property(env, o, "params", params_to_js(env, &p));
+  return o;
+}
+
+/* encrypt(key: BigUint64Array, noiseLog2, seed, stream0, msgs: BigUint64Array) -> BigUint64Array */
+static napi_value js_encrypt(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  uint64_t *key, *msgs, seed, stream0, *out;
+  size_t dim, count;
+  int32_t noise;
+  if (argc < 5 || !get_typed(env, argv[0], napi_biguint64_array, (void**)&key, &dim) ||
+      napi_get_value_int32(env, argv[1], &noise) != napi_ok || !get_u64(env, argv[2], &seed) ||
+      !get_u64(env, argv[3], &stream0) || !get_typed(env, argv[4], napi_biguint64_array, (void**)&msgs, &count)) {
+    napi_throw_type_error(env, "EINVAL", "encrypt(key, noiseLog2, seed, stream0, msgs)");
+    return NULL;
+  }
+  napi_value res = new_u64_array(env, count * (dim + 1), &out);
+  if (!res) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  int rc = tfhe_hip_lwe_encrypt((uint32_t)dim, key, noise, seed, stream0, msgs, count, out);
+  if (rc) return throw_tfhe(env, rc);
+  return res;
+}
+
+/* phase(key, cts) -> BigUint64Array of b - <a, s> */
+static napi_value js_phase(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  uint64_t *key, *ct, *out;
+  size_t dim, n;
+  if (argc < 2 || !get_typed(env, argv[0], napi_biguint64_array, (void**)&key, &dim) ||
+      !get_typed(env, argv[1], napi_biguint64_array, (void**)&ct, &n) || n % (dim + 1)) {
+    napi_throw_type_error(env, "EINVAL", "phase(key, cts)");
+    return NULL;
+  }
+  napi_value res = new_u64_array(env, n / (dim + 1), &out);
+  int rc = tfhe_hip_lwe_phase((uint32_t)dim, key, ct, n / (dim + 1), out);
+  if (rc) return throw_tfhe(env, rc);
+  return res;
+}
+
+/* lutConstant(N, value) / lutFromTable(N, msgModulus, table: BigUint64Array, deltaOut) */
+static napi_value js_lut_constant(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  uint32_t N;
+  uint64_t v, *out;
+  if (argc < 2 || napi_get_value_uint32(env, argv[0], &N) != napi_ok || !get_u64(env, argv[1], &v)) {
+    napi_throw_type_error(env, "EINVAL", "lutConstant(N, value)");
+    return NULL;
+  }
+  napi_value res = new_u64_array(env, N, &out);
+  int rc = tfhe_hip_lut_constant(N, v, out);
+  if (rc) return throw_tfhe(env, rc);
+  return res;
+}
+
+static napi_value js_lut_from_table(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  uint32_t N, mm;
+  uint64_t *table, delta, *out;
+  size_t tl;
+  if (argc < 4 || napi_get_value_uint32(env, argv[0], &N) != napi_ok ||
+      napi_get_value_uint32(env, argv[1], &mm) != napi_ok ||
+      !get_typed(env, argv[2], napi_biguint64_array, (void**)&table, &tl) || tl < mm || !get_u64(env, argv[3], &delta)) {
+    napi_throw_type_error(env, "EINVAL", "lutFromTable(N, msgModulus, table, deltaOut)");
+    return NULL;
+  }
+  napi_value res = new_u64_array(env, N, &out);
+  int rc = tfhe_hip_lut_from_table(N, mm, table, delta, out);
+  if (rc) return throw_tfhe(env, rc);
+  return res;
+}
+
+/* ------------------------------------------------------------------------------ engine */
+static void finalize_ctx(napi_env env, void* data, void* hint) {
+  (void)env; (void)hint;
+  if (data) tfhe_hip_destroy((tfhe_ctx*)data);
+}
+
+typedef struct {
+  tfhe_ctx* ctx;
+  tfhe_params p;
+} ctx_box;
+
+static void finalize_box(napi_env env, void* data, void* hint) {
+  ctx_box* b = (ctx_box*)data;
+  if (b) {
+    finalize_ctx(env, b->ctx, hint);
+    free(b);
+  }
+}
+
+static ctx_box* get_box(napi_env env, napi_value v) {
+  void* d = NULL;
+  if (napi_get_value_external(env, v, &d) != napi_ok) return NULL;
+  return (ctx_box*)d;
+}
+
+/* createEngine(params, device) -> external handle (destroyed by GC or destroyEngine) */
+static napi_value js_create(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  tfhe_params p;
+  int32_t dev = 0;
+  if (argc < 1 || !get_params(env, argv[0], &p)) {
+    napi_throw_type_error(env, "EINVAL", "createEngine(params[, device])");
+    return NULL;
+  }
+  if (argc > 1) napi_get_value_int32(env, argv[1], &dev);
+  tfhe_ctx* c = NULL;
+  int rc = tfhe_hip_create(&p, dev, &c);
+  if (rc) return throw_tfhe(env, rc);
+  ctx_box* b = (ctx_box*)calloc(1, sizeof(ctx_box));
+  b->ctx = c;
+  b->p = p;
+  napi_value ext;
+  NAPI_CALL(env, napi_create_external(env, b, finalize_box, NULL, &ext));
+  return ext;
+}
+
+static napi_value js_destroy(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  ctx_box* b = argc ? get_box(env, argv[0]) : NULL;
+  if (b && b->ctx) {
+    tfhe_hip_destroy(b->ctx);
+    b->ctx = NULL;
+  }
+  return NULL;
+}
+
+/* loadKeys(handle, bsk, ksk) */
+static napi_value js_load_keys(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  ctx_box* b = argc ? get_box(env, argv[0]) : NULL;
+  uint64_t *bsk, *ksk;
+  size_t bl, kl;
+  if (!b || !b->ctx || argc < 3 || !get_typed(env, argv[1], napi_biguint64_array, (void**)&bsk, &bl) ||
+      !get_typed(env, argv[2], napi_biguint64_array, (void**)&ksk, &kl)) {
+    napi_throw_type_error(env, "EINVAL", "loadKeys(engine, bsk, ksk)");
+    return NULL;
+  }
+  int rc = tfhe_hip_load_keys(b->ctx, bsk, bl, ksk, kl);
+  if (rc) return throw_tfhe(env, rc);
+  return NULL;
+}
+
+/* ---- async work: pbs / nand ------------------------------------------------------------ */
+typedef struct {
+  napi_async_work work;
+  napi_deferred deferred;
+  napi_ref refs[4];
+  int nrefs;
+  tfhe_ctx* ctx;
+  int kind; /* 0 = pbs, 1 = nand */
+  const uint64_t *in, *in2, *luts;
+  const uint32_t* lut_index;
+  size_t B, n_lut;
+  uint64_t* out;
+  napi_ref out_ref;
+  int rc;
+  char err[256];
+} job_t;
+
+static void job_execute(napi_env env, void* data) {
+  (void)env;
+  job_t* j = (job_t*)data;
+  if (j->kind == 0) j->rc = tfhe_hip_pbs(j->ctx, j->in, j->B, j->luts, j->n_lut, j->lut_index, j->out);
+  else j->rc = tfhe_hip_nand(j->ctx, j->in, j->in2, j->B, j->out);
+  if (j->rc) snprintf(j->err, sizeof(j->err), "%s", tfhe_hip_last_error());
+}
+
+static void job_complete(napi_env env, napi_status status, void* data) {
+  job_t* j = (job_t*)data;
+  napi_value out;
+  napi_get_reference_value(env, j->out_ref, &out);
+  if (status == napi_ok && j->rc == 0) {
+    napi_resolve_deferred(env, j->deferred, out);
+  } else {
+    napi_value err, msg, code, num;
+    char cbuf[16];
+    snprintf(cbuf, sizeof(cbuf), "%d", j->rc);
+    napi_create_string_utf8(env, j->rc ? j->err : "async work cancelled", NAPI_AUTO_LENGTH, &msg);
+    napi_create_string_utf8(env, cbuf, NAPI_AUTO_LENGTH, &code);
+    napi_create_error(env, code, msg, &err);
+    napi_create_int32(env, j->rc, &num);
+    napi_set_named_property(env, err, "status", num);
+    napi_reject_deferred(env, j->deferred, err);
+  }
+  for (int i = 0; i < j->nrefs; i++) napi_delete_reference(env, j->refs[i]);
+  napi_delete_reference(env, j->out_ref);
+  napi_delete_async_work(env, j->work);
+  free(j);
+}
+
+static napi_value queue_job(napi_env env, job_t* j, napi_value* keep, int nkeep, size_t out_len) {
+  napi_value promise, out, name;
+  uint64_t* outp;
+  out = new_u64_array(env, out_len, &outp);
+  if (!out) {
+    free(j);
+    return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  }
+  j->out = outp;
+  napi_create_reference(env, out, 1, &j->out_ref);
+  for (int i = 0; i < nkeep; i++) napi_create_reference(env, keep[i], 1, &j->refs[j->nrefs++]);
+  NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
+  napi_create_string_utf8(env, "tfhe_hip", NAPI_AUTO_LENGTH, &name);
+  NAPI_CALL(env, napi_create_async_work(env, NULL, name, job_execute, job_complete, j, &j->work));
+  NAPI_CALL(env, napi_queue_async_work(env, j->work));
+  return promise;
+}
+
+/* pbs(handle, cts, luts[, lutIndex]) -> Promise<BigUint64Array> */
+static napi_value js_pbs(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  ctx_box* b = argc ? get_box(env, argv[0]) : NULL;
+  uint64_t *in, *luts;
+  uint32_t* idx = NULL;
+  size_t n_in, n_l, n_idx = 0;
+  if (!b || !b->ctx || argc < 3 || !get_typed(env, argv[1], napi_biguint64_array, (void**)&in, &n_in) ||
+      !get_typed(env, argv[2], napi_biguint64_array, (void**)&luts, &n_l)) {
+    napi_throw_type_error(env, "EINVAL", "pbs(engine, cts, luts[, lutIndex])");
+    return NULL;
+  }
+  napi_valuetype t = napi_undefined;
+  if (argc > 3) napi_typeof(env, argv[3], &t);
+  if (t != napi_undefined && t != napi_null && !get_typed(env, argv[3], napi_uint32_array, (void**)&idx, &n_idx)) {
+    napi_throw_type_error(env, "EINVAL", "lutIndex must be a Uint32Array");
+    return NULL;
+  }
+  job_t* j = (job_t*)calloc(1, sizeof(job_t));
+  j->ctx = b->ctx;
+  j->kind = 0;
+  j->in = in;
+  j->luts = luts;
+  j->lut_index = idx;
+  const tfhe_params p = b->p;
+  const size_t dim = (size_t)tfhe_hip_io_dim(&p) + 1;
+  if (n_in % dim || n_l % p.N || (idx && n_idx != n_in / dim)) {
+    free(j);
+    napi_throw_range_error(env, "EINVAL", "pbs: buffer sizes do not match the parameter set");
+    return NULL;
+  }
+  j->B = n_in / dim;
+  j->n_lut = n_l / p.N;
+  napi_value keep[3] = {argv[1], argv[2], idx ? argv[3] : argv[1]};
+  return queue_job(env, j, keep, 3, n_in);
+}
+
+/* nand(handle, c1, c2) -> Promise<BigUint64Array> */
+static napi_value js_nand(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  ctx_box* b = argc ? get_box(env, argv[0]) : NULL;
+  uint64_t *c1, *c2;
+  size_t n1, n2;
+  if (!b || !b->ctx || argc < 3 || !get_typed(env, argv[1], napi_biguint64_array, (void**)&c1, &n1) ||
+      !get_typed(env, argv[2], napi_biguint64_array, (void**)&c2, &n2) || n1 != n2) {
+    napi_throw_type_error(env, "EINVAL", "nand(engine, c1, c2) with equal-length BigUint64Arrays");
+    return NULL;
+  }
+  const size_t dim = (size_t)b->p.n + 1;
+  if (n1 % dim) {
+    napi_throw_range_error(env, "EINVAL", "nand: length is not a multiple of n + 1");
+    return NULL;
+  }
+  job_t* j = (job_t*)calloc(1, sizeof(job_t));
+  j->ctx = b->ctx;
+  j->kind = 1;
+  j->in = c1;
+  j->in2 = c2;
+  j->B = n1 / dim;
+  napi_value keep[2] = {argv[1], argv[2]};
+  return queue_job(env, j, keep, 2, n1);
+}
+
+static napi_value js_last_error(napi_env env, napi_callback_info info) {
+  (void)info;
+  napi_value s;
+  napi_create_string_utf8(env, tfhe_hip_last_error(), NAPI_AUTO_LENGTH, &s);
+  return s;
+}
+
+static napi_value init(napi_env env, napi_value exports) {
+  napi_property_descriptor d[] = {
+      {"paramsPreset", 0, js_params_preset, 0, 0, 0, napi_enumerable, 0},
+      {"keygen", 0, js_keygen, 0, 0, 0, napi_enumerable, 0},
+      {"encrypt", 0, js_encrypt, 0, 0, 0, napi_enumerable, 0},
+      {"phase", 0, js_phase, 0, 0, 0, napi_enumerable, 0},
+      {"lutConstant", 0, js_lut_constant, 0, 0, 0, napi_enumerable, 0},
+      {"lutFromTable", 0, js_lut_from_table, 0, 0, 0, napi_enumerable, 0},
+      {"createEngine", 0, js_create, 0, 0, 0, napi_enumerable, 0},
+      {"destroyEngine", 0, js_destroy, 0, 0, 0, napi_enumerable, 0},
+      {"loadKeys", 0, js_load_keys, 0, 0, 0, napi_enumerable, 0},
+      {"pbs", 0, js_pbs, 0, 0, 0, napi_enumerable, 0},
+      {"nand", 0, js_nand, 0, 0, 0, napi_enumerable, 0},
+      {"lastError", 0, js_last_error, 0, 0, 0, napi_enumerable, 0},
+  };
+  napi_define_properties(env, exports, sizeof(d) / sizeof(d[0]), d);
+  return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

@@ -1,0 +1,51 @@
+"""The N-API boundary: js/ (addon + JS shim) driven by node.  CPU checks run here; the GPU checks
+are marked gpu.  Key material through N-API must equal the Python/ctypes path byte-for-byte."""
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+NODE = shutil.which("node")
+ADDON = os.path.join(ROOT, "js", "build", "tfhe_napi.node")
+pytestmark = pytest.mark.skipif(NODE is None or not os.path.exists("/usr/include/node/node_api.h"),
+                                reason="node / N-API headers not available")
+
+
+def _ensure_addon():
+    if not os.path.exists(ADDON):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "js")], check=True)
+
+
+def _run(script, timeout):
+    _ensure_addon()
+    r = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", script)], capture_output=True, text=True,
+                       timeout=timeout, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_js_addon_cpu(product_keys):
+    out = _run("cpu_check.js", 300)
+    assert out["exports"] == sorted(["paramsPreset", "keygen", "encrypt", "phase", "lutConstant", "lutFromTable",
+                                     "createEngine", "destroyEngine", "loadKeys", "pbs", "nand", "lastError"])
+    ck, sk = product_keys
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+    assert out["lwe_key_sha"] == sha(ck.lwe_key)
+    assert out["bsk_sha"] == sha(sk.bsk)
+    assert out["ksk_sha"] == sha(sk.ksk)
+    cts = ck.encrypt_bool(np.array([True, False, True]), seed=0xC0FFEE02, stream0=5)
+    assert out["ct_sha"] == sha(cts)
+    assert out["err"] == "-1"
+    if out["engine"] != "created":  # no GPU here: a clean error, not an abort
+        assert out["engine"] in ("-1", "-3")
+
+
+@pytest.mark.gpu
+def test_js_addon_gpu():
+    assert _run("gpu_check.js", 600)["ok"] is True
