@@ -29,7 +29,8 @@ __all__ = [
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtfhe_hip.so")
+# TFHE_HIP_LIB overrides the in-tree library (A/B builds of kernel variants in tools/ab.sh).
+LIB_PATH = os.environ.get("TFHE_HIP_LIB") or os.path.join(_HERE, "libtfhe_hip.so")
 PRESET_GATE = 0
 PRESET_FHEVM = 1
 MU = 1 << 61  # gate encoding: true = +1/8, false = -1/8 of the 2^64 torus

@@ -42,11 +42,11 @@ __host__ __device__ constexpr int zeta_exp(int k) {
   return 6 * ((brv_bits(k - (1 << d), d) * 16) >> d);
 }
 
-// In-lane forward stages (spans 16, 8, 4, 2 of the 32-point transform) on the 16 local values.
-template <int KIND>
-__host__ __device__ __forceinline__ void fwd_inlane16(u64 (&x)[16]) {
+// In-lane forward stages (spans FIRST, ..., 2 of the 32-point transform) on the 16 local values.
+template <int KIND, int FIRST>
+__host__ __device__ __forceinline__ void fwd_inlane16_from(u64 (&x)[16]) {
 #pragma unroll
-  for (int ln = 16; ln >= 2; ln >>= 1) {
+  for (int ln = FIRST; ln >= 2; ln >>= 1) {
 #pragma unroll
     for (int e = 0; e < 16; e++) {
       if ((e % ln) < ln / 2) {
@@ -57,6 +57,11 @@ __host__ __device__ __forceinline__ void fwd_inlane16(u64 (&x)[16]) {
       }
     }
   }
+}
+
+template <int KIND>
+__host__ __device__ __forceinline__ void fwd_inlane16(u64 (&x)[16]) {
+  fwd_inlane16_from<KIND, 16>(x);
 }
 
 // In-lane inverse stages (spans 2, 4, 8, 16), Gentleman-Sande, each stage x2.

@@ -56,18 +56,27 @@ __device__ __forceinline__ u32 decomp_7x3(u64 x) {
   return packed;
 }
 
-// value held by lane L ^ 32
-__device__ __forceinline__ u64 xchg32(u64 v) { return __shfl_xor(v, 32); }
+// Cross-lane pair exchange with v_permlane32_swap: with both operands = v, every lane receives
+// (u, w) = (value of lane L & 31, value of lane (L & 31) + 32) — the two inputs of the pair's
+// butterfly — with no selects and no LDS round trip (ds_bpermute).
+__device__ __forceinline__ void pair_values(u64 v, u64& lo, u64& hi) {
+  const u32 v0 = (u32)v, v1 = (u32)(v >> 32);
+  const auto r0 = __builtin_amdgcn_permlane32_swap(v0, v0, false, false);
+  const auto r1 = __builtin_amdgcn_permlane32_swap(v1, v1, false, false);
+  lo = (u64)r0[0] | ((u64)r1[0] << 32);
+  hi = (u64)r0[1] | ((u64)r1[1] << 32);
+}
 
 // span-1 stage of the 32-point transform: positions (2e, 2e+1) live on lanes (L, L^32).
+// Lane half 0 keeps u + t, half 1 keeps u - t, t = zeta * v: computed as u + (+-t).
 template <int KIND>
 __device__ __forceinline__ void fwd_cross(u64 (&x)[16], bool hi) {
 #pragma unroll
   for (int e = 0; e < 16; e++) {
-    const u64 mine = x[e], oth = xchg32(mine);
-    const u64 u = hi ? oth : mine, v = hi ? mine : oth;
+    u64 u, v;
+    pair_values(x[e], u, v);
     const u64 t = gl_mul_pow2(v, zeta_exp<KIND>(16 + e));
-    x[e] = hi ? gl_sub(u, t) : gl_add(u, t);
+    x[e] = gl_add(u, hi ? gl_neg(t) : t);
   }
 }
 
@@ -75,8 +84,8 @@ template <int KIND>
 __device__ __forceinline__ void inv_cross(u64 (&x)[16], bool hi) {
 #pragma unroll
   for (int e = 0; e < 16; e++) {
-    const u64 mine = x[e], oth = xchg32(mine);
-    const u64 U = hi ? oth : mine, V = hi ? mine : oth;
+    u64 U, V;
+    pair_values(x[e], U, V);
     x[e] = hi ? gl_mul_pow2(gl_sub(U, V), 192 - zeta_exp<KIND>(16 + e)) : gl_add(U, V);
   }
 }
@@ -138,26 +147,113 @@ __global__ __launch_bounds__(64) void bsk_to_ntt_kernel(const u64* __restrict__ 
 }
 
 // ------------------------------------------------------------------------------------------
-// One component c of the external product: decompose (X^a - 1) * acc_c, and for each level l
-// accumulate NTT(digits) (.) BSK_i[(c, l)][j] into out_j.
-__device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int a, int c, u64* T, int lane,
-                                                   const u64* __restrict__ bsk_i, const u64* __restrict__ twf,
-                                                   u64 (&out0)[16], u64 (&out1)[16]) {
+// Blind rotation + sample extraction.
+//
+// A workgroup = BR_WAVES wavefronts = BR_WAVES ciphertexts that walk the CMUX loop in lockstep.
+// The external product consumes the BSK in 6 "level steps" per CMUX (row r = c*3 + l, both
+// columns j: 16 KB contiguous in the device layout).  Each step's chunk is streamed ONCE per
+// workgroup into LDS with global_load_lds (16 B/lane, lane-linear image), double-buffered: chunk
+// g+1 is in flight while step g computes, so the MAC reads BSK from LDS instead of waiting on L2 /
+// MALL latency with only 2 waves per SIMD (ablation: the register-streamed MAC took 1/3 of the
+// kernel).  Twiddles are LDS-resident too.  Per wavefront LDS: the 8.4 KB transpose/rotation
+// scratch.  Total 114 KB -> one workgroup (8 waves, 2 per SIMD) per CU.
+constexpr int BR_WAVES = 8;
+constexpr int BR_THREADS = 64 * BR_WAVES;
+constexpr int CHUNK_U64 = 2 * N1K;                 // one level step: rows (c,l), j = 0,1
+constexpr int CHUNK_GLDS = CHUNK_U64 * 8 / 1024;   // 1 KB wave-instructions per chunk (16)
+
+struct BrShared {
+  u64 T[BR_WAVES][T_LDS];        // per-wave transpose / rotation scratch
+  u64 K[2][CHUNK_U64];           // double-buffered BSK chunk
+  u64 tw[2][N1K];                // forward / inverse twiddles
+};
+
+// ordering of one wavefront's own LDS writes before its reads (LDS executes a wave's ops in order;
+// this only stops the compiler from moving them and waits for the writes to retire)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// issue this wave's share of chunk g (2 x 1 KB) into buffer dst
+__device__ __forceinline__ void load_chunk(const u64* __restrict__ bsk, int g, u64* dst, int wave, int lane) {
+  const char* src = (const char*)(bsk + (size_t)g * CHUNK_U64);
+#pragma unroll
+  for (int q = 0; q < CHUNK_GLDS / BR_WAVES; q++) {
+    const int blk = wave * (CHUNK_GLDS / BR_WAVES) + q;  // which 1 KB piece
+    __builtin_amdgcn_global_load_lds((const void*)(src + blk * 1024 + lane * 16),
+                                     (__attribute__((address_space(3))) void*)((char*)dst + blk * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void ntt1024_fwd_digits_lds(const u32 (&dig)[16], int l, u64 (&x)[16], u64* T, int lane,
+                                                       const u64* tw) {
+  const bool hi = lane >= 32;
+  const int c = lane & 31, s = lane >> 5;
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const long long u = (long long)((dig[e] >> (8 * l)) & 0xFFu) - 64;
+    const long long w = ((long long)((dig[e + 8] >> (8 * l)) & 0xFFu) - 64) * (1ll << 48);
+    const long long a = u + w, b = u - w;
+    x[e] = (u64)a + (a < 0 ? GL_P : 0ull);
+    x[e + 8] = (u64)b + (b < 0 ? GL_P : 0ull);
+  }
+  fwd_inlane16_from<NEGA, 8>(x);
+  fwd_cross<NEGA>(x, hi);
+#pragma unroll
+  for (int e = 0; e < 16; e++) x[e] = gl_mul(x[e], tw[64 * e + lane]);
+#pragma unroll
+  for (int e = 0; e < 16; e++) T[(2 * e + s) * TSTRIDE + c] = x[e];
+  wave_lds_sync();
+#pragma unroll
+  for (int e = 0; e < 16; e++) x[e] = T[c * TSTRIDE + 2 * e + s];
+  wave_lds_sync();
+  fwd_inlane16<CYC>(x);
+  fwd_cross<CYC>(x, hi);
+}
+
+__device__ __forceinline__ void ntt1024_inv_lds(u64 (&x)[16], u64* T, int lane, const u64* tw) {
+  const bool hi = lane >= 32;
+  const int c = lane & 31, s = lane >> 5;
+  inv_cross<CYC>(x, hi);
+  inv_inlane16<CYC>(x);
+#pragma unroll
+  for (int e = 0; e < 16; e++) T[c * TSTRIDE + 2 * e + s] = x[e];
+  wave_lds_sync();
+#pragma unroll
+  for (int e = 0; e < 16; e++) x[e] = T[(2 * e + s) * TSTRIDE + c];
+  wave_lds_sync();
+#pragma unroll
+  for (int e = 0; e < 16; e++) x[e] = gl_mul(x[e], tw[64 * e + lane]);
+  inv_cross<NEGA>(x, hi);
+  inv_inlane16<NEGA>(x);
+}
+
+// One component c of the external product for CMUX i: decompose (X^a - 1) * acc_c, then for each
+// level l (global step g = 6i + 3c + l) accumulate NTT(digits) (.) BSK_i[(c, l)][j] into out_j.
+__device__ __forceinline__ void ext_prod_component_wg(const u64 (&acc)[16], int a, int c, int i, int n_steps,
+                                                      BrShared& sh, u64* T, int wave, int lane,
+                                                      const u64* __restrict__ bsk, u64 (&out0)[16],
+                                                      u64 (&out1)[16]) {
 #pragma unroll
   for (int e = 0; e < 16; e++) T[64 * e + lane] = acc[e];
-  __syncthreads();
+  wave_lds_sync();
   u32 dig[16];
 #pragma unroll
   for (int e = 0; e < 16; e++) dig[e] = decomp_7x3(gl_sub(rot_read(T, 64 * e + lane, a), acc[e]));
-  __syncthreads();
+  wave_lds_sync();
 #pragma unroll 1
   for (int l = 0; l < 3; l++) {
+    const int g = i * 6 + c * 3 + l;
+    // chunk g has landed (every wave drained its glds: __syncthreads waits vmcnt(0)) and every wave
+    // is done reading buffer (g+1)&1 (step g-1): refill it with chunk g+1
+    __syncthreads();
+    if (g + 1 < n_steps) load_chunk(bsk, g + 1, sh.K[(g + 1) & 1], wave, lane);
     u64 x[16];
-#pragma unroll
-    for (int e = 0; e < 16; e++) x[e] = gl_from_i32((int)((dig[e] >> (8 * l)) & 0xFFu) - 64);
-    ntt1024_fwd(x, T, lane, twf);
-    const u64* k0 = bsk_i + (size_t)((c * 3 + l) * 2 + 0) * N1K + lane;
-    const u64* k1 = bsk_i + (size_t)((c * 3 + l) * 2 + 1) * N1K + lane;
+    ntt1024_fwd_digits_lds(dig, l, x, T, lane, sh.tw[0]);
+    const u64* k0 = sh.K[g & 1] + lane;
+    const u64* k1 = sh.K[g & 1] + N1K + lane;
 #pragma unroll
     for (int e = 0; e < 16; e++) {
       out0[e] = gl_add(out0[e], gl_mul(x[e], k0[64 * e]));
@@ -166,16 +262,25 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int a, 
   }
 }
 
-// Blind rotation + sample extraction.  One wavefront (= one block) per ciphertext.
 template <bool WRITE_ACC, bool WRITE_BIG>
-__global__ __launch_bounds__(64, 2) void blind_rotate_kernel(
-    const u64* __restrict__ lwe_in, int n, const u64* __restrict__ luts, const u32* __restrict__ lut_index, int n_lut,
-    const u64* __restrict__ bsk, const u64* __restrict__ twf, const u64* __restrict__ twi, u64* __restrict__ out_big,
-    u64* __restrict__ out_acc) {
-  __shared__ __attribute__((aligned(16))) u64 T[T_LDS];
-  const int lane = threadIdx.x;
-  const size_t b = blockIdx.x;
+__global__ __launch_bounds__(BR_THREADS, 1) void blind_rotate_kernel(
+    const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
+    int n_lut, const u64* __restrict__ bsk, const u64* __restrict__ twf, const u64* __restrict__ twi,
+    u64* __restrict__ out_big, u64* __restrict__ out_acc) {
+  __shared__ __attribute__((aligned(16))) BrShared sh;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t b_raw = (size_t)blockIdx.x * BR_WAVES + wave;
+  const bool live = b_raw < B;
+  const size_t b = live ? b_raw : B - 1;  // padding waves run a copy of the last ciphertext, store nothing
   const u64* ct = lwe_in + b * (size_t)(n + 1);
+  u64* T = sh.T[wave];
+  const int n_steps = n * 6;
+
+  for (int q = threadIdx.x; q < N1K; q += BR_THREADS) {
+    sh.tw[0][q] = twf[q];
+    sh.tw[1][q] = twi[q];
+  }
+  load_chunk(bsk, 0, sh.K[0], wave, lane);
 
   // acc = (0, X^{-b~} * lut)
   u64 accA[16], accB[16];
@@ -191,23 +296,24 @@ __global__ __launch_bounds__(64, 2) void blind_rotate_kernel(
     }
   }
 
+  // No per-ciphertext skip of a~_i == 0 steps: the workgroup walks the loop in lockstep; such a
+  // step decomposes 0 and adds exactly 0, so the result is bit-identical.
   for (int i = 0; i < n; i++) {
     const int a = ms2048(ct[i]);
-    if (a == 0) continue;  // (X^0 - 1) * acc == 0: the CMUX is the identity (wave-uniform branch)
-    const u64* bsk_i = bsk + (size_t)i * (12 * N1K);
     u64 out0[16], out1[16];
 #pragma unroll
     for (int e = 0; e < 16; e++) { out0[e] = 0; out1[e] = 0; }
-    ext_prod_component(accA, a, 0, T, lane, bsk_i, twf, out0, out1);
-    ext_prod_component(accB, a, 1, T, lane, bsk_i, twf, out0, out1);
-    ntt1024_inv(out0, T, lane, twi);
+    ext_prod_component_wg(accA, a, 0, i, n_steps, sh, T, wave, lane, bsk, out0, out1);
+    ext_prod_component_wg(accB, a, 1, i, n_steps, sh, T, wave, lane, bsk, out0, out1);
+    ntt1024_inv_lds(out0, T, lane, sh.tw[1]);
 #pragma unroll
     for (int e = 0; e < 16; e++) accA[e] = gl_add(accA[e], out0[e]);
-    ntt1024_inv(out1, T, lane, twi);
+    ntt1024_inv_lds(out1, T, lane, sh.tw[1]);
 #pragma unroll
     for (int e = 0; e < 16; e++) accB[e] = gl_add(accB[e], out1[e]);
   }
 
+  if (!live) return;
   if (WRITE_ACC) {
     u64* oa = out_acc + b * 2048;
 #pragma unroll
@@ -348,16 +454,16 @@ hipError_t launch_blind_rotate(const u64* lwe_in, size_t B, int n, const u64* lu
                                const u64* bsk, const u64* twf, const u64* twi, u64* out_big, u64* out_acc,
                                hipStream_t s) {
   if (B == 0) return hipSuccess;
-  dim3 grid((unsigned)B), block(64);
+  dim3 grid((unsigned)((B + BR_WAVES - 1) / BR_WAVES)), block(BR_THREADS);
   if (out_acc && out_big)
-    hipLaunchKernelGGL((blind_rotate_kernel<true, true>), grid, block, 0, s, lwe_in, n, luts, lut_index, n_lut, bsk,
+    hipLaunchKernelGGL((blind_rotate_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index, n_lut, bsk,
                        twf, twi, out_big, out_acc);
   else if (out_acc)
-    hipLaunchKernelGGL((blind_rotate_kernel<true, false>), grid, block, 0, s, lwe_in, n, luts, lut_index, n_lut, bsk,
-                       twf, twi, out_big, out_acc);
+    hipLaunchKernelGGL((blind_rotate_kernel<true, false>), grid, block, 0, s, lwe_in, n, B, luts, lut_index, n_lut,
+                       bsk, twf, twi, out_big, out_acc);
   else
-    hipLaunchKernelGGL((blind_rotate_kernel<false, true>), grid, block, 0, s, lwe_in, n, luts, lut_index, n_lut, bsk,
-                       twf, twi, out_big, out_acc);
+    hipLaunchKernelGGL((blind_rotate_kernel<false, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index, n_lut,
+                       bsk, twf, twi, out_big, out_acc);
   return hipGetLastError();
 }
 
