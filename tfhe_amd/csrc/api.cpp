@@ -12,7 +12,6 @@
 #include "../../include/tfhe_hip.h"
 #include "client.h"
 #include "gl64.h"
-#include "ntt32.h"
 #include "pbs_kernels.h"
 
 using tfhe::u64;
@@ -75,8 +74,7 @@ struct tfhe_ctx {
   hipStream_t stream = nullptr;
   u64* d_bsk = nullptr;  // NTT layout, x N^-1
   u64* d_ksk = nullptr;
-  u64* d_twf = nullptr;  // 1024 forward twiddles (R16 layout)
-  u64* d_twi = nullptr;
+  u64* d_tw = nullptr;  // 4 x 1024 twiddle tables of the device NTT layout
   u64 ninv = 0;
   bool keys = false;
   // workspaces
@@ -156,8 +154,8 @@ int pbs_device(tfhe_ctx* c, const u64* d_in, size_t B, const u64* d_luts, size_t
   int rc = grow((void**)&c->d_big, &c->big_cap, B * big * sizeof(u64));
   if (rc) return rc;
   timed_begin(c, 0, s);
-  HIP_TRY(tfhe::launch_blind_rotate(d_in, B, (int)c->p.n, d_luts, d_idx, (int)n_lut, c->d_bsk, c->d_twf, c->d_twi,
-                                    c->d_big, nullptr, s));
+  HIP_TRY(tfhe::launch_blind_rotate(d_in, B, (int)c->p.n, d_luts, d_idx, (int)n_lut, c->d_bsk, c->d_tw, c->d_big,
+                                    nullptr, s));
   timed_end(c, 0, s);
   timed_begin(c, 1, s);
   HIP_TRY(tfhe::launch_keyswitch(c->d_big, B, (int)(c->p.k * c->p.N), c->d_ksk, (int)c->p.n, d_out, s));
@@ -270,23 +268,15 @@ int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out) {
   };
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail(TFHE_HIP_EDEVICE, "create: hipStreamCreate failed"));
-  // twiddles, R16 layout: element (lane L, e) <-> m = 2e + (L >> 5), i2 = L & 31
+  // twiddle tables of the device NTT layout (pbs_kernels.hip: make_ntt_tables)
   using namespace tfhe;
   const uint32_t N = p->N;
-  const u64 psi = canonical_psi(N), psi_inv = gl_pow(psi, GL_P - 2);
-  std::vector<u64> twf(N), twi(N);
-  for (int L = 0; L < 64; L++)
-    for (int e = 0; e < 16; e++) {
-      const int m = 2 * e + (L >> 5), i2 = L & 31;
-      const u64 ex = (u64)i2 * (2 * brv5(m) + 1);
-      twf[64 * e + L] = gl_pow(psi, ex);
-      twi[64 * e + L] = gl_pow(psi_inv, ex);
-    }
+  std::vector<u64> tw(4 * N);
+  make_ntt_tables(canonical_psi(N), tw.data());
   c->ninv = gl_pow(N, GL_P - 2);
-  if (hipMalloc(&c->d_twf, N * 8) != hipSuccess || hipMalloc(&c->d_twi, N * 8) != hipSuccess)
+  if (hipMalloc(&c->d_tw, tw.size() * 8) != hipSuccess)
     return cleanup(fail(TFHE_HIP_ENOMEM, "create: twiddle allocation failed"));
-  if (hipMemcpy(c->d_twf, twf.data(), N * 8, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(c->d_twi, twi.data(), N * 8, hipMemcpyHostToDevice) != hipSuccess)
+  if (hipMemcpy(c->d_tw, tw.data(), tw.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
     return cleanup(fail(TFHE_HIP_EDEVICE, "create: twiddle upload failed"));
   *out = c;
   return 0;
@@ -302,8 +292,7 @@ void tfhe_hip_destroy(tfhe_ctx* c) {
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     (void)hipFree(c->d_bsk);
     (void)hipFree(c->d_ksk);
-    (void)hipFree(c->d_twf);
-    (void)hipFree(c->d_twi);
+    (void)hipFree(c->d_tw);
     (void)hipFree(c->d_big);
     (void)hipFree(c->d_stage);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -336,7 +325,7 @@ static int load_keys_impl(tfhe_ctx* c, const uint64_t* bsk, size_t bsk_len, cons
     tmp = (void*)bsk;
   }
   const size_t polys = bsk_len / c->p.N;
-  HIP_TRY(tfhe::launch_bsk_to_ntt((const u64*)tmp, c->d_bsk, (int)(polys / 12), c->d_twf, c->ninv, c->stream));
+  HIP_TRY(tfhe::launch_bsk_to_ntt((const u64*)tmp, c->d_bsk, (int)(polys / 12), c->d_tw, c->ninv, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->keys = true;
   return 0;
@@ -400,7 +389,7 @@ int tfhe_hip_blind_rotate(tfhe_ctx* c, const uint64_t* lwe_in, size_t B, const u
                  B * acc_len * 8);
   if (rc) return rc;
   HIP_TRY(tfhe::launch_blind_rotate((const u64*)d[0], B, (int)c->p.n, (const u64*)d[1], (const u32*)d[2], (int)n_lut,
-                                    c->d_bsk, c->d_twf, c->d_twi, nullptr, (u64*)d[3], c->stream));
+                                    c->d_bsk, c->d_tw, nullptr, (u64*)d[3], c->stream));
   HIP_TRY(hipMemcpyAsync(acc_out, d[3], B * acc_len * 8, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return 0;
@@ -449,8 +438,8 @@ static int ntt_impl(tfhe_ctx* c, uint64_t* polys, size_t count, bool inverse) {
   std::vector<void*> d;
   int rc = stage(c, {{polys, bytes}}, d, 0);
   if (rc) return rc;
-  if (inverse) HIP_TRY(tfhe::launch_ntt_inv((u64*)d[0], count, c->d_twi, c->ninv, c->stream));
-  else HIP_TRY(tfhe::launch_ntt_fwd((u64*)d[0], count, c->d_twf, c->stream));
+  if (inverse) HIP_TRY(tfhe::launch_ntt_inv((u64*)d[0], count, c->d_tw, c->ninv, c->stream));
+  else HIP_TRY(tfhe::launch_ntt_fwd((u64*)d[0], count, c->d_tw, c->stream));
   HIP_TRY(hipMemcpyAsync(polys, d[0], bytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return 0;

@@ -5,7 +5,7 @@
 // reference's exact wrapping product); an NTT over this prime gives it with integer arithmetic,
 // so GPU == CPU oracle bit-for-bit.  2^64 == 2^32 - 1 and 2^96 == -1 (mod p), so reductions are
 // shifts/adds, and every 64th / 32nd root of unity is a power of two (2^3, 2^6): the 32-point
-// sub-transforms of the NTT need no multiplies at all (see ntt32.h).
+// sub-transforms of the NTT need no multiplies at all (see ntt16.h).
 //
 // All functions return canonical values in [0, p) given canonical inputs (gl_reduce128 and
 // gl_mul accept any 64-bit words).

@@ -1,30 +1,31 @@
 // pbs_kernels.hip — gfx950 kernels of the PBS hot path (P-GATE: n=630, k=1, N=1024, 7x3, KS 2x8).
 //
 //   bsk_to_ntt      standard-domain BSK -> device NTT layout (x N^-1), once per key load
-//   blind_rotate    the CMUX loop: one wavefront owns one ciphertext for all n iterations;
-//                   decompose -> 32x32 NTT (in registers + one LDS transpose) -> GGSW MAC with the
-//                   BSK row streamed from L2/HBM -> inverse NTT -> accumulate; sample extract and the
-//                   Z_p -> 2^64 switch are fused into the epilogue
+//   blind_rotate    the CMUX loop: 8 wavefronts (8 ciphertexts) per workgroup walk the loop in
+//                   lockstep; per CMUX: decompose -> NTT (in registers, 2 LDS transposes) ->
+//                   GGSW MAC with the BSK chunk streamed once per workgroup into LDS -> inverse
+//                   NTT -> accumulate; sample extract + Z_p -> 2^64 fused in the epilogue
 //   keyswitch       batched LWE keyswitch kN -> n (64 ciphertexts x 64 columns per workgroup)
 //   ntt_fwd/inv     natural-order NTT over the same device routines (parity tests of the NTT)
 //   sample_extract  stage-level entry point (the fused epilogue's twin)
 //
-// Register layout ("R16"): one wavefront processes one polynomial at a time; lane L holds the 16
-// coefficients {64*e + L : e < 16}.  In the NTT domain lane L = 32*s + m, element e holds
-// A^[brv5(m) + 32*brv5(2e + s)].  A ciphertext's accumulator (2 polys), the two external-product
-// outputs (2 polys), one working polynomial and its packed digits all stay in VGPRs (~210/lane,
-// 2 waves per SIMD); LDS holds only the 8.4 KB transpose / rotation scratch of each wavefront.
+// Register layout: one wavefront processes one polynomial at a time, 16 u64 per lane.
+//   natural (coefficient) layout: lane L, element e  <->  coefficient 64 e + L
+//   NTT layout (after ntt1024_fwd): lane L, element e <-> A^[ntt_natural_index(L, e)]
+// A ciphertext's accumulator (2 polys), the two external-product outputs (2 polys), one working
+// polynomial and its packed digits stay in VGPRs (256/lane, 2 waves per SIMD).
 #include <hip/hip_runtime.h>
 
 #include "gl64.h"
-#include "ntt32.h"
+#include "ntt16.h"
 #include "pbs_kernels.h"
 
 namespace tfhe {
 
 constexpr int N1K = 1024;
-constexpr int TSTRIDE = 33;            // LDS row stride (u64) of the 32x32 transpose: conflict-free
-constexpr int T_LDS = 32 * TSTRIDE;    // u64 of LDS scratch per wavefront (>= 1024 natural layout)
+constexpr int T1_STRIDE = 68;              // transpose-1 row stride (u64): conflict-free reads/writes
+constexpr int T_LDS = 16 * T1_STRIDE;      // u64 of LDS scratch per wavefront (>= 1024)
+constexpr int TW_U64 = 4 * N1K;            // twiddle tables: tw1 fwd, tw2 fwd, tw1 inv, tw2 inv
 
 // round(x * 2048 / 2^64) mod 2048  (modulus switch)
 __device__ __forceinline__ int ms2048(u64 x) { return (int)((((x >> 52) + 1) >> 1) & 2047u); }
@@ -56,83 +57,93 @@ __device__ __forceinline__ u32 decomp_7x3(u64 x) {
   return packed;
 }
 
-// Cross-lane pair exchange with v_permlane32_swap: with both operands = v, every lane receives
-// (u, w) = (value of lane L & 31, value of lane (L & 31) + 32) — the two inputs of the pair's
-// butterfly — with no selects and no LDS round trip (ds_bpermute).
-__device__ __forceinline__ void pair_values(u64 v, u64& lo, u64& hi) {
-  const u32 v0 = (u32)v, v1 = (u32)(v >> 32);
-  const auto r0 = __builtin_amdgcn_permlane32_swap(v0, v0, false, false);
-  const auto r1 = __builtin_amdgcn_permlane32_swap(v1, v1, false, false);
-  lo = (u64)r0[0] | ((u64)r1[0] << 32);
-  hi = (u64)r0[1] | ((u64)r1[1] << 32);
+// Ordering of one wavefront's own LDS writes before its reads of another lane's data (LDS runs a
+// wave's operations in order; this stops the compiler moving them and retires the writes).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// span-1 stage of the 32-point transform: positions (2e, 2e+1) live on lanes (L, L^32).
-// Lane half 0 keeps u + t, half 1 keeps u - t, t = zeta * v: computed as u + (+-t).
-template <int KIND>
-__device__ __forceinline__ void fwd_cross(u64 (&x)[16], bool hi) {
+// ---------------------------------------------------------------------------------------------
+// 1024-point negacyclic NTT of the wavefront's polynomial (ntt16.h for the factorization).
+// tw points at the 4 tables [tw1 fwd | tw2 fwd | tw1 inv | tw2 inv] (LDS or global).
+// Transpose 1: lane L, slot e -> T[e][L] (stride 68) -> lane (e1 = L >> 2, i3 = L & 3) reads
+//              T[e1][4 e2 + i3].  Transpose 2: lane L2, slot f -> T[f][L2 ^ (f >> 2 & 3)]
+//              (XOR swizzle) -> lane (e1, fhi = L & 3) reads element 4 flo + i3 from
+//              T[4 fhi + flo][(4 e1 + i3) ^ fhi].  Both are bank-conflict free.
+__device__ __forceinline__ void ntt1024_fwd_tail(u64 (&x)[16], u64* T, int lane, const u64* tw) {
+  const int e1 = lane >> 2, q = lane & 3;
 #pragma unroll
-  for (int e = 0; e < 16; e++) {
-    u64 u, v;
-    pair_values(x[e], u, v);
-    const u64 t = gl_mul_pow2(v, zeta_exp<KIND>(16 + e));
-    x[e] = gl_add(u, hi ? gl_neg(t) : t);
+  for (int e = 0; e < 16; e++) x[e] = gl_mul(x[e], tw[64 * e + lane]);
+#pragma unroll
+  for (int e = 0; e < 16; e++) T[e * T1_STRIDE + lane] = x[e];
+  wave_lds_sync();
+#pragma unroll
+  for (int e = 0; e < 16; e++) x[e] = T[e1 * T1_STRIDE + 4 * e + q];
+  wave_lds_sync();
+  cyc16_fwd(x);
+#pragma unroll
+  for (int f = 0; f < 16; f++) x[f] = gl_mul(x[f], tw[N1K + 64 * f + lane]);
+#pragma unroll
+  for (int f = 0; f < 16; f++) T[f * 64 + (lane ^ ((f >> 2) & 3))] = x[f];
+  wave_lds_sync();
+#pragma unroll
+  for (int e = 0; e < 16; e++) x[e] = T[(4 * q + (e >> 2)) * 64 + ((4 * e1 + (e & 3)) ^ q)];
+  wave_lds_sync();
+  cyc4x4_fwd(x);
+}
+
+__device__ __forceinline__ void ntt1024_fwd(u64 (&x)[16], u64* T, int lane, const u64* tw) {
+  nega16_fwd(x);
+  ntt1024_fwd_tail(x, T, lane, tw);
+}
+
+// Forward NTT of a digit polynomial (|d| <= 64, byte l of dig[e] holds d + 64): the first
+// pass-1 stage (span 8, twiddle 2^48) is exact in int64 (|d + 2^48 d'| < 2^55): no reduction.
+__device__ __forceinline__ void ntt1024_fwd_digits(const u32 (&dig)[16], int l, u64 (&x)[16], u64* T, int lane,
+                                                   const u64* tw) {
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const long long u = (long long)((dig[e] >> (8 * l)) & 0xFFu) - 64;
+    const long long w = ((long long)((dig[e + 8] >> (8 * l)) & 0xFFu) - 64) * (1ll << 48);
+    const long long a = u + w, b = u - w;
+    x[e] = (u64)a + (a < 0 ? GL_P : 0ull);
+    x[e + 8] = (u64)b + (b < 0 ? GL_P : 0ull);
   }
+  nega16_fwd_from4(x);
+  ntt1024_fwd_tail(x, T, lane, tw);
 }
 
-template <int KIND>
-__device__ __forceinline__ void inv_cross(u64 (&x)[16], bool hi) {
+// Inverse, x 1024 (the 1/N is folded into the BSK): NTT layout in, natural layout out.
+__device__ __forceinline__ void ntt1024_inv(u64 (&x)[16], u64* T, int lane, const u64* tw) {
+  const int e1 = lane >> 2, q = lane & 3;
+  cyc4x4_inv(x);
 #pragma unroll
-  for (int e = 0; e < 16; e++) {
-    u64 U, V;
-    pair_values(x[e], U, V);
-    x[e] = hi ? gl_mul_pow2(gl_sub(U, V), 192 - zeta_exp<KIND>(16 + e)) : gl_add(U, V);
-  }
+  for (int e = 0; e < 16; e++) T[(4 * q + (e >> 2)) * 64 + ((4 * e1 + (e & 3)) ^ q)] = x[e];
+  wave_lds_sync();
+#pragma unroll
+  for (int f = 0; f < 16; f++) x[f] = T[f * 64 + (lane ^ ((f >> 2) & 3))];
+  wave_lds_sync();
+#pragma unroll
+  for (int f = 0; f < 16; f++) x[f] = gl_mul(x[f], tw[3 * N1K + 64 * f + lane]);
+  cyc16_inv(x);
+#pragma unroll
+  for (int e = 0; e < 16; e++) T[e1 * T1_STRIDE + 4 * e + q] = x[e];
+  wave_lds_sync();
+#pragma unroll
+  for (int e = 0; e < 16; e++) x[e] = T[e * T1_STRIDE + lane];
+  wave_lds_sync();
+#pragma unroll
+  for (int e = 0; e < 16; e++) x[e] = gl_mul(x[e], tw[2 * N1K + 64 * e + lane]);
+  nega16_inv(x);
 }
 
-// Forward negacyclic NTT of the wavefront's polynomial: natural layout in, NTT layout out.
-__device__ __forceinline__ void ntt1024_fwd(u64 (&x)[16], u64* T, int lane, const u64* twf) {
-  asm volatile("" : "+s"(twf));  // keep the twiddle loads inside the CMUX loop (no LICM: saves 32 VGPRs)
-  const bool hi = lane >= 32;
-  const int c = lane & 31, s = lane >> 5;
-  fwd_inlane16<NEGA>(x);
-  fwd_cross<NEGA>(x, hi);
-#pragma unroll
-  for (int e = 0; e < 16; e++) x[e] = gl_mul(x[e], twf[64 * e + lane]);
-#pragma unroll
-  for (int e = 0; e < 16; e++) T[(2 * e + s) * TSTRIDE + c] = x[e];
-  __syncthreads();
-#pragma unroll
-  for (int e = 0; e < 16; e++) x[e] = T[c * TSTRIDE + 2 * e + s];
-  __syncthreads();
-  fwd_inlane16<CYC>(x);
-  fwd_cross<CYC>(x, hi);
-}
-
-// Inverse (x 1024; the 1/N is folded into the BSK): NTT layout in, natural layout out.
-__device__ __forceinline__ void ntt1024_inv(u64 (&x)[16], u64* T, int lane, const u64* twi) {
-  asm volatile("" : "+s"(twi));  // keep the twiddle loads inside the CMUX loop (no LICM: saves 32 VGPRs)
-  const bool hi = lane >= 32;
-  const int c = lane & 31, s = lane >> 5;
-  inv_cross<CYC>(x, hi);
-  inv_inlane16<CYC>(x);
-#pragma unroll
-  for (int e = 0; e < 16; e++) T[c * TSTRIDE + 2 * e + s] = x[e];
-  __syncthreads();
-#pragma unroll
-  for (int e = 0; e < 16; e++) x[e] = T[(2 * e + s) * TSTRIDE + c];
-  __syncthreads();
-#pragma unroll
-  for (int e = 0; e < 16; e++) x[e] = gl_mul(x[e], twi[64 * e + lane]);
-  inv_cross<NEGA>(x, hi);
-  inv_inlane16<NEGA>(x);
-}
-
-// ------------------------------------------------------------------------------------------
-// BSK conversion: one wavefront per polynomial (i, r, j); device layout [i][r][j][e][L] — the same
-// polynomial order as the standard layout, each polynomial in NTT layout, scaled by N^-1.
+// ---------------------------------------------------------------------------------------------
+// BSK conversion: one wavefront per polynomial (i, r, j); device layout [i][r][j][e][L] — the
+// standard layout's polynomial order, each polynomial in NTT layout, scaled by N^-1.
 __global__ __launch_bounds__(64) void bsk_to_ntt_kernel(const u64* __restrict__ bsk_std, u64* __restrict__ bsk_ntt,
-                                                        const u64* __restrict__ twf, u64 ninv) {
+                                                        const u64* __restrict__ tw, u64 ninv) {
   __shared__ __attribute__((aligned(16))) u64 T[T_LDS];
   const int lane = threadIdx.x;
   const size_t q = blockIdx.x;
@@ -140,13 +151,13 @@ __global__ __launch_bounds__(64) void bsk_to_ntt_kernel(const u64* __restrict__ 
   u64 x[16];
 #pragma unroll
   for (int e = 0; e < 16; e++) x[e] = src[64 * e + lane];
-  ntt1024_fwd(x, T, lane, twf);
+  ntt1024_fwd(x, T, lane, tw);
   u64* dst = bsk_ntt + q * N1K;
 #pragma unroll
   for (int e = 0; e < 16; e++) dst[64 * e + lane] = gl_mul(x[e], ninv);
 }
 
-// ------------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------------
 // Blind rotation + sample extraction.
 //
 // A workgroup = BR_WAVES wavefronts = BR_WAVES ciphertexts that walk the CMUX loop in lockstep.
@@ -154,27 +165,18 @@ __global__ __launch_bounds__(64) void bsk_to_ntt_kernel(const u64* __restrict__ 
 // columns j: 16 KB contiguous in the device layout).  Each step's chunk is streamed ONCE per
 // workgroup into LDS with global_load_lds (16 B/lane, lane-linear image), double-buffered: chunk
 // g+1 is in flight while step g computes, so the MAC reads BSK from LDS instead of waiting on L2 /
-// MALL latency with only 2 waves per SIMD (ablation: the register-streamed MAC took 1/3 of the
-// kernel).  Twiddles are LDS-resident too.  Per wavefront LDS: the 8.4 KB transpose/rotation
-// scratch.  Total 114 KB -> one workgroup (8 waves, 2 per SIMD) per CU.
+// MALL latency with only 2 waves per SIMD.  Twiddles are LDS-resident.  Per wavefront LDS: the
+// 8.7 KB transpose/rotation scratch.  Total 134 KB -> one workgroup (8 waves, 2/SIMD) per CU.
 constexpr int BR_WAVES = 8;
 constexpr int BR_THREADS = 64 * BR_WAVES;
-constexpr int CHUNK_U64 = 2 * N1K;                 // one level step: rows (c,l), j = 0,1
-constexpr int CHUNK_GLDS = CHUNK_U64 * 8 / 1024;   // 1 KB wave-instructions per chunk (16)
+constexpr int CHUNK_U64 = 2 * N1K;                // one level step: rows (c,l), j = 0,1
+constexpr int CHUNK_GLDS = CHUNK_U64 * 8 / 1024;  // 1 KB wave-instructions per chunk (16)
 
 struct BrShared {
-  u64 T[BR_WAVES][T_LDS];        // per-wave transpose / rotation scratch
-  u64 K[2][CHUNK_U64];           // double-buffered BSK chunk
-  u64 tw[2][N1K];                // forward / inverse twiddles
+  u64 T[BR_WAVES][T_LDS];  // per-wave transpose / rotation scratch
+  u64 K[2][CHUNK_U64];     // double-buffered BSK chunk
+  u64 tw[TW_U64];          // twiddle tables
 };
-
-// ordering of one wavefront's own LDS writes before its reads (LDS executes a wave's ops in order;
-// this only stops the compiler from moving them and waits for the writes to retire)
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // issue this wave's share of chunk g (2 x 1 KB) into buffer dst
 __device__ __forceinline__ void load_chunk(const u64* __restrict__ bsk, int g, u64* dst, int wave, int lane) {
@@ -187,55 +189,11 @@ __device__ __forceinline__ void load_chunk(const u64* __restrict__ bsk, int g, u
   }
 }
 
-__device__ __forceinline__ void ntt1024_fwd_digits_lds(const u32 (&dig)[16], int l, u64 (&x)[16], u64* T, int lane,
-                                                       const u64* tw) {
-  const bool hi = lane >= 32;
-  const int c = lane & 31, s = lane >> 5;
-#pragma unroll
-  for (int e = 0; e < 8; e++) {
-    const long long u = (long long)((dig[e] >> (8 * l)) & 0xFFu) - 64;
-    const long long w = ((long long)((dig[e + 8] >> (8 * l)) & 0xFFu) - 64) * (1ll << 48);
-    const long long a = u + w, b = u - w;
-    x[e] = (u64)a + (a < 0 ? GL_P : 0ull);
-    x[e + 8] = (u64)b + (b < 0 ? GL_P : 0ull);
-  }
-  fwd_inlane16_from<NEGA, 8>(x);
-  fwd_cross<NEGA>(x, hi);
-#pragma unroll
-  for (int e = 0; e < 16; e++) x[e] = gl_mul(x[e], tw[64 * e + lane]);
-#pragma unroll
-  for (int e = 0; e < 16; e++) T[(2 * e + s) * TSTRIDE + c] = x[e];
-  wave_lds_sync();
-#pragma unroll
-  for (int e = 0; e < 16; e++) x[e] = T[c * TSTRIDE + 2 * e + s];
-  wave_lds_sync();
-  fwd_inlane16<CYC>(x);
-  fwd_cross<CYC>(x, hi);
-}
-
-__device__ __forceinline__ void ntt1024_inv_lds(u64 (&x)[16], u64* T, int lane, const u64* tw) {
-  const bool hi = lane >= 32;
-  const int c = lane & 31, s = lane >> 5;
-  inv_cross<CYC>(x, hi);
-  inv_inlane16<CYC>(x);
-#pragma unroll
-  for (int e = 0; e < 16; e++) T[c * TSTRIDE + 2 * e + s] = x[e];
-  wave_lds_sync();
-#pragma unroll
-  for (int e = 0; e < 16; e++) x[e] = T[(2 * e + s) * TSTRIDE + c];
-  wave_lds_sync();
-#pragma unroll
-  for (int e = 0; e < 16; e++) x[e] = gl_mul(x[e], tw[64 * e + lane]);
-  inv_cross<NEGA>(x, hi);
-  inv_inlane16<NEGA>(x);
-}
-
 // One component c of the external product for CMUX i: decompose (X^a - 1) * acc_c, then for each
 // level l (global step g = 6i + 3c + l) accumulate NTT(digits) (.) BSK_i[(c, l)][j] into out_j.
-__device__ __forceinline__ void ext_prod_component_wg(const u64 (&acc)[16], int a, int c, int i, int n_steps,
-                                                      BrShared& sh, u64* T, int wave, int lane,
-                                                      const u64* __restrict__ bsk, u64 (&out0)[16],
-                                                      u64 (&out1)[16]) {
+__device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int a, int c, int i, int n_steps,
+                                                   BrShared& sh, u64* T, int wave, int lane,
+                                                   const u64* __restrict__ bsk, u64 (&out0)[16], u64 (&out1)[16]) {
 #pragma unroll
   for (int e = 0; e < 16; e++) T[64 * e + lane] = acc[e];
   wave_lds_sync();
@@ -251,7 +209,7 @@ __device__ __forceinline__ void ext_prod_component_wg(const u64 (&acc)[16], int 
     __syncthreads();
     if (g + 1 < n_steps) load_chunk(bsk, g + 1, sh.K[(g + 1) & 1], wave, lane);
     u64 x[16];
-    ntt1024_fwd_digits_lds(dig, l, x, T, lane, sh.tw[0]);
+    ntt1024_fwd_digits(dig, l, x, T, lane, sh.tw);
     const u64* k0 = sh.K[g & 1] + lane;
     const u64* k1 = sh.K[g & 1] + N1K + lane;
 #pragma unroll
@@ -265,8 +223,8 @@ __device__ __forceinline__ void ext_prod_component_wg(const u64 (&acc)[16], int 
 template <bool WRITE_ACC, bool WRITE_BIG>
 __global__ __launch_bounds__(BR_THREADS, 1) void blind_rotate_kernel(
     const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
-    int n_lut, const u64* __restrict__ bsk, const u64* __restrict__ twf, const u64* __restrict__ twi,
-    u64* __restrict__ out_big, u64* __restrict__ out_acc) {
+    int n_lut, const u64* __restrict__ bsk, const u64* __restrict__ tw_g, u64* __restrict__ out_big,
+    u64* __restrict__ out_acc) {
   __shared__ __attribute__((aligned(16))) BrShared sh;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t b_raw = (size_t)blockIdx.x * BR_WAVES + wave;
@@ -276,10 +234,7 @@ __global__ __launch_bounds__(BR_THREADS, 1) void blind_rotate_kernel(
   u64* T = sh.T[wave];
   const int n_steps = n * 6;
 
-  for (int q = threadIdx.x; q < N1K; q += BR_THREADS) {
-    sh.tw[0][q] = twf[q];
-    sh.tw[1][q] = twi[q];
-  }
+  for (int q = threadIdx.x; q < TW_U64; q += BR_THREADS) sh.tw[q] = tw_g[q];
   load_chunk(bsk, 0, sh.K[0], wave, lane);
 
   // acc = (0, X^{-b~} * lut)
@@ -303,12 +258,12 @@ __global__ __launch_bounds__(BR_THREADS, 1) void blind_rotate_kernel(
     u64 out0[16], out1[16];
 #pragma unroll
     for (int e = 0; e < 16; e++) { out0[e] = 0; out1[e] = 0; }
-    ext_prod_component_wg(accA, a, 0, i, n_steps, sh, T, wave, lane, bsk, out0, out1);
-    ext_prod_component_wg(accB, a, 1, i, n_steps, sh, T, wave, lane, bsk, out0, out1);
-    ntt1024_inv_lds(out0, T, lane, sh.tw[1]);
+    ext_prod_component(accA, a, 0, i, n_steps, sh, T, wave, lane, bsk, out0, out1);
+    ext_prod_component(accB, a, 1, i, n_steps, sh, T, wave, lane, bsk, out0, out1);
+    ntt1024_inv(out0, T, lane, sh.tw);
 #pragma unroll
     for (int e = 0; e < 16; e++) accA[e] = gl_add(accA[e], out0[e]);
-    ntt1024_inv_lds(out1, T, lane, sh.tw[1]);
+    ntt1024_inv(out1, T, lane, sh.tw);
 #pragma unroll
     for (int e = 0; e < 16; e++) accB[e] = gl_add(accB[e], out1[e]);
   }
@@ -336,7 +291,7 @@ __global__ __launch_bounds__(BR_THREADS, 1) void blind_rotate_kernel(
   }
 }
 
-// ------------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------------
 __global__ void sample_extract_kernel(const u64* __restrict__ acc, size_t B, u64* __restrict__ out) {
   const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * (N1K + 1)) return;
@@ -350,7 +305,7 @@ __global__ void sample_extract_kernel(const u64* __restrict__ acc, size_t B, u64
   out[gid] = gl_to_torus(v);
 }
 
-// ------------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------------
 // Keyswitch kN -> n, base 2^2 x 8 levels (tfhe-rs SignedDecomposer digits in {-2..2}).
 // Workgroup = 64 output columns x 64 ciphertexts; wave w owns ciphertexts 16w..16w+15 of the tile.
 constexpr int KS_LEVELS = 8;
@@ -416,54 +371,67 @@ __global__ __launch_bounds__(256) void keyswitch_kernel(const u64* __restrict__ 
   }
 }
 
-// ------------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------------
 // Natural-order NTT over the device routines (one block = one polynomial).
-__global__ __launch_bounds__(64) void ntt_fwd_kernel(u64* __restrict__ polys, const u64* __restrict__ twf) {
+__global__ __launch_bounds__(64) void ntt_fwd_kernel(u64* __restrict__ polys, const u64* __restrict__ tw) {
   __shared__ __attribute__((aligned(16))) u64 T[T_LDS];
   const int lane = threadIdx.x;
   u64* p = polys + (size_t)blockIdx.x * N1K;
   u64 x[16];
 #pragma unroll
   for (int e = 0; e < 16; e++) x[e] = p[64 * e + lane];
-  ntt1024_fwd(x, T, lane, twf);
+  ntt1024_fwd(x, T, lane, tw);
 #pragma unroll
-  for (int e = 0; e < 16; e++) p[brv5(lane & 31) + 32 * brv5(2 * e + (lane >> 5))] = x[e];
+  for (int e = 0; e < 16; e++) p[ntt_natural_index(lane, e)] = x[e];
 }
 
-__global__ __launch_bounds__(64) void ntt_inv_kernel(u64* __restrict__ polys, const u64* __restrict__ twi, u64 ninv) {
+__global__ __launch_bounds__(64) void ntt_inv_kernel(u64* __restrict__ polys, const u64* __restrict__ tw, u64 ninv) {
   __shared__ __attribute__((aligned(16))) u64 T[T_LDS];
   const int lane = threadIdx.x;
   u64* p = polys + (size_t)blockIdx.x * N1K;
   u64 x[16];
 #pragma unroll
-  for (int e = 0; e < 16; e++) x[e] = p[brv5(lane & 31) + 32 * brv5(2 * e + (lane >> 5))];
+  for (int e = 0; e < 16; e++) x[e] = p[ntt_natural_index(lane, e)];
   __syncthreads();
-  ntt1024_inv(x, T, lane, twi);
+  ntt1024_inv(x, T, lane, tw);
 #pragma unroll
   for (int e = 0; e < 16; e++) p[64 * e + lane] = gl_mul(x[e], ninv);
 }
 
-// ------------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------------
+// host-side twiddle tables for the device NTT layout (4 x 1024 u64: tw1 fwd, tw2 fwd, tw1 inv, tw2 inv)
+void make_ntt_tables(u64 psi, u64* tw) {
+  const u64 psi_inv = gl_pow(psi, GL_P - 2), two_inv = gl_pow(2, GL_P - 2);
+  for (int e = 0; e < 16; e++)
+    for (int L = 0; L < 64; L++) {
+      const u64 e1x = (u64)L * (2 * brv4(e) + 1);  // tw1: psi^(i' (2 j1 + 1)), i' = L, j1 = brv4(e)
+      const u64 e2x = (u64)3 * (L & 3) * brv4(e);   // tw2: 2^(3 i3 j2), i3 = L & 3, j2 = brv4(f = e)
+      tw[64 * e + L] = gl_pow(psi, e1x);
+      tw[N1K + 64 * e + L] = gl_pow(2, e2x);
+      tw[2 * N1K + 64 * e + L] = gl_pow(psi_inv, e1x);
+      tw[3 * N1K + 64 * e + L] = gl_pow(two_inv, e2x);
+    }
+}
+
 // launchers
-hipError_t launch_bsk_to_ntt(const u64* bsk_std, u64* bsk_ntt, int n, const u64* twf, u64 ninv, hipStream_t s) {
-  hipLaunchKernelGGL(bsk_to_ntt_kernel, dim3((unsigned)n * 12), dim3(64), 0, s, bsk_std, bsk_ntt, twf, ninv);
+hipError_t launch_bsk_to_ntt(const u64* bsk_std, u64* bsk_ntt, int n, const u64* tw, u64 ninv, hipStream_t s) {
+  hipLaunchKernelGGL(bsk_to_ntt_kernel, dim3((unsigned)n * 12), dim3(64), 0, s, bsk_std, bsk_ntt, tw, ninv);
   return hipGetLastError();
 }
 
 hipError_t launch_blind_rotate(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index, int n_lut,
-                               const u64* bsk, const u64* twf, const u64* twi, u64* out_big, u64* out_acc,
-                               hipStream_t s) {
+                               const u64* bsk, const u64* tw, u64* out_big, u64* out_acc, hipStream_t s) {
   if (B == 0) return hipSuccess;
   dim3 grid((unsigned)((B + BR_WAVES - 1) / BR_WAVES)), block(BR_THREADS);
   if (out_acc && out_big)
     hipLaunchKernelGGL((blind_rotate_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index, n_lut, bsk,
-                       twf, twi, out_big, out_acc);
+                       tw, out_big, out_acc);
   else if (out_acc)
     hipLaunchKernelGGL((blind_rotate_kernel<true, false>), grid, block, 0, s, lwe_in, n, B, luts, lut_index, n_lut,
-                       bsk, twf, twi, out_big, out_acc);
+                       bsk, tw, out_big, out_acc);
   else
     hipLaunchKernelGGL((blind_rotate_kernel<false, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index, n_lut,
-                       bsk, twf, twi, out_big, out_acc);
+                       bsk, tw, out_big, out_acc);
   return hipGetLastError();
 }
 
@@ -481,15 +449,15 @@ hipError_t launch_keyswitch(const u64* in_big, size_t B, int big_dim, const u64*
   return hipGetLastError();
 }
 
-hipError_t launch_ntt_fwd(u64* polys, size_t count, const u64* twf, hipStream_t s) {
+hipError_t launch_ntt_fwd(u64* polys, size_t count, const u64* tw, hipStream_t s) {
   if (count == 0) return hipSuccess;
-  hipLaunchKernelGGL(ntt_fwd_kernel, dim3((unsigned)count), dim3(64), 0, s, polys, twf);
+  hipLaunchKernelGGL(ntt_fwd_kernel, dim3((unsigned)count), dim3(64), 0, s, polys, tw);
   return hipGetLastError();
 }
 
-hipError_t launch_ntt_inv(u64* polys, size_t count, const u64* twi, u64 ninv, hipStream_t s) {
+hipError_t launch_ntt_inv(u64* polys, size_t count, const u64* tw, u64 ninv, hipStream_t s) {
   if (count == 0) return hipSuccess;
-  hipLaunchKernelGGL(ntt_inv_kernel, dim3((unsigned)count), dim3(64), 0, s, polys, twi, ninv);
+  hipLaunchKernelGGL(ntt_inv_kernel, dim3((unsigned)count), dim3(64), 0, s, polys, tw, ninv);
   return hipGetLastError();
 }
 
