@@ -1,0 +1,482 @@
+"""Encrypted unsigned integers on the GPU gate bootstrap (the operator layer).
+
+An encrypted w-bit integer is w gate-encoded bits (true = +1/8, false = -1/8 of the 2^64 torus,
+LSB first) under the small LWE key.  Every gate is ONE keyswitch-PBS of a linear combination of
+ciphertexts with the constant LUT 1/8 (TFHE gate bootstrapping); negation is free.
+
+Operators are written as coroutines that ``yield`` one circuit LEVEL at a time (a list of arrays of
+linear combinations) and receive the bootstrapped arrays back.  ``Circuit.run_many`` steps any
+number of independent operator coroutines in lockstep and bootstraps the union of their levels in
+one ``Engine.pbs`` launch, so a set of requests costs max(depth) launches, not sum(depth) — the
+shape the GPU wants (a launch runs ~2k PBS in the time of one: SURVEY §8d).
+
+Semantics follow the fhEVM Solidity operators whose KATs the reference replays
+(tests/fhevm-suite/e2e/test/fhevmOperations*.ts, fixture tests/golden/fhevm_kats.json): wrapping
+add/sub/mul mod 2^w, two's-complement neg, bitwise and/or/xor/not, comparisons to an encrypted
+bool, unsigned min/max, shl/shr/rotl/rotr by (amount mod w), div/rem by a plaintext divisor
+(x/0 = all-ones, x%0 = x as tfhe-rs), plaintext operands on either side, and mixed widths
+zero-extended to the wider type.
+
+Gates (inputs ±1/8; every |phase| stays <= 3/8 so no combination wraps past 1/2):
+  AND  = PBS(a + b - 1/8)        OR  = PBS(a + b + 1/8)        XOR = PBS(2(a + b) + 1/4)
+  MAJ  = PBS(a + b + c)          XOR3 = PBS(-2(a + b + c))     NOT = -a,  XNOR = -XOR
+MAJ is the full-adder carry and also the parallel-prefix carry operator: with OR-type propagate
+(P = carry-out given carry-in 1, G = given carry-in 0, so G implies P)
+  (G, P)_hi o (G, P)_lo = (MAJ(G_hi, P_hi, G_lo), MAJ(G_hi, P_hi, P_lo)),
+so a Kogge-Stone adder is 1 + log2(w) + 1 levels.  Small batches (latency-bound) use it; batches
+that fill the GPU use the ripple adder (XOR3 + MAJ per bit, fewest PBS).
+"""
+from __future__ import annotations
+
+from typing import Generator, List, Sequence, Union
+
+import numpy as np
+
+from . import MU, ClientKey, Engine
+
+_M64 = 1 << 64
+WIDTHS = (8, 16, 32)
+
+
+# --------------------------------------------------------------------------------------------
+# linear combinations (all arithmetic mod 2^64, vectorised over any leading shape)
+# --------------------------------------------------------------------------------------------
+def _lin(terms, const: int = 0) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        out = None
+        for w, c in terms:
+            t = c * np.uint64(w % _M64)
+            out = t if out is None else out + t
+        out = np.array(out, dtype=np.uint64, copy=True)
+        out[..., -1] += np.uint64(const % _M64)
+    return out
+
+
+def AND(a, b):
+    return _lin([(1, a), (1, b)], -MU)
+
+
+def OR(a, b):
+    return _lin([(1, a), (1, b)], MU)
+
+
+def XOR(a, b):
+    return _lin([(2, a), (2, b)], 2 * MU)
+
+
+def MAJ(a, b, c):
+    return _lin([(1, a), (1, b), (1, c)])
+
+
+def XOR3(a, b, c):
+    return _lin([(-2, a), (-2, b), (-2, c)])
+
+
+def NOT(a):
+    with np.errstate(over="ignore"):
+        return (np.uint64(0) - a).astype(np.uint64)
+
+
+# --------------------------------------------------------------------------------------------
+# lockstep scheduler
+# --------------------------------------------------------------------------------------------
+Level = List[np.ndarray]
+Op = Generator[Level, List[np.ndarray], object]
+
+
+class Circuit:
+    """Runs operator coroutines on an Engine: every yielded level is one batched PBS launch."""
+
+    def __init__(self, engine: Engine, capacity: int = 2048):
+        self.engine = engine
+        self.dim = engine.params.n + 1
+        self.lut = engine.gate_lut()
+        self.capacity = capacity      # PBS one launch completes in ~one PBS latency (8 x 256 CUs)
+        self.pbs_count = 0
+        self.launches = 0
+
+    def trivial(self, bits) -> np.ndarray:
+        """Noise-free encryptions (0, ..., 0, ±1/8) of clear bits (plaintext operands)."""
+        bits = np.asarray(bits, dtype=bool)
+        out = np.zeros(bits.shape + (self.dim,), dtype=np.uint64)
+        out[..., -1] = np.where(bits, np.uint64(MU), np.uint64(_M64 - MU))
+        return out
+
+    def bootstrap(self, lins: Sequence[np.ndarray]) -> List[np.ndarray]:
+        shapes = [l.shape[:-1] for l in lins]
+        flat = np.concatenate([l.reshape(-1, self.dim) for l in lins], axis=0) if lins else \
+            np.zeros((0, self.dim), np.uint64)
+        if flat.shape[0]:
+            out = self.engine.pbs(flat, self.lut)
+            self.pbs_count += flat.shape[0]
+            self.launches += 1
+        else:
+            out = flat
+        res, off = [], 0
+        for s in shapes:
+            cnt = int(np.prod(s, dtype=np.int64))
+            res.append(out[off:off + cnt].reshape(s + (self.dim,)))
+            off += cnt
+        return res
+
+    def run(self, op: Op):
+        return self.run_many([op])[0]
+
+    def run_many(self, ops: Sequence[Op]) -> list:
+        results = [None] * len(ops)
+        pending = {}
+        for i, g in enumerate(ops):
+            try:
+                pending[i] = (g, next(g))
+            except StopIteration as e:
+                results[i] = e.value
+        while pending:
+            order = list(pending)
+            lins, counts = [], []
+            for i in order:
+                lvl = pending[i][1]
+                lins.extend(lvl)
+                counts.append(len(lvl))
+            outs = self.bootstrap(lins)
+            off = 0
+            for i, cnt in zip(order, counts):
+                g = pending[i][0]
+                try:
+                    pending[i] = (g, g.send(outs[off:off + cnt]))
+                except StopIteration as e:
+                    results[i] = e.value
+                    del pending[i]
+                off += cnt
+        return results
+
+    def prefer_prefix(self, batch: int, width: int) -> bool:
+        """Latency-bound (the level's PBS fit in one launch wave) -> log-depth prefix adder."""
+        return batch * width * 2 <= self.capacity
+
+
+# --------------------------------------------------------------------------------------------
+# bit-vector circuits: arrays of shape (B, w, dim), LSB first
+# --------------------------------------------------------------------------------------------
+def _zeros(c: Circuit, B: int, w: int) -> np.ndarray:
+    return c.trivial(np.zeros((B, w), dtype=bool))
+
+
+def g_bitwise(kind: str, a: np.ndarray, b: np.ndarray) -> Op:
+    gate = {"and": AND, "or": OR, "xor": XOR}[kind]
+    (r,) = yield [gate(a, b)]
+    return r
+
+
+def g_add(c: Circuit, a: np.ndarray, b: np.ndarray, cin: bool = False, want_sum: bool = True,
+          want_carry: bool = False, prefix: bool = None) -> Op:
+    """a + b + cin over w bits.  Returns (sum bits or None, carry-out or None)."""
+    B, w = a.shape[0], a.shape[1]
+    if prefix is None:
+        prefix = c.prefer_prefix(B, w)
+    if not prefix:
+        carry = c.trivial(np.full((B,), cin, dtype=bool))
+        sums = []
+        for i in range(w):
+            lvl = []
+            need_carry = i < w - 1 or want_carry
+            if need_carry:
+                lvl.append(MAJ(a[:, i], b[:, i], carry))
+            if want_sum:
+                lvl.append(XOR3(a[:, i], b[:, i], carry))
+            out = yield lvl
+            if want_sum:
+                sums.append(out[-1])
+            if need_carry:
+                carry = out[0]
+        return (np.stack(sums, axis=1) if want_sum else None), (carry if want_carry else None)
+    # Kogge-Stone: inclusive prefixes (G, P)[0..i]
+    G, P = yield [AND(a, b), OR(a, b)]
+    if not want_sum:
+        # only the full-span carry is needed: reduction tree
+        while G.shape[1] > 1:
+            if G.shape[1] % 2:
+                # pad with an identity element on the high side: G = 0, P = 1
+                G = np.concatenate([G, _zeros(c, B, 1)], axis=1)
+                P = np.concatenate([P, NOT(_zeros(c, B, 1))], axis=1)
+            lo_G, hi_G, lo_P, hi_P = G[:, 0::2], G[:, 1::2], P[:, 0::2], P[:, 1::2]
+            G, P = yield [MAJ(hi_G, hi_P, lo_G), MAJ(hi_G, hi_P, lo_P)]
+        return None, (P[:, 0] if cin else G[:, 0])
+    d = 1
+    while d < w:
+        hi_G, hi_P = G[:, d:], P[:, d:]
+        nG, nP = yield [MAJ(hi_G, hi_P, G[:, :-d]), MAJ(hi_G, hi_P, P[:, :-d])]
+        G = np.concatenate([G[:, :d], nG], axis=1)
+        P = np.concatenate([P[:, :d], nP], axis=1)
+        d *= 2
+    pref = P if cin else G
+    carries = np.concatenate([c.trivial(np.full((B, 1), cin, dtype=bool)), pref[:, :w - 1]], axis=1)
+    (s,) = yield [XOR3(a, b, carries)]
+    return s, (pref[:, w - 1] if want_carry else None)
+
+
+def g_sub(c: Circuit, a, b, want_sum=True, want_carry=False) -> Op:
+    """a - b = a + ~b + 1; carry-out = (a >= b)."""
+    return (yield from g_add(c, a, NOT(b), True, want_sum, want_carry))
+
+
+def g_ge(c: Circuit, a, b) -> Op:
+    _, cout = yield from g_add(c, a, NOT(b), True, want_sum=False, want_carry=True)
+    return cout
+
+
+def g_eq(c: Circuit, a, b) -> Op:
+    (x,) = yield [XOR(a, b)]
+    cur = NOT(x)                                    # XNOR per bit
+    B = a.shape[0]
+    while cur.shape[1] > 1:
+        if cur.shape[1] % 2:
+            cur = np.concatenate([cur, NOT(_zeros(c, B, 1))], axis=1)
+        (cur,) = yield [AND(cur[:, 0::2], cur[:, 1::2])]
+    return cur[:, 0]
+
+
+def g_select(cond: np.ndarray, x: np.ndarray, y: np.ndarray) -> Op:
+    """cond ? x : y bitwise (2 levels: two ANDs, one OR; at most one AND is true)."""
+    cw = np.broadcast_to(cond[:, None, :], x.shape)
+    t, f = yield [AND(cw, x), AND(NOT(cw), y)]
+    (r,) = yield [OR(t, f)]
+    return r
+
+
+def g_mul(c: Circuit, a: np.ndarray, b: Union[np.ndarray, int], prefix=None) -> Op:
+    """a * b mod 2^w: partial products (one level; none when b is plaintext), carry-save 3:2
+    compression (XOR3 + MAJ: one level per layer), final adder."""
+    B, w = a.shape[0], a.shape[1]
+    rows = []
+    if isinstance(b, (int, np.integer)):
+        k = int(b) % (1 << w)
+        for j in range(w):
+            if (k >> j) & 1:
+                rows.append(np.concatenate([_zeros(c, B, j), a[:, :w - j]], axis=1))
+    else:
+        lvl = [AND(a[:, :w - j], np.broadcast_to(b[:, j:j + 1], (B, w - j, c.dim))) for j in range(w)]
+        pp = yield lvl
+        rows = [np.concatenate([_zeros(c, B, j), pp[j]], axis=1) for j in range(w)]
+    if not rows:
+        return _zeros(c, B, w)
+    while len(rows) > 2:
+        ntrip = len(rows) // 3
+        lvl = []
+        for t in range(ntrip):
+            x, y, z = rows[3 * t:3 * t + 3]
+            lvl += [XOR3(x, y, z), MAJ(x[:, :w - 1], y[:, :w - 1], z[:, :w - 1])]
+        out = yield lvl
+        nrows = []
+        for t in range(ntrip):
+            nrows.append(out[2 * t])
+            nrows.append(np.concatenate([_zeros(c, B, 1), out[2 * t + 1]], axis=1))
+        rows = nrows + rows[3 * ntrip:]
+    if len(rows) == 1:
+        return rows[0]
+    s, _ = yield from g_add(c, rows[0], rows[1], prefix=prefix)
+    return s
+
+
+def g_div_rem_scalar(c: Circuit, a: np.ndarray, d: int) -> Op:
+    """Restoring division by a plaintext divisor: returns (quotient, remainder)."""
+    B, w = a.shape[0], a.shape[1]
+    d = int(d) % (1 << w)
+    if d == 0:  # tfhe-rs / fhEVM: quotient all ones, remainder = numerator
+        return NOT(_zeros(c, B, w)), a
+    L = d.bit_length()
+    q = _zeros(c, B, w)
+    # after shifting in the top k bits, R = a[w-k:] ; while k < L, R < d so q bits are 0
+    k0 = L - 1
+    R = a[:, w - k0:] if k0 > 0 else np.zeros((B, 0, c.dim), np.uint64)   # R has k0 bits
+    for i in range(w - L, -1, -1):
+        R = np.concatenate([a[:, i:i + 1], R], axis=1)         # (R << 1) | a_i  : L..w bits
+        r = R.shape[1]
+        dbits = c.trivial(np.broadcast_to(((d >> np.arange(r)) & 1).astype(bool), (B, r)))
+        t, ge = yield from g_add(c, R, NOT(dbits), True, want_sum=True, want_carry=True)
+        q[:, i] = ge
+        R = yield from g_select(ge, t, R)
+        R = R[:, :max(L, 1)] if r > L else R                   # R < d < 2^L after the step
+    rem = np.concatenate([R, _zeros(c, B, w - R.shape[1])], axis=1) if R.shape[1] < w else R[:, :w]
+    return q, rem
+
+
+def _shift_clear(c: Circuit, a: np.ndarray, k: int, kind: str) -> np.ndarray:
+    B, w = a.shape[0], a.shape[1]
+    k %= w
+    if kind == "shl":
+        return np.concatenate([_zeros(c, B, k), a[:, :w - k]], axis=1)
+    if kind == "shr":
+        return np.concatenate([a[:, k:], _zeros(c, B, k)], axis=1)
+    if kind == "rotl":
+        return np.roll(a, k, axis=1)
+    if kind == "rotr":
+        return np.roll(a, -k, axis=1)
+    raise ValueError(kind)
+
+
+def g_shift(c: Circuit, a: np.ndarray, amount: Union[np.ndarray, int], kind: str) -> Op:
+    """Shift / rotate by (amount mod w): a plaintext amount is rewiring (free); an encrypted one
+    is a barrel shifter, one select layer (2 levels) per amount bit."""
+    if isinstance(amount, (int, np.integer)):
+        return _shift_clear(c, a, int(amount), kind)
+    w = a.shape[1]
+    cur = a
+    for k in range((w - 1).bit_length()):
+        cur = yield from g_select(amount[:, k], _shift_clear(c, cur, 1 << k, kind), cur)
+    return cur
+
+
+# --------------------------------------------------------------------------------------------
+# typed values and the fhEVM operator dispatch
+# --------------------------------------------------------------------------------------------
+class FheUint:
+    """A batch of B encrypted w-bit unsigned integers: ``bits`` is (B, w, n+1), LSB first."""
+
+    def __init__(self, circuit: Circuit, bits: np.ndarray):
+        self.c, self.bits = circuit, bits
+
+    @property
+    def width(self) -> int:
+        return self.bits.shape[1]
+
+    @property
+    def batch(self) -> int:
+        return self.bits.shape[0]
+
+    @staticmethod
+    def _bits_of(values, width: int) -> np.ndarray:
+        v = np.atleast_1d(np.asarray(values, dtype=np.uint64))
+        return ((v[:, None] >> np.arange(width, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
+
+    @classmethod
+    def encrypt(cls, circuit: Circuit, ck: ClientKey, values, width: int, seed: int = 1,
+                stream0: int = 0) -> "FheUint":
+        b = cls._bits_of(values, width)
+        ct = ck.encrypt_bool(b.reshape(-1), seed, stream0).reshape(b.shape[0], width, -1)
+        return cls(circuit, ct)
+
+    @classmethod
+    def trivial(cls, circuit: Circuit, values, width: int) -> "FheUint":
+        return cls(circuit, circuit.trivial(cls._bits_of(values, width)))
+
+    def decrypt(self, ck: ClientKey) -> np.ndarray:
+        return decrypt_bits(ck, self.bits)
+
+    def cast(self, width: int) -> "FheUint":
+        """Zero-extend / truncate."""
+        if width == self.width:
+            return self
+        if width < self.width:
+            return FheUint(self.c, self.bits[:, :width])
+        return FheUint(self.c, np.concatenate([self.bits, _zeros(self.c, self.batch, width - self.width)], 1))
+
+    # synchronous operator sugar (each call runs its own levels; use Circuit.run_many + fhevm_op
+    # to batch independent operations)
+    def _r(self, op):
+        return self.c.run(op)
+
+    def __add__(self, o):
+        return FheUint(self.c, self._r(fhevm_op(self.c, "add", self, o)).bits)
+
+    def __sub__(self, o):
+        return FheUint(self.c, self._r(fhevm_op(self.c, "sub", self, o)).bits)
+
+    def __mul__(self, o):
+        return FheUint(self.c, self._r(fhevm_op(self.c, "mul", self, o)).bits)
+
+    def __and__(self, o):
+        return self._r(fhevm_op(self.c, "and", self, o))
+
+    def __or__(self, o):
+        return self._r(fhevm_op(self.c, "or", self, o))
+
+    def __xor__(self, o):
+        return self._r(fhevm_op(self.c, "xor", self, o))
+
+    def __neg__(self):
+        return self._r(fhevm_op(self.c, "neg", self))
+
+    def __invert__(self):
+        return FheUint(self.c, NOT(self.bits))
+
+    def op(self, name: str, other=None):
+        return self._r(fhevm_op(self.c, name, self, other))
+
+
+def decrypt_bits(ck: ClientKey, bits: np.ndarray) -> np.ndarray:
+    B, w = bits.shape[0], bits.shape[1]
+    b = ck.decrypt_bool(bits.reshape(-1, bits.shape[-1])).reshape(B, w).astype(np.uint64)
+    return (b << np.arange(w, dtype=np.uint64)[None, :]).sum(axis=1).astype(np.uint64)
+
+
+BINARY_OPS = ("add", "sub", "mul", "div", "rem", "and", "or", "xor", "shl", "shr", "rotl", "rotr",
+              "eq", "ne", "ge", "gt", "le", "lt", "min", "max")
+UNARY_OPS = ("neg", "not")
+BOOL_RESULT = ("eq", "ne", "ge", "gt", "le", "lt")
+
+
+def fhevm_op(c: Circuit, op: str, lhs, rhs=None) -> Op:
+    """One fhEVM operator as a coroutine.  ``lhs``/``rhs`` are FheUint or plaintext ints (at most
+    one plaintext); mixed widths widen to the larger (fhevm TFHE.sol overloads).  Returns a
+    FheUint, or for comparisons an encrypted bool array of shape (B, n+1)."""
+    if op in UNARY_OPS:
+        a = lhs.bits
+        if op == "not":
+            return FheUint(c, NOT(a))
+        s, _ = yield from g_sub(c, _zeros(c, a.shape[0], a.shape[1]), a)
+        return FheUint(c, s)
+    if op not in BINARY_OPS:
+        raise ValueError(f"unknown operator {op!r}")
+    l_enc, r_enc = isinstance(lhs, FheUint), isinstance(rhs, FheUint)
+    if not (l_enc or r_enc):
+        raise ValueError("at least one operand must be encrypted")
+    if op in ("shl", "shr", "rotl", "rotr"):
+        if not l_enc:
+            raise ValueError("shift of a plaintext by an encrypted amount is not an fhEVM overload")
+        if r_enc:
+            nb = max(1, (lhs.width - 1).bit_length())
+            amt = rhs.bits if rhs.width >= nb else rhs.cast(nb).bits
+        else:
+            amt = int(rhs)
+        return FheUint(c, (yield from g_shift(c, lhs.bits, amt, op)))
+    if op in ("div", "rem"):
+        if not l_enc or r_enc:
+            raise ValueError("div/rem take an encrypted numerator and a plaintext divisor")
+        q, r = yield from g_div_rem_scalar(c, lhs.bits, int(rhs))
+        return FheUint(c, q if op == "div" else r)
+    w = max(x.width for x in (lhs, rhs) if isinstance(x, FheUint))
+    B = (lhs if l_enc else rhs).batch
+
+    def bits(x):
+        return x.cast(w).bits if isinstance(x, FheUint) else c.trivial(
+            np.broadcast_to(FheUint._bits_of(np.full(B, int(x) % (1 << w), dtype=np.uint64), w), (B, w)))
+
+    if op == "mul":
+        if not l_enc:
+            return FheUint(c, (yield from g_mul(c, rhs.cast(w).bits, int(lhs))))
+        if not r_enc:
+            return FheUint(c, (yield from g_mul(c, lhs.cast(w).bits, int(rhs))))
+        return FheUint(c, (yield from g_mul(c, bits(lhs), bits(rhs))))
+    a, b = bits(lhs), bits(rhs)
+    if op in ("and", "or", "xor"):
+        return FheUint(c, (yield from g_bitwise(op, a, b)))
+    if op == "add":
+        s, _ = yield from g_add(c, a, b)
+        return FheUint(c, s)
+    if op == "sub":
+        s, _ = yield from g_sub(c, a, b)
+        return FheUint(c, s)
+    if op in ("eq", "ne"):
+        e = yield from g_eq(c, a, b)
+        return e if op == "eq" else NOT(e)
+    if op in ("ge", "lt"):
+        g = yield from g_ge(c, a, b)
+        return g if op == "ge" else NOT(g)
+    if op in ("le", "gt"):
+        g = yield from g_ge(c, b, a)
+        return g if op == "le" else NOT(g)
+    # min / max
+    lt = NOT((yield from g_ge(c, a, b)))
+    if op == "min":
+        return FheUint(c, (yield from g_select(lt, a, b)))
+    return FheUint(c, (yield from g_select(lt, b, a)))
