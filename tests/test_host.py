@@ -90,3 +90,19 @@ def test_fhevm_params_unsupported_on_device_build():
     # P-FHEVM (N=2048, KS->PBS) is a "next" row: the device path must refuse it loudly, not compute wrong.
     with pytest.raises(tfhe_amd.TfheError):
         tfhe_amd.Engine(tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM), 0)
+
+
+def test_gl64_primitives_exact(tmp_path):
+    """Goldilocks primitives of the device kernels (tfhe_amd/csrc/gl64.h, compiled for the host)
+    against 128-bit reference arithmetic, including non-canonical inputs."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    exe = str(tmp_path / "gl64_check")
+    subprocess.run([hipcc, "-O2", "-std=c++17", "-I", os.path.join(ROOT, "tfhe_amd", "csrc"),
+                    os.path.join(ROOT, "tools", "microbench", "gl64_check.cpp"), "-o", exe],
+                   check=True, capture_output=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout

@@ -25,24 +25,47 @@ __host__ __device__ __forceinline__ u64 gl_mulhi(u64 a, u64 b) {
   return (u64)(((unsigned __int128)a * b) >> 64);
 }
 
-// (hi * 2^64 + lo) mod p, canonical.  hi = hh * 2^32 + hl:  == lo - hh + hl * (2^32 - 1).
-__host__ __device__ __forceinline__ u64 gl_reduce128(u64 hi, u64 lo) {
-  const u64 hh = hi >> 32, hl = hi & GL_EPS;
-  u64 t0 = lo - hh;
-  t0 = (lo < hh) ? t0 - GL_EPS : t0;
-  const u64 t1 = (hl << 32) - hl;
-  u64 t2 = t0 + t1;
-  t2 = (t2 < t1) ? t2 + GL_EPS : t2;
-  return (t2 >= GL_P) ? t2 - GL_P : t2;
+// a * b + z as a 128-bit (hi, lo) pair — never overflows: 4 chained v_mad_u64_u32 (32x32 + 64),
+// every partial sum bounded below 2^64 (the 64-bit addend rides in the first two).
+__host__ __device__ __forceinline__ void gl_mac128(u64 a, u64 b, u64 z, u64& hi, u64& lo) {
+  const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
+  const u64 t = (u64)a0 * b0 + (u32)z;                   // <= 2^64 - 2^32
+  const u64 u = (u64)a1 * b0 + ((t >> 32) + (z >> 32));  // <= 2^64 - 1
+  const u64 v = (u64)a0 * b1 + (u32)u;                   // <  2^64
+  hi = (u64)a1 * b1 + ((u >> 32) + (v >> 32));           // <= 2^64 - 1
+  lo = (v << 32) | (u32)t;
 }
 
-// (hi * 2^64 + lo) mod p for hi < 2^32.
-__host__ __device__ __forceinline__ u64 gl_reduce96(u64 hi, u64 lo) {
-  const u64 t1 = (hi << 32) - hi;
-  u64 t2 = lo + t1;
-  t2 = (t2 < t1) ? t2 + GL_EPS : t2;
-  return (t2 >= GL_P) ? t2 - GL_P : t2;
+// Reductions of hi * 2^64 + lo (hi = hh * 2^32 + hl):  == lo - hh + hl * (2^32 - 1)  (mod p).
+// t = lo - hh (+p on borrow: t >= 2^64 - 2^32 + 1 there, so t - EPS does not wrap); then
+// r = hl * EPS + t in one mad.  On carry the true value is r + EPS and r <= 2^64 - 2^33, so
+// r + EPS < p; without carry r may still be >= p.  Exact for every (hi, lo).
+__host__ __device__ __forceinline__ u64 gl_reduce128_lazy(u64 hi, u64 lo) {  // any 64-bit word
+  const u64 hh = hi >> 32, hl = hi & GL_EPS;
+  u64 t = lo - hh;
+  t = (lo < hh) ? t + GL_P : t;
+  const u64 r = hl * GL_EPS + t;
+  return (r < t) ? r + GL_EPS : r;
 }
+__host__ __device__ __forceinline__ u64 gl_reduce128(u64 hi, u64 lo) {  // canonical
+  const u64 hh = hi >> 32, hl = hi & GL_EPS;
+  u64 t = lo - hh;
+  t = (lo < hh) ? t + GL_P : t;
+  const u64 r = hl * GL_EPS + t;
+  return (r < t || r >= GL_P) ? r + GL_EPS : r;  // carry: r + EPS < p;  r >= p: r + EPS == r - p
+}
+
+// (hi * 2^64 + lo) mod p for hi < 2^32: r = hi * EPS + lo (one mad), same carry argument.
+__host__ __device__ __forceinline__ u64 gl_reduce96_lazy(u64 hi, u64 lo) {
+  const u64 r = hi * GL_EPS + lo;
+  return (r < lo) ? r + GL_EPS : r;
+}
+__host__ __device__ __forceinline__ u64 gl_reduce96(u64 hi, u64 lo) {
+  const u64 r = hi * GL_EPS + lo;
+  return (r < lo || r >= GL_P) ? r + GL_EPS : r;
+}
+
+__host__ __device__ __forceinline__ u64 gl_canon(u64 x) { return (x >= GL_P) ? x + GL_EPS : x; }
 
 __host__ __device__ __forceinline__ u64 gl_add(u64 a, u64 b) {
   const u64 s = a + b;
@@ -57,28 +80,38 @@ __host__ __device__ __forceinline__ u64 gl_sub(u64 a, u64 b) {
 
 __host__ __device__ __forceinline__ u64 gl_neg(u64 a) { return a ? GL_P - a : 0; }
 
-__host__ __device__ __forceinline__ u64 gl_mul(u64 a, u64 b) { return gl_reduce128(gl_mulhi(a, b), a * b); }
+__host__ __device__ __forceinline__ u64 gl_mul(u64 a, u64 b) {
+  u64 hi, lo;
+  gl_mac128(a, b, 0, hi, lo);
+  return gl_reduce128(hi, lo);
+}
 
-// x * 2^s mod p.  s is a compile-time constant after unrolling (every call site below is in a
-// fully unrolled loop), so the branches fold away.  2^192 == 1, 2^96 == -1.
+// z + a * b mod p, lazily reduced (any 64-bit word in, any 64-bit word out): the MAC of the
+// external product accumulates with this and canonicalizes once per output (gl_canon).
+__host__ __device__ __forceinline__ u64 gl_mac_lazy(u64 z, u64 a, u64 b) {
+  u64 hi, lo;
+  gl_mac128(a, b, z, hi, lo);
+  return gl_reduce128_lazy(hi, lo);
+}
+
+// x * 2^r mod p for 0 <= r < 96 (r a compile-time constant after unrolling: the branches fold
+// away).  Canonical output for r > 0 and any 64-bit x; r = 0 returns x.  Steps of at most 32 bits
+// keep the high part below 2^32, so each step is one mad + a carry fix (gl_reduce96).
+__host__ __device__ __forceinline__ u64 gl_shl_mod(u64 x, int r) {
+  if (r == 0) return x;
+  while (r > 32) {
+    x = gl_reduce96_lazy(x >> 32, x << 32);
+    r -= 32;
+  }
+  return gl_reduce96(x >> (64 - r), x << r);
+}
+
+// x * 2^s mod p for any integer s (2^192 == 1, 2^96 == -1); canonical for canonical x.
 __host__ __device__ __forceinline__ u64 gl_mul_pow2(u64 x, int s) {
   s %= 192;
   if (s < 0) s += 192;
-  const bool neg = s >= 96;
-  const int r = neg ? s - 96 : s;
-  u64 v;
-  if (r == 0) {
-    v = x;
-  } else if (r <= 32) {
-    v = gl_reduce96(x >> (64 - r), x << r);
-  } else if (r < 64) {
-    v = gl_reduce128(x >> (64 - r), x << r);
-  } else {  // 64 <= r < 96: two steps
-    const u64 y = gl_reduce96(x >> 32, x << 32);
-    const int r2 = r - 32;
-    v = gl_reduce128(y >> (64 - r2), y << r2);
-  }
-  return neg ? gl_neg(v) : v;
+  if (s >= 96) return gl_neg(gl_shl_mod(x, s - 96));
+  return gl_shl_mod(x, s);
 }
 
 // small signed digit -> Z_p

@@ -8,8 +8,9 @@
 //   pass 2a  cyclic 16-point, root psi^128 = 2^12, CT over X^(2L) - w^(2t) = (X^L - w^t)(X^L + w^t)
 //   tw 2     2^(3 i3 j2)                                 (table; a power of two)
 //   pass 2b  4 cyclic 4-point transforms, root 2^48
-// Multiplying by 2^s is shifts plus a 96/128-bit fold (gl_mul_pow2): no general multiply inside
-// a pass.  All loops are fully unrolled: every index and shift is a compile-time constant.
+// Multiplying by 2^s is shifts plus one mad-based fold per 32 bits (gl_shl_mod; the sign of
+// 2^96 = -1 swaps the butterfly's add and sub): no general multiply inside a pass.  All loops are
+// fully unrolled: every index and shift is a compile-time constant.
 #pragma once
 #include "gl64.h"
 
@@ -45,9 +46,12 @@ __host__ __device__ __forceinline__ void ct_fwd(u64 (&x)[NX]) {
     for (int j = 0; j < n; j++) {
       if ((j % (2 * ln)) < ln) {
         const int k = (n / 2) / ln + j / (2 * ln);
-        const u64 t = gl_mul_pow2(x[BASE + j + ln], zeta_exp<NEGA_, LOGN, REXP>(k));
-        x[BASE + j + ln] = gl_sub(x[BASE + j], t);
-        x[BASE + j] = gl_add(x[BASE + j], t);
+        const int z = zeta_exp<NEGA_, LOGN, REXP>(k) % 192;
+        // 2^z = -2^(z - 96) for z >= 96: the sign swaps the butterfly's add and sub
+        const u64 t = gl_shl_mod(x[BASE + j + ln], z >= 96 ? z - 96 : z);
+        const u64 u = x[BASE + j];
+        x[BASE + j] = z >= 96 ? gl_sub(u, t) : gl_add(u, t);
+        x[BASE + j + ln] = z >= 96 ? gl_add(u, t) : gl_sub(u, t);
       }
     }
   }
@@ -64,8 +68,9 @@ __host__ __device__ __forceinline__ void gs_inv(u64 (&x)[NX]) {
       if ((j % (2 * ln)) < ln) {
         const int k = (n / 2) / ln + j / (2 * ln);
         const u64 u = x[BASE + j], v = x[BASE + j + ln];
+        const int z = (192 - zeta_exp<NEGA_, LOGN, REXP>(k) % 192) % 192;
         x[BASE + j] = gl_add(u, v);
-        x[BASE + j + ln] = gl_mul_pow2(gl_sub(u, v), 192 - zeta_exp<NEGA_, LOGN, REXP>(k));
+        x[BASE + j + ln] = z >= 96 ? gl_shl_mod(gl_sub(v, u), z - 96) : gl_shl_mod(gl_sub(u, v), z);
       }
     }
   }

@@ -214,8 +214,8 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int a, 
     const u64* k1 = sh.K[g & 1] + N1K + lane;
 #pragma unroll
     for (int e = 0; e < 16; e++) {
-      out0[e] = gl_add(out0[e], gl_mul(x[e], k0[64 * e]));
-      out1[e] = gl_add(out1[e], gl_mul(x[e], k1[64 * e]));
+      out0[e] = gl_mac_lazy(out0[e], x[e], k0[64 * e]);  // lazily reduced: canonicalized before the
+      out1[e] = gl_mac_lazy(out1[e], x[e], k1[64 * e]);  // inverse NTT
     }
   }
 }
@@ -260,6 +260,8 @@ __global__ __launch_bounds__(BR_THREADS, 1) void blind_rotate_kernel(
     for (int e = 0; e < 16; e++) { out0[e] = 0; out1[e] = 0; }
     ext_prod_component(accA, a, 0, i, n_steps, sh, T, wave, lane, bsk, out0, out1);
     ext_prod_component(accB, a, 1, i, n_steps, sh, T, wave, lane, bsk, out0, out1);
+#pragma unroll
+    for (int e = 0; e < 16; e++) { out0[e] = gl_canon(out0[e]); out1[e] = gl_canon(out1[e]); }
     ntt1024_inv(out0, T, lane, sh.tw);
 #pragma unroll
     for (int e = 0; e < 16; e++) accA[e] = gl_add(accA[e], out0[e]);
