@@ -106,6 +106,34 @@ __host__ __device__ __forceinline__ u64 gl_shl_mod(u64 x, int r) {
   return gl_reduce96(x >> (64 - r), x << r);
 }
 
+// x * 2^-t mod p for 1 <= t <= 32, any 64-bit x, canonical output.  With x = xh 2^t + xl and
+// 2^-t = -2^(96-t):  x 2^-t == xh - xl 2^(32-t) 2^64 == xh + y - y 2^32,  y = xl 2^(32-t) < 2^32.
+// s = xh + y < 2^63 + 2^32 (no wrap); s - y 2^32 >= -(p - 1), so one conditional +p lands in [1, p).
+__host__ __device__ __forceinline__ u64 gl_shr_mod(u64 x, int t) {
+  const u64 xh = x >> t;
+  const u32 y = (u32)x << (32 - t);
+  const u64 s = xh + y;
+  const u64 yy = (u64)y << 32;
+  const u64 d = s - yy;
+  return (s < yy) ? d + GL_P : d;
+}
+
+// 2^z * x == (neg ? -v : v) for a compile-time z: the cheapest of shl by r = z mod 96 (r <= 64)
+// or shr by 96 - r (r > 64, one fold instead of three), with the sign of 2^96 = -1 reported back
+// so callers fold it into an add/sub.  v is canonical unless r == 0 (then v = x).
+__host__ __device__ __forceinline__ u64 gl_pow2_twiddle(u64 x, int z, bool& neg) {
+  z %= 192;
+  if (z < 0) z += 192;
+  const bool s = z >= 96;
+  const int r = z % 96;
+  if (r > 64) {
+    neg = !s;
+    return gl_shr_mod(x, 96 - r);
+  }
+  neg = s;
+  return gl_shl_mod(x, r);
+}
+
 // x * 2^s mod p for any integer s (2^192 == 1, 2^96 == -1); canonical for canonical x.
 __host__ __device__ __forceinline__ u64 gl_mul_pow2(u64 x, int s) {
   s %= 192;

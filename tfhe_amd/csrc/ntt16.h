@@ -46,12 +46,11 @@ __host__ __device__ __forceinline__ void ct_fwd(u64 (&x)[NX]) {
     for (int j = 0; j < n; j++) {
       if ((j % (2 * ln)) < ln) {
         const int k = (n / 2) / ln + j / (2 * ln);
-        const int z = zeta_exp<NEGA_, LOGN, REXP>(k) % 192;
-        // 2^z = -2^(z - 96) for z >= 96: the sign swaps the butterfly's add and sub
-        const u64 t = gl_shl_mod(x[BASE + j + ln], z >= 96 ? z - 96 : z);
+        bool neg;  // the sign of the power-of-two twiddle swaps the butterfly's add and sub
+        const u64 t = gl_pow2_twiddle(x[BASE + j + ln], zeta_exp<NEGA_, LOGN, REXP>(k), neg);
         const u64 u = x[BASE + j];
-        x[BASE + j] = z >= 96 ? gl_sub(u, t) : gl_add(u, t);
-        x[BASE + j + ln] = z >= 96 ? gl_add(u, t) : gl_sub(u, t);
+        x[BASE + j] = neg ? gl_sub(u, t) : gl_add(u, t);
+        x[BASE + j + ln] = neg ? gl_add(u, t) : gl_sub(u, t);
       }
     }
   }
@@ -68,9 +67,11 @@ __host__ __device__ __forceinline__ void gs_inv(u64 (&x)[NX]) {
       if ((j % (2 * ln)) < ln) {
         const int k = (n / 2) / ln + j / (2 * ln);
         const u64 u = x[BASE + j], v = x[BASE + j + ln];
-        const int z = (192 - zeta_exp<NEGA_, LOGN, REXP>(k) % 192) % 192;
+        const int z = 192 - zeta_exp<NEGA_, LOGN, REXP>(k) % 192;
+        bool neg = false;  // sign known at compile time: the subtraction is ordered to absorb it
+        (void)gl_pow2_twiddle(0, z, neg);
         x[BASE + j] = gl_add(u, v);
-        x[BASE + j + ln] = z >= 96 ? gl_shl_mod(gl_sub(v, u), z - 96) : gl_shl_mod(gl_sub(u, v), z);
+        x[BASE + j + ln] = gl_pow2_twiddle(neg ? gl_sub(v, u) : gl_sub(u, v), z, neg);
       }
     }
   }

@@ -84,7 +84,7 @@ __device__ __forceinline__ void ntt1024_fwd_tail(u64 (&x)[16], u64* T, int lane,
   wave_lds_sync();
   cyc16_fwd(x);
 #pragma unroll
-  for (int f = 0; f < 16; f++) x[f] = gl_mul(x[f], tw[N1K + 64 * f + lane]);
+  for (int f = 1; f < 16; f++) x[f] = gl_mul(x[f], tw[N1K + 64 * f + lane]);  // tw2 column f = 0 is 1
 #pragma unroll
   for (int f = 0; f < 16; f++) T[f * 64 + (lane ^ ((f >> 2) & 3))] = x[f];
   wave_lds_sync();
@@ -126,7 +126,7 @@ __device__ __forceinline__ void ntt1024_inv(u64 (&x)[16], u64* T, int lane, cons
   for (int f = 0; f < 16; f++) x[f] = T[f * 64 + (lane ^ ((f >> 2) & 3))];
   wave_lds_sync();
 #pragma unroll
-  for (int f = 0; f < 16; f++) x[f] = gl_mul(x[f], tw[3 * N1K + 64 * f + lane]);
+  for (int f = 1; f < 16; f++) x[f] = gl_mul(x[f], tw[3 * N1K + 64 * f + lane]);  // f = 0 is 1
   cyc16_inv(x);
 #pragma unroll
   for (int e = 0; e < 16; e++) T[e1 * T1_STRIDE + 4 * e + q] = x[e];

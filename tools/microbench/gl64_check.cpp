@@ -67,6 +67,16 @@ int main() {
     const u64 s = gl_shl_mod(x, r);
     const u64 want = ref_mod((u128)x * pw[r]);
     if (r > 0 ? s != want : s != x) { if (bad++ < 5) printf("shl %lx r=%d -> %lx want %lx\n", x, r, s, want); }
+    if (r >= 1 && r <= 32) {  // x * 2^-r == x * 2^(192 - r)
+      const u64 sr = gl_shr_mod(x, r);
+      if (sr != ref_mod((u128)x * pw[192 - r])) { if (bad++ < 5) printf("shr %lx r=%d -> %lx\n", x, r, sr); }
+    }
+    for (int z = (int)(i % 7); z < 192; z += 7) {
+      bool ng = false;
+      const u64 tv = gl_pow2_twiddle(x, z, ng);
+      const u64 got = ng ? (GL_P - tv % GL_P) % GL_P : tv % GL_P;
+      if (got != ref_mod((u128)x * pw[z])) { if (bad++ < 5) printf("tw %lx z=%d\n", x, z); }
+    }
     const u64 cx = x % GL_P;
     const int s2 = (int)(i % 192);
     if (gl_mul_pow2(cx, s2) != ref_mod((u128)cx * pw[s2])) { if (bad++ < 5) printf("pow2 %lx s=%d\n", cx, s2); }
