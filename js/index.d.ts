@@ -45,29 +45,58 @@ export class FheBool {
   xor(o: FheBool): Promise<FheBool>;
   not(): FheBool;
 }
+export type FheOp = 'add' | 'sub' | 'mul' | 'div' | 'rem' | 'and' | 'or' | 'xor' | 'shl' | 'shr' | 'rotl' | 'rotr'
+  | 'eq' | 'ne' | 'ge' | 'gt' | 'le' | 'lt' | 'min' | 'max' | 'neg' | 'not';
 declare class FheUintN {
-  constructor(engine: Engine, ct: BigUint64Array);
-  readonly ct: BigUint64Array;
+  constructor(engine: Engine, ct: BigUint64Array, count?: number);
+  readonly ct: BigUint64Array;   // value-major [count][bits][n+1]
+  readonly count: number;
   static readonly bitWidth: number;
   decrypt(ck: ClientKey): bigint[];
-  and(o: FheUintN): Promise<FheUintN>;
-  or(o: FheUintN): Promise<FheUintN>;
-  xor(o: FheUintN): Promise<FheUintN>;
+  /** any fhEVM operator (js/integer.js); comparisons resolve to FheBool */
+  op(name: FheOp, other?: FheUintN | number | bigint | null): Promise<FheUintN | FheBool>;
+  and(o: FheUintN | bigint): Promise<FheUintN>;
+  or(o: FheUintN | bigint): Promise<FheUintN>;
+  xor(o: FheUintN | bigint): Promise<FheUintN>;
   not(): FheUintN;
+  add(o: FheUintN | bigint): Promise<FheUintN>;
+  sub(o: FheUintN | bigint): Promise<FheUintN>;
+  mul(o: FheUintN | bigint): Promise<FheUintN>;
+  eq(o: FheUintN | bigint): Promise<FheBool>;
+  ne(o: FheUintN | bigint): Promise<FheBool>;
+  lt(o: FheUintN | bigint): Promise<FheBool>;
+  le(o: FheUintN | bigint): Promise<FheBool>;
+  gt(o: FheUintN | bigint): Promise<FheBool>;
+  ge(o: FheUintN | bigint): Promise<FheBool>;
+  min(o: FheUintN | bigint): Promise<FheUintN>;
+  max(o: FheUintN | bigint): Promise<FheUintN>;
 }
 export class FheUint8 extends FheUintN { static encrypt(v: number | bigint | Array<number | bigint>, ck: ClientKey, e: Engine, seed?: bigint, stream0?: bigint): FheUint8; }
 export class FheUint16 extends FheUintN { static encrypt(v: number | bigint | Array<number | bigint>, ck: ClientKey, e: Engine, seed?: bigint, stream0?: bigint): FheUint16; }
 export class FheUint32 extends FheUintN { static encrypt(v: number | bigint | Array<number | bigint>, ck: ClientKey, e: Engine, seed?: bigint, stream0?: bigint): FheUint32; }
+export class FheUint64 extends FheUintN { static encrypt(v: number | bigint | Array<number | bigint>, ck: ClientKey, e: Engine, seed?: bigint, stream0?: bigint): FheUint64; }
 
-export interface EvaluateRequest { op: 'and' | 'or' | 'xor' | 'not'; left: Uint8Array; right?: Uint8Array; bitWidth: 8 | 16 | 32; }
+/** ciphertext bytes: 'TFA1' | u8 kind | u8 0 | u16 width | u32 lwe_dim | u32 count | u64[] (LE) */
+export function serializeCiphertext(kind: 0 | 1, width: number, lweDim: number, count: number, words: BigUint64Array): Uint8Array;
+export function parseCiphertext(bytes: Uint8Array | number[]): { kind: number; width: number; lweDim: number; count: number; words: BigUint64Array };
+
+export interface EvaluateRequest { op: FheOp; left: Uint8Array; right?: Uint8Array | number | bigint | null; bitWidth?: number; }
 export class LuxFHELocalClient {
   constructor(config?: { params?: TfheParams; seed?: bigint; device?: number });
   initialize(): Promise<void>;
   getPublicKey(): Promise<Uint8Array>;
-  encrypt_uint8(v: number): Promise<Uint8Array>;
-  encrypt_uint16(v: number): Promise<Uint8Array>;
-  encrypt_uint32(v: number): Promise<Uint8Array>;
+  encryptValue(value: number | bigint | string, bitWidth: number): Uint8Array;
+  encrypt_bool(v: boolean): Promise<Uint8Array>;
+  encrypt_uint8(v: number | bigint): Promise<Uint8Array>;
+  encrypt_uint16(v: number | bigint): Promise<Uint8Array>;
+  encrypt_uint32(v: number | bigint): Promise<Uint8Array>;
+  encrypt_uint64(v: number | bigint): Promise<Uint8Array>;
+  encrypt_uint128(v: number | bigint): Promise<Uint8Array>;
+  encrypt_uint256(v: number | bigint): Promise<Uint8Array>;
+  encrypt_address(a: string | bigint): Promise<Uint8Array>;
+  /** requests submitted concurrently share PBS launches (lockstep circuit levels) */
   evaluate(req: EvaluateRequest): Promise<Uint8Array>;
-  decrypt(ct: Uint8Array, bitWidth: 8 | 16 | 32): Promise<bigint>;
+  decrypt(ct: Uint8Array): Promise<bigint>;
+  unseal(address: string, ct: Uint8Array): Promise<bigint>;
   close(): void;
 }

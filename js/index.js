@@ -8,13 +8,14 @@
  *   genKeys / ClientKey / ServerKey   <- TfheClientKey.generate + server key (tfhe.ts:20-28)
  *   Engine.pbs / keyswitchProgrammableBootstrap / generateAccumulator
  *                                      <- ServerKey::keyswitch_programmable_bootstrap (biometrics main.rs:65-71)
- *   FheBool (nand/and/or/xor/not), FheUint8/16/32 bitwise ops
+ *   FheBool (nand/and/or/xor/not), FheUint8..256 with every fhEVM operator (js/integer.js)
  *   LuxFHELocalClient                  <- LuxFHEClient (luxfhejs) method names, computed locally
  * Every homomorphic operation runs on the GPU through libtfhe_hip.so (N-API, async work);
  * keygen / encrypt / decrypt are the client-side host code of the same library.
  */
 const path = require('path');
 const native = require(path.join(__dirname, 'build', 'tfhe_napi.node'));
+const integer = require('./integer.js');
 
 const PRESET_GATE = 0;
 const PRESET_FHEVM = 1;
@@ -121,16 +122,50 @@ class FheBool {
   not() { return new FheBool(this.engine, gateLin(this.ct, null, -1, 0, 0, this.ctLen)); }
 }
 
-/** FheUintN as N gate-encoded bits (LSB first); bitwise ops bootstrap all bits in one batch. */
+/**
+ * Ciphertext bytes (the opaque Uint8Array of the HTTP API and LuxFHEClient): a 16-byte header
+ *   'TFA1' | u8 kind (0 = ebool, 1 = euint) | u8 0 | u16 width | u32 lwe_dim | u32 count
+ * then count x width x (lwe_dim + 1) u64 little-endian (value-major, LSB bit first).
+ */
+const CT_MAGIC = 0x31414654; // 'TFA1'
+function serializeCiphertext(kind, width, lweDim, count, words) {
+  const out = new Uint8Array(16 + words.byteLength);
+  const dv = new DataView(out.buffer);
+  dv.setUint32(0, CT_MAGIC, true);
+  dv.setUint8(4, kind);
+  dv.setUint16(6, width, true);
+  dv.setUint32(8, lweDim, true);
+  dv.setUint32(12, count, true);
+  out.set(new Uint8Array(words.buffer, words.byteOffset, words.byteLength), 16);
+  return out;
+}
+function parseCiphertext(bytes) {
+  const u8 = bytes instanceof Uint8Array ? bytes : Uint8Array.from(bytes);
+  if (u8.length < 16) throw new Error('ciphertext too short');
+  const dv = new DataView(u8.buffer, u8.byteOffset, u8.byteLength);
+  if (dv.getUint32(0, true) !== CT_MAGIC) throw new Error('not a tfhe_amd ciphertext (bad magic)');
+  const kind = dv.getUint8(4), width = dv.getUint16(6, true), lweDim = dv.getUint32(8, true), count = dv.getUint32(12, true);
+  const nWords = count * width * (lweDim + 1);
+  if (u8.length !== 16 + 8 * nWords) throw new Error(`ciphertext length ${u8.length} != header size ${16 + 8 * nWords}`);
+  const words = new BigUint64Array(u8.buffer.slice(u8.byteOffset + 16, u8.byteOffset + u8.byteLength));
+  return { kind, width, lweDim, count, words };
+}
+
+/** FheUintN: a batch of N-bit encrypted integers over gate bootstrapping (js/integer.js). */
 function makeUint(bits) {
   return class {
-    constructor(engine, ct) { this.engine = engine; this.ct = ct; this.bits = bits; }
+    constructor(engine, ct, count = null) {
+      this.engine = engine;
+      this.ct = ct; // value-major [count][bits][n+1]
+      this.bits = bits;
+      this.count = count === null ? ct.length / (bits * (engine.params.n + 1)) : count;
+    }
     static get bitWidth() { return bits; }
     static encrypt(values, clientKey, engine, seed = 1n, stream0 = 0n) {
       const vs = Array.isArray(values) ? values : [values];
       const flat = [];
       for (const v of vs) for (let j = 0; j < bits; j++) flat.push(((BigInt(v) >> BigInt(j)) & 1n) === 1n);
-      return new this(engine, clientKey.encryptBool(flat, seed, stream0));
+      return new this(engine, clientKey.encryptBool(flat, seed, stream0), vs.length);
     }
     decrypt(clientKey) {
       const b = clientKey.decryptBool(this.ct);
@@ -142,75 +177,145 @@ function makeUint(bits) {
       }
       return out;
     }
-    _wrap(ct) { return new this.constructor(this.engine, ct); }
-    async and(o) { return this._wrap((await new FheBool(this.engine, this.ct).and(new FheBool(this.engine, o.ct))).ct); }
-    async or(o) { return this._wrap((await new FheBool(this.engine, this.ct).or(new FheBool(this.engine, o.ct))).ct); }
-    async xor(o) { return this._wrap((await new FheBool(this.engine, this.ct).xor(new FheBool(this.engine, o.ct))).ct); }
-    not() { return this._wrap(new FheBool(this.engine, this.ct).not().ct); }
+    _vec(circuit) { return integer.FheUintVec.fromValueMajor(circuit, this.ct, this.count, bits); }
+    /** any fhEVM operator (js/integer.js); other: FheUint* of any width or a plaintext */
+    async op(name, other = null) {
+      const c = new integer.Circuit(this.engine);
+      const rhs = other && other.ct ? other._vec(c) : other;
+      const r = await c.run(integer.fhevmOp(c, name, this._vec(c), rhs));
+      if (r instanceof integer.FheUintVec) return new (UINT_CLASSES[r.width] || makeUint(r.width))(this.engine, r.toValueMajor(), r.B);
+      return new FheBool(this.engine, r);
+    }
+    and(o) { return this.op('and', o); }
+    or(o) { return this.op('or', o); }
+    xor(o) { return this.op('xor', o); }
+    not() { return new this.constructor(this.engine, gateLin(this.ct, null, -1, 0, 0, this.engine.params.n + 1), this.count); }
+    add(o) { return this.op('add', o); }
+    sub(o) { return this.op('sub', o); }
+    mul(o) { return this.op('mul', o); }
+    eq(o) { return this.op('eq', o); }
+    ne(o) { return this.op('ne', o); }
+    lt(o) { return this.op('lt', o); }
+    le(o) { return this.op('le', o); }
+    gt(o) { return this.op('gt', o); }
+    ge(o) { return this.op('ge', o); }
+    min(o) { return this.op('min', o); }
+    max(o) { return this.op('max', o); }
   };
 }
-const FheUint8 = makeUint(8);
-const FheUint16 = makeUint(16);
-const FheUint32 = makeUint(32);
+const UINT_CLASSES = {};
+for (const w of [8, 16, 32, 64, 128, 160, 256]) UINT_CLASSES[w] = makeUint(w);
+const FheUint8 = UINT_CLASSES[8];
+const FheUint16 = UINT_CLASSES[16];
+const FheUint32 = UINT_CLASSES[32];
+const FheUint64 = UINT_CLASSES[64];
 
 /**
  * LuxFHEClient-compatible local client (packages/luxfhejs/src/index.ts:42-200 method names).
- * encrypt_* return the serialized ciphertext bytes (Uint8Array) like the HTTP client; evaluate()
- * covers the bitwise ops of POST /evaluate (e2e/test/fhe.test.ts:105-175) on the GPU.
+ * encrypt_* return serialized ciphertext bytes (Uint8Array) like the HTTP client; evaluate() takes
+ * the POST /evaluate shape (e2e/test/fhe.test.ts:105-175) and runs every fhEVM operator on the GPU.
+ * Requests submitted concurrently are evaluated in lockstep (one PBS launch per circuit level).
  */
 class LuxFHELocalClient {
   constructor(config = {}) {
     this.params = config.params || paramsPreset(PRESET_GATE);
     this.seed = BigInt(config.seed || 0x7F4E0001n);
     this.device = config.device || 0;
-    this.engine = null;
+    this.engine = config.engine || null;
     this.clientKey = null;
     this.serverKey = null;
     this.stream = 0n;
+    this.queue = [];
+    this.busy = false;
+    this.launches = 0;
   }
   async initialize() {
     [this.clientKey, this.serverKey] = genKeys(this.params, this.seed);
-    this.engine = new Engine(this.params, this.device).loadKeys(this.serverKey);
+    if (!this.engine) this.engine = new Engine(this.params, this.device).loadKeys(this.serverKey);
   }
+  /** key descriptor: params + SHA-256 of the evaluation keys (this scheme has no public encryption key) */
   async getPublicKey() {
-    // this scheme's evaluation key = BSK || KSK (standard domain, u64 LE)
-    const b = this.serverKey.bsk, k = this.serverKey.ksk;
-    const out = new Uint8Array((b.length + k.length) * 8);
-    out.set(new Uint8Array(b.buffer, b.byteOffset, b.byteLength), 0);
-    out.set(new Uint8Array(k.buffer, k.byteOffset, k.byteLength), b.byteLength);
+    const crypto = require('crypto');
+    const h = crypto.createHash('sha256');
+    for (const a of [this.serverKey.bsk, this.serverKey.ksk]) h.update(new Uint8Array(a.buffer, a.byteOffset, a.byteLength));
+    const p = this.params;
+    const head = new Uint32Array([0x314B4654, p.n, p.k, p.N, p.pbs_base_log, p.pbs_level, p.ks_base_log, p.ks_level, p.order]);
+    const out = new Uint8Array(head.byteLength + 32);
+    out.set(new Uint8Array(head.buffer), 0);
+    out.set(h.digest(), head.byteLength);
     return out;
   }
-  _enc(value, bitWidth) {
-    const cls = { 8: FheUint8, 16: FheUint16, 32: FheUint32 }[bitWidth];
-    if (!cls) throw new Error(`Encryption failed: bitWidth ${bitWidth} not supported by the local engine`);
-    const ct = cls.encrypt([value], this.clientKey, this.engine, this.seed + 1n, this.stream).ct;
-    this.stream += BigInt(bitWidth);
-    return new Uint8Array(ct.buffer, ct.byteOffset, ct.byteLength);
+  encryptValue(value, bitWidth) {
+    const w = Number(bitWidth);
+    if (!(w >= 1 && w <= 256)) throw new Error(`Encryption failed: bitWidth ${bitWidth} not supported`);
+    const v = BigInt.asUintN(w, BigInt(value));
+    const flat = [];
+    for (let j = 0; j < w; j++) flat.push(((v >> BigInt(j)) & 1n) === 1n);
+    const ct = this.clientKey.encryptBool(flat, this.seed + 1n, this.stream);
+    this.stream += BigInt(w);
+    return serializeCiphertext(w === 1 ? 0 : 1, w, this.params.n, 1, ct);
   }
-  async encrypt_uint8(v) { return this._enc(v, 8); }
-  async encrypt_uint16(v) { return this._enc(v, 16); }
-  async encrypt_uint32(v) { return this._enc(v, 32); }
-  _ct(bytes) { return new BigUint64Array(bytes.buffer.slice(bytes.byteOffset, bytes.byteOffset + bytes.byteLength)); }
-  async evaluate({ op, left, right, bitWidth }) {
-    const cls = { 8: FheUint8, 16: FheUint16, 32: FheUint32 }[bitWidth];
-    const a = new cls(this.engine, this._ct(left));
-    const b = right ? new cls(this.engine, this._ct(right)) : null;
-    let r;
-    if (op === 'and') r = await a.and(b);
-    else if (op === 'or') r = await a.or(b);
-    else if (op === 'xor') r = await a.xor(b);
-    else if (op === 'not') r = a.not();
-    else throw new Error(`evaluate: op ${op} not supported by the local engine`);
-    return new Uint8Array(r.ct.buffer, r.ct.byteOffset, r.ct.byteLength);
+  async encrypt_bool(v) { return this.encryptValue(v ? 1 : 0, 1); }
+  async encrypt_uint8(v) { return this.encryptValue(v, 8); }
+  async encrypt_uint16(v) { return this.encryptValue(v, 16); }
+  async encrypt_uint32(v) { return this.encryptValue(v, 32); }
+  async encrypt_uint64(v) { return this.encryptValue(v, 64); }
+  async encrypt_uint128(v) { return this.encryptValue(v, 128); }
+  async encrypt_uint256(v) { return this.encryptValue(v, 256); }
+  async encrypt_address(a) { return this.encryptValue(BigInt(a), 160); }
+
+  _operand(x, bitWidth, circuit) {
+    if (x === null || x === undefined) return null;
+    if (typeof x === 'number' || typeof x === 'bigint' || typeof x === 'string') return BigInt(x);
+    const ct = parseCiphertext(x);
+    if (ct.lweDim !== this.params.n) throw new Error(`ciphertext lwe_dim ${ct.lweDim} != engine n ${this.params.n}`);
+    return integer.FheUintVec.fromValueMajor(circuit, ct.words, ct.count, ct.width);
   }
-  async decrypt(bytes, bitWidth) {
-    const cls = { 8: FheUint8, 16: FheUint16, 32: FheUint32 }[bitWidth];
-    return new cls(this.engine, this._ct(bytes)).decrypt(this.clientKey)[0];
+  /** POST /evaluate: { op, left, right?, bitWidth } -> ciphertext bytes (ebool for comparisons) */
+  evaluate(req) {
+    return new Promise((resolve, reject) => {
+      this.queue.push({ req, resolve, reject });
+      this._pump();
+    });
   }
-  close() { if (this.engine) this.engine.destroy(); }
+  async _pump() {
+    if (this.busy || !this.queue.length) return;
+    this.busy = true;
+    const jobs = this.queue.splice(0);
+    const c = new integer.Circuit(this.engine);
+    const live = [];
+    for (const j of jobs) {
+      try {
+        const { op, left, right } = j.req;
+        live.push({ j, gen: integer.fhevmOp(c, op, this._operand(left, j.req.bitWidth, c), this._operand(right, j.req.bitWidth, c)) });
+      } catch (e) { j.reject(e); }
+    }
+    try {
+      const res = await c.runMany(live.map((x) => x.gen));
+      this.launches += c.launches;
+      res.forEach((r, i) => {
+        if (r instanceof integer.FheUintVec) live[i].j.resolve(serializeCiphertext(1, r.width, this.params.n, r.B, r.toValueMajor()));
+        else live[i].j.resolve(serializeCiphertext(0, 1, this.params.n, r.length / (this.params.n + 1), r));
+      });
+    } catch (e) {
+      live.forEach((x) => x.j.reject(e));
+    }
+    this.busy = false;
+    this._pump();
+  }
+  /** -> bigint (first value of the ciphertext) */
+  async decrypt(bytes) {
+    const ct = parseCiphertext(bytes);
+    const c = { dim: this.params.n + 1 };
+    const vec = integer.FheUintVec.fromValueMajor(c, ct.words, ct.count, ct.width);
+    return integer.decryptColumns(this.clientKey, vec.cols, ct.count)[0];
+  }
+  async unseal(_addr, data) { return this.decrypt(data); }
+  close() { if (this.engine && this.engine.destroy) this.engine.destroy(); }
 }
 
 module.exports = {
-  native, PRESET_GATE, PRESET_FHEVM, MU, paramsPreset, genKeys, ClientKey, ServerKey, Engine,
-  FheBool, FheUint8, FheUint16, FheUint32, LuxFHELocalClient,
+  native, integer, PRESET_GATE, PRESET_FHEVM, MU, paramsPreset, genKeys, ClientKey, ServerKey, Engine,
+  FheBool, FheUint8, FheUint16, FheUint32, FheUint64, UINT_CLASSES, LuxFHELocalClient,
+  serializeCiphertext, parseCiphertext,
 };

@@ -49,3 +49,26 @@ def test_js_addon_cpu(product_keys):
 @pytest.mark.gpu
 def test_js_addon_gpu():
     assert _run("gpu_check.js", 600)["ok"] is True
+
+
+def _run_plain(script, *args, timeout=600):
+    _ensure_addon()
+    r = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", script), *args], capture_output=True, text=True,
+                       timeout=timeout, cwd=ROOT)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    return r.stdout.strip().splitlines()[-1]
+
+
+def test_js_integer_kats_cpu():
+    """js/integer.js replays all 936 fhEVM KATs (cleartext test double; same 27 launches as Python)."""
+    assert _run_plain("integer_check.js").startswith("OK 936 KATs, 27 launches")
+
+
+def test_js_server_cpu():
+    """js/server.js over HTTP with the reference's request shapes (fhe.test.ts, hardhat plugin)."""
+    assert _run_plain("server_check.js").startswith("OK server")
+
+
+@pytest.mark.gpu
+def test_js_server_gpu():
+    assert _run_plain("server_check.js", "gpu", timeout=900).startswith("OK server (gpu)")
