@@ -5,7 +5,7 @@ One step = one full programmable bootstrap (blind rotate -> sample extract -> ke
 batch of 4096 independent LWE ciphertexts per GPU, P-GATE parameters (n=630, k=1, N=1024,
 PBS 2^7 x 3, KS 2^2 x 8), inputs resident in HBM before the timed region.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--cpu-sample S]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--cpu-sample S] [--preset gate|fhevm]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 Multi-GPU: weak scaling.  Rank 0 generates the key set, uploads it to its GPU and broadcasts the
@@ -17,6 +17,10 @@ The roofline figure is for the dominant kernel (blind rotation + fused sample ex
 events recorded by libtfhe_hip.so on the launch stream around every launch in the timed region;
 algorithmic bytes per PBS = 61,952,960 (BSK 61,931,520 + LWE in 5,048 + LUT 8,192 + extracted
 LWE 8,200: SURVEY §8d), peak 8.0 TB/s (MI355X HBM3E, MI355X_MICROARCH.md).
+
+--preset fhevm runs the same protocol on the production fhEVM parameter set (P-FHEVM: n=918, k=1,
+N=2048, PBS 2^23 x 1, KS 2^4 x 4, KS -> PBS; shortint messages m < 16, identity LUT) as a secondary
+line; the headline metric is P-GATE.
 
 cpu_baseline: rank 0 at N=1 only — the oracle's C restatement (oracle/, -O3, OpenMP, one PBS per
 thread) on a bounded sample of the same inputs, same keys; the sample's outputs are also
@@ -43,6 +47,9 @@ KEY_SEED = 0x7F4E0001
 INPUT_SEED = 0xC0FFEE00
 BR_BYTES_PER_PBS = 61_931_520 + 5_048 + 8_192 + 8_200   # blind-rotate kernel, key-streaming model (r = 1)
 PBS_BYTES_PER_PBS = 103_303_024                           # whole PBS incl. KSK stream
+# P-FHEVM blind rotate: BSK 918 x 2 x 2 x 2048 x 8 + small LWE in 919 x 8 + LUT 2048 x 8 + big LWE out 2049 x 8
+BR_BYTES_PER_PBS_FHEVM = 60_162_048 + 7_352 + 16_384 + 16_392
+FHEVM_MM = 16                                            # message 2 bits x carry 2 bits
 HBM_PEAK_GBS = 8000.0
 
 
@@ -64,15 +71,16 @@ def pmc_traffic(B: int):
     return None
 
 
-def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int):
+def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int, preset: int = 0,
+                 lut_host: np.ndarray = None):
     """Oracle PBS on host cores over `sample` ciphertexts of the same batch (same keys)."""
     from oracle import oracle as O
-    prm = O.params(0)
+    prm = O.params(preset)
     t = time.time()
     keys = O.Keys(prm, KEY_SEED)
     keys.bsk_ntt
     log(f"oracle keys in {time.time() - t:.1f}s")
-    lut = O.lut_constant(1024, O.MU)[None]
+    lut = O.lut_constant(1024, O.MU)[None] if lut_host is None else lut_host[None]
     sel = cts[:sample]
     O.pbs_batch(prm, keys, sel[: max(1, threads // 4)], lut, threads=threads)  # warm tables
     t = time.time()
@@ -83,7 +91,7 @@ def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int
         "unit": "PBS/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{sample} PBS of the same P-GATE batch (first {sample} ciphertexts), C oracle "
+        "sample": f"{sample} PBS of the same {'P-GATE' if preset == 0 else 'P-FHEVM'} batch (first {sample} ciphertexts), C oracle "
                   f"(oracle/tfhe_oracle.c, -O3 -march=x86-64-v3, OpenMP {threads} threads, one PBS per thread), "
                   f"{dt:.1f}s",
     }, bool(np.array_equal(ref, gpu_out[:sample]))
@@ -98,6 +106,8 @@ def main() -> int:
     ap.add_argument("--cpu-sample", type=int, default=0, help="PBS in the CPU baseline sample (0 = auto)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on GPUs; gloo only for rehearsals")
+    ap.add_argument("--preset", choices=["gate", "fhevm"], default="gate",
+                    help="gate = the BASELINE metric (P-GATE); fhevm = production fhEVM parameters (secondary line)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses device 0 (with --dist-backend gloo)")
     args = ap.parse_args()
@@ -118,7 +128,9 @@ def main() -> int:
         else:
             dist.init_process_group(args.dist_backend)
 
-    params = tfhe_amd.Params.preset(tfhe_amd.PRESET_GATE)
+    fhevm = args.preset == "fhevm"
+    params = tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM if fhevm else tfhe_amd.PRESET_GATE)
+    br_bytes = BR_BYTES_PER_PBS_FHEVM if fhevm else BR_BYTES_PER_PBS
     B = args.batch
 
     # ---- key set: generated on rank 0, broadcast once over RCCL ---------------------------------
@@ -144,10 +156,16 @@ def main() -> int:
 
     # ---- inputs: this rank's batch, encrypted on the host, resident in HBM ----------------------
     rng = np.random.default_rng(rank_batch_seed(INPUT_SEED, rank))
-    bits = rng.integers(0, 2, B).astype(bool)
-    cts = ck.encrypt_bool(bits, seed=INPUT_SEED + 1, stream0=rank * B)
+    if fhevm:
+        msgs = rng.integers(0, FHEVM_MM, B).astype(np.uint64)
+        cts = ck.encrypt(msgs, FHEVM_MM, seed=INPUT_SEED + 1, stream0=rank * B)
+        lut_host = eng.generate_accumulator(lambda m: m, FHEVM_MM)
+    else:
+        bits = rng.integers(0, 2, B).astype(bool)
+        cts = ck.encrypt_bool(bits, seed=INPUT_SEED + 1, stream0=rank * B)
+        lut_host = eng.gate_lut()
     d_in = torch.from_numpy(cts.view(np.int64)).to(dev)
-    d_lut = torch.from_numpy(eng.gate_lut().view(np.int64)).to(dev)
+    d_lut = torch.from_numpy(lut_host.view(np.int64)).to(dev)
     d_out = torch.empty_like(d_in)
     stream = torch.cuda.current_stream(dev)
 
@@ -177,7 +195,10 @@ def main() -> int:
     elapsed_max = float(t_max.item())
 
     out = d_out.cpu().numpy().view(np.uint64)
-    correct = bool(np.array_equal(ck.decrypt_bool(out), bits))
+    if fhevm:
+        correct = bool(np.array_equal(ck.decrypt(out, FHEVM_MM), msgs))
+    else:
+        correct = bool(np.array_equal(ck.decrypt_bool(out), bits))
     ok = torch.tensor([1 if correct else 0], dtype=torch.int32, device=dev)
     if world > 1:
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
@@ -185,12 +206,12 @@ def main() -> int:
     ms_per_step = elapsed_max * 1e3 / args.steps
     value = world * B * args.steps / elapsed_max
     br_avg = br_ms / max(br_n, 1)
-    achieved = B * BR_BYTES_PER_PBS / (br_avg * 1e-3) / 1e9
+    achieved = B * br_bytes / (br_avg * 1e-3) / 1e9
 
     result = None
     if rank == 0:
         result = {
-            "metric": METRIC,
+            "metric": METRIC if not fhevm else f"PBS/sec at P-FHEVM (N=2048, KS->PBS), batch={B}",
             "value": round(value, 1),
             "unit": "PBS/s",
             "n_gpus": world,
@@ -201,23 +222,27 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic: ChaCha20-seeded LWE encryptions of uniform bits (key seed 0x7F4E0001), gate LUT",
+            "data": ("synthetic: ChaCha20-seeded LWE encryptions of uniform bits (key seed 0x7F4E0001), gate LUT"
+                     if not fhevm else "synthetic: ChaCha20-seeded shortint encryptions m < 16 under the big key "
+                     "(key seed 0x7F4E0001), identity LUT"),
             "config": {
-                "workload": "P-GATE PBS (blind rotate + sample extract + keyswitch), n=630 k=1 N=1024, "
-                            f"PBS 2^7x3, KS 2^2x8, batch {B} per GPU",
+                "workload": ("P-GATE PBS (blind rotate + sample extract + keyswitch), n=630 k=1 N=1024, "
+                             f"PBS 2^7x3, KS 2^2x8, batch {B} per GPU") if not fhevm else
+                            ("P-FHEVM PBS (keyswitch + blind rotate + sample extract), n=918 k=1 N=2048, "
+                             f"PBS 2^23x1, KS 2^4x4, batch {B} per GPU"),
                 "batch_per_gpu": B,
                 "params": params.as_dict(),
                 "parallelism": f"batch-sharded x{world}, BSK/KSK RCCL broadcast once",
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "blind_rotate_kernel (+fused sample extract)",
+                "kernel": ("blind_rotate2048_kernel" if fhevm else "blind_rotate_kernel") + " (+fused sample extract)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(B),
-                "bytes_per_launch": B * BR_BYTES_PER_PBS,
+                "traffic": None if fhevm else pmc_traffic(B),
+                "bytes_per_launch": B * br_bytes,
                 "kernel_ms": round(br_avg, 3),
                 "launches": br_n,
             },
@@ -227,9 +252,10 @@ def main() -> int:
         }
         if world == 1 and not args.no_cpu:
             threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-            # ~10-20 s of CPU work: the oracle does ~3.5 PBS/s per thread at P-GATE
-            sample = args.cpu_sample or max(40 * threads, 64)
-            cb, exact = cpu_baseline(cts, out, min(sample, B), threads)
+            # ~10-20 s of CPU work: the oracle does ~3.5 PBS/s per thread at P-GATE (~1.3 at P-FHEVM)
+            sample = args.cpu_sample or (max(16 * threads, 32) if fhevm else max(40 * threads, 64))
+            cb, exact = cpu_baseline(cts, out, min(sample, B), threads, 1 if fhevm else 0,
+                                     lut_host if fhevm else None)
             result["cpu_baseline"] = cb
             result["sample_bitexact"] = exact
         print(json.dumps(result), flush=True)

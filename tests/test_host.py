@@ -49,6 +49,23 @@ def test_keygen_matches_oracle(product_keys, oracle_keys):
     assert int(sk.bsk.max()) < 0xFFFFFFFF00000001  # canonical Z_p
 
 
+def test_keygen_and_encrypt_match_oracle_fhevm(oracle_mod):
+    """P-FHEVM (N=2048, KS->PBS): keys, encryptions under the big (GLWE) key, LUTs."""
+    prm = oracle_mod.params(1)
+    ok = oracle_mod.Keys(prm, KEY_SEED)
+    ck, sk = tfhe_amd.gen_keys(tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM), KEY_SEED)
+    assert np.array_equal(ck.lwe_key, ok.lwe_key) and np.array_equal(ck.glwe_key, ok.glwe_key)
+    assert np.array_equal(sk.bsk, ok.bsk) and np.array_equal(sk.ksk, ok.ksk)
+    msgs = (np.arange(16, dtype=np.uint64) * np.uint64((1 << 63) // 16))
+    a = ck.encrypt_torus(msgs, seed=0xC0FFEE03)
+    assert a.shape == (16, 2049)
+    assert np.array_equal(a, ok.encrypt(msgs, seed=0xC0FFEE03))
+    assert np.array_equal(ck.decrypt(a, 16), np.arange(16))
+    tab = [(m * m + 3) % 16 for m in range(16)]
+    assert np.array_equal(tfhe_amd.lut_from_table(2048, 16, tab, (1 << 63) // 16),
+                          oracle_mod.lut_from_table(2048, 16, tab, (1 << 63) // 16))
+
+
 def test_encrypt_phase_matches_oracle(product_keys, oracle_keys):
     ck, _ = product_keys
     msgs = np.array([1 << 61, (1 << 64) - (1 << 61), 0, 12345], dtype=np.uint64)
@@ -86,10 +103,13 @@ def test_engine_without_gpu_raises_not_aborts():
         tfhe_amd.Engine(tfhe_amd.Params.preset(tfhe_amd.PRESET_GATE), 0)
 
 
-def test_fhevm_params_unsupported_on_device_build():
-    # P-FHEVM (N=2048, KS->PBS) is a "next" row: the device path must refuse it loudly, not compute wrong.
-    with pytest.raises(tfhe_amd.TfheError):
-        tfhe_amd.Engine(tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM), 0)
+def test_unsupported_params_refused_on_device_build():
+    # a parameter set without device kernels must be refused loudly (EUNSUPPORTED), never computed
+    p = tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM)
+    p.ks_level = 5
+    with pytest.raises(tfhe_amd.TfheError) as ei:
+        tfhe_amd.Engine(p, 0)
+    assert ei.value.code == -5
 
 
 def test_gl64_primitives_exact(tmp_path):

@@ -46,9 +46,13 @@ bool params_valid(const tfhe_params* p) {
 }
 
 // The device kernels of this build: P-GATE shape (k=1, N=1024, PBS 7x3, KS 2x8, PBS then KS).
+// the device kernels of this build: P-GATE (N = 1024, PBS -> KS) and P-FHEVM (N = 2048, KS -> PBS)
 bool params_on_device(const tfhe_params* p) {
-  return p->k == 1 && p->N == 1024 && p->pbs_base_log == 7 && p->pbs_level == 3 && p->ks_base_log == 2 &&
-         p->ks_level == 8 && p->order == 0;
+  const bool gate = p->k == 1 && p->N == 1024 && p->pbs_base_log == 7 && p->pbs_level == 3 && p->ks_base_log == 2 &&
+                    p->ks_level == 8 && p->order == 0;
+  const bool fhevm = p->k == 1 && p->N == 2048 && p->pbs_base_log == 23 && p->pbs_level == 1 &&
+                     p->ks_base_log == 4 && p->ks_level == 4 && p->order == 1;
+  return gate || fhevm;
 }
 
 // canonical psi: primitive 2N-th root of unity with psi^(2N/64) = 8 (generator 7)
@@ -147,19 +151,41 @@ void timed_end(tfhe_ctx* c, int which, hipStream_t s) {
 
 uint32_t io_dim(const tfhe_params& p) { return p.order == 0 ? p.n : p.k * p.N; }
 
-// PBS on device buffers (caller holds c->mu, device set).
+hipError_t launch_br(tfhe_ctx* c, const u64* in, size_t B, const u64* luts, const u32* idx, size_t n_lut, u64* out_big,
+                     u64* out_acc, hipStream_t s) {
+  if (c->p.N == 2048)
+    return tfhe::launch_blind_rotate_2048(in, B, (int)c->p.n, luts, idx, (int)n_lut, c->d_bsk, c->d_tw, out_big, out_acc,
+                                          s);
+  return tfhe::launch_blind_rotate(in, B, (int)c->p.n, luts, idx, (int)n_lut, c->d_bsk, c->d_tw, out_big, out_acc, s);
+}
+
+hipError_t launch_ks(tfhe_ctx* c, const u64* in_big, size_t B, u64* out, hipStream_t s) {
+  return tfhe::launch_keyswitch(in_big, B, (int)(c->p.k * c->p.N), c->d_ksk, (int)c->p.n, (int)c->p.ks_base_log,
+                                (int)c->p.ks_level, out, s);
+}
+
+// PBS on device buffers (caller holds c->mu, device set).  Order 0 (P-GATE): BR + SE -> KS;
+// order 1 (P-FHEVM): KS -> BR + SE.  Timing slot 0 = blind rotate, 1 = keyswitch.
 int pbs_device(tfhe_ctx* c, const u64* d_in, size_t B, const u64* d_luts, size_t n_lut, const u32* d_idx, u64* d_out,
                hipStream_t s) {
-  const size_t big = (size_t)c->p.k * c->p.N + 1;
-  int rc = grow((void**)&c->d_big, &c->big_cap, B * big * sizeof(u64));
+  const size_t big = (size_t)c->p.k * c->p.N + 1, small = (size_t)c->p.n + 1;
+  int rc = grow((void**)&c->d_big, &c->big_cap, B * (c->p.order == 0 ? big : small) * sizeof(u64));
   if (rc) return rc;
-  timed_begin(c, 0, s);
-  HIP_TRY(tfhe::launch_blind_rotate(d_in, B, (int)c->p.n, d_luts, d_idx, (int)n_lut, c->d_bsk, c->d_tw, c->d_big,
-                                    nullptr, s));
-  timed_end(c, 0, s);
-  timed_begin(c, 1, s);
-  HIP_TRY(tfhe::launch_keyswitch(c->d_big, B, (int)(c->p.k * c->p.N), c->d_ksk, (int)c->p.n, d_out, s));
-  timed_end(c, 1, s);
+  if (c->p.order == 0) {
+    timed_begin(c, 0, s);
+    HIP_TRY(launch_br(c, d_in, B, d_luts, d_idx, n_lut, c->d_big, nullptr, s));
+    timed_end(c, 0, s);
+    timed_begin(c, 1, s);
+    HIP_TRY(launch_ks(c, c->d_big, B, d_out, s));
+    timed_end(c, 1, s);
+  } else {
+    timed_begin(c, 1, s);
+    HIP_TRY(launch_ks(c, d_in, B, c->d_big, s));
+    timed_end(c, 1, s);
+    timed_begin(c, 0, s);
+    HIP_TRY(launch_br(c, c->d_big, B, d_luts, d_idx, n_lut, d_out, nullptr, s));
+    timed_end(c, 0, s);
+  }
   return 0;
 }
 
@@ -252,7 +278,8 @@ int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out) {
   if (!params_valid(p)) return fail(TFHE_HIP_EINVAL, "create: invalid parameters");
   if (!params_on_device(p))
     return fail(TFHE_HIP_EUNSUPPORTED,
-                "create: device kernels of this build cover k=1, N=1024, PBS 7x3, KS 2x8, PBS->KS (P-GATE); got "
+                "create: device kernels of this build cover P-GATE (k=1, N=1024, PBS 7x3, KS 2x8, PBS->KS) and "
+                "P-FHEVM (k=1, N=2048, PBS 23x1, KS 4x4, KS->PBS); got "
                 "k=%u N=%u pbs %ux%u ks %ux%u order %u",
                 p->k, p->N, p->pbs_base_log, p->pbs_level, p->ks_base_log, p->ks_level, p->order);
   int ndev = 0;
@@ -271,8 +298,9 @@ int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out) {
   // twiddle tables of the device NTT layout (pbs_kernels.hip: make_ntt_tables)
   using namespace tfhe;
   const uint32_t N = p->N;
-  std::vector<u64> tw(4 * N);
-  make_ntt_tables(canonical_psi(N), tw.data());
+  std::vector<u64> tw(N == 2048 ? ntt2048_tables_len() : 4 * N);
+  if (N == 2048) make_ntt2048_tables(canonical_psi(N), tw.data());
+  else make_ntt_tables(canonical_psi(N), tw.data());
   c->ninv = gl_pow(N, GL_P - 2);
   if (hipMalloc(&c->d_tw, tw.size() * 8) != hipSuccess)
     return cleanup(fail(TFHE_HIP_ENOMEM, "create: twiddle allocation failed"));
@@ -325,7 +353,10 @@ static int load_keys_impl(tfhe_ctx* c, const uint64_t* bsk, size_t bsk_len, cons
     tmp = (void*)bsk;
   }
   const size_t polys = bsk_len / c->p.N;
-  HIP_TRY(tfhe::launch_bsk_to_ntt((const u64*)tmp, c->d_bsk, (int)(polys / 12), c->d_tw, c->ninv, c->stream));
+  if (c->p.N == 2048)
+    HIP_TRY(tfhe::launch_bsk_to_ntt_2048((const u64*)tmp, c->d_bsk, polys, c->d_tw, c->ninv, c->stream));
+  else
+    HIP_TRY(tfhe::launch_bsk_to_ntt((const u64*)tmp, c->d_bsk, (int)(polys / 12), c->d_tw, c->ninv, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->keys = true;
   return 0;
@@ -388,8 +419,7 @@ int tfhe_hip_blind_rotate(tfhe_ctx* c, const uint64_t* lwe_in, size_t B, const u
   int rc = stage(c, {{lwe_in, B * din * 8}, {luts, n_lut * c->p.N * 8}, {lut_index, lut_index ? B * 4 : 0}}, d,
                  B * acc_len * 8);
   if (rc) return rc;
-  HIP_TRY(tfhe::launch_blind_rotate((const u64*)d[0], B, (int)c->p.n, (const u64*)d[1], (const u32*)d[2], (int)n_lut,
-                                    c->d_bsk, c->d_tw, nullptr, (u64*)d[3], c->stream));
+  HIP_TRY(launch_br(c, (const u64*)d[0], B, (const u64*)d[1], (const u32*)d[2], n_lut, nullptr, (u64*)d[3], c->stream));
   HIP_TRY(hipMemcpyAsync(acc_out, d[3], B * acc_len * 8, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return 0;
@@ -404,7 +434,8 @@ int tfhe_hip_sample_extract(tfhe_ctx* c, const uint64_t* acc, size_t B, uint64_t
   std::vector<void*> d;
   int rc = stage(c, {{acc, B * acc_len * 8}}, d, B * big * 8);
   if (rc) return rc;
-  HIP_TRY(tfhe::launch_sample_extract((const u64*)d[0], B, (u64*)d[1], c->stream));
+  if (c->p.N == 2048) HIP_TRY(tfhe::launch_sample_extract_2048((const u64*)d[0], B, (u64*)d[1], c->stream));
+  else HIP_TRY(tfhe::launch_sample_extract((const u64*)d[0], B, (u64*)d[1], c->stream));
   HIP_TRY(hipMemcpyAsync(out, d[1], B * big * 8, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return 0;
@@ -420,8 +451,7 @@ int tfhe_hip_keyswitch(tfhe_ctx* c, const uint64_t* in, size_t B, uint64_t* out)
   std::vector<void*> d;
   int rc = stage(c, {{in, B * big * 8}}, d, B * small * 8);
   if (rc) return rc;
-  HIP_TRY(tfhe::launch_keyswitch((const u64*)d[0], B, (int)(c->p.k * c->p.N), c->d_ksk, (int)c->p.n, (u64*)d[1],
-                                 c->stream));
+  HIP_TRY(launch_ks(c, (const u64*)d[0], B, (u64*)d[1], c->stream));
   HIP_TRY(hipMemcpyAsync(out, d[1], B * small * 8, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return 0;
@@ -438,8 +468,13 @@ static int ntt_impl(tfhe_ctx* c, uint64_t* polys, size_t count, bool inverse) {
   std::vector<void*> d;
   int rc = stage(c, {{polys, bytes}}, d, 0);
   if (rc) return rc;
-  if (inverse) HIP_TRY(tfhe::launch_ntt_inv((u64*)d[0], count, c->d_tw, c->ninv, c->stream));
-  else HIP_TRY(tfhe::launch_ntt_fwd((u64*)d[0], count, c->d_tw, c->stream));
+  if (c->p.N == 2048) {
+    if (inverse) HIP_TRY(tfhe::launch_ntt2048_inv((u64*)d[0], count, c->d_tw, c->ninv, c->stream));
+    else HIP_TRY(tfhe::launch_ntt2048_fwd((u64*)d[0], count, c->d_tw, c->stream));
+  } else {
+    if (inverse) HIP_TRY(tfhe::launch_ntt_inv((u64*)d[0], count, c->d_tw, c->ninv, c->stream));
+    else HIP_TRY(tfhe::launch_ntt_fwd((u64*)d[0], count, c->d_tw, c->stream));
+  }
   HIP_TRY(hipMemcpyAsync(polys, d[0], bytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return 0;
@@ -450,6 +485,7 @@ int tfhe_hip_ntt_inv(tfhe_ctx* c, uint64_t* polys, size_t count) { return ntt_im
 
 int tfhe_hip_nand(tfhe_ctx* c, const uint64_t* c1, const uint64_t* c2, size_t B, uint64_t* out) {
   if (!c || (B && (!c1 || !c2 || !out))) return fail(TFHE_HIP_EINVAL, "nand: bad arguments");
+  if (c->p.order != 0) return fail(TFHE_HIP_EUNSUPPORTED, "nand: gate bootstrapping needs a PBS->KS (small-key) parameter set");
   if (B == 0) return 0;
   const size_t dim = (size_t)c->p.n + 1;
   std::vector<u64> in(B * dim), lut(c->p.N);

@@ -12,7 +12,21 @@ hipError_t launch_bsk_to_ntt(const u64* bsk_std, u64* bsk_ntt, int n, const u64*
 hipError_t launch_blind_rotate(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index, int n_lut,
                                const u64* bsk, const u64* tw, u64* out_big, u64* out_acc, hipStream_t s);
 hipError_t launch_sample_extract(const u64* acc, size_t B, u64* out, hipStream_t s);
-hipError_t launch_keyswitch(const u64* in_big, size_t B, int big_dim, const u64* ksk, int n, u64* out, hipStream_t s);
+hipError_t launch_keyswitch(const u64* in_big, size_t B, int big_dim, const u64* ksk, int n, int base_log, int levels,
+                           u64* out, hipStream_t s);
 hipError_t launch_ntt_fwd(u64* polys, size_t count, const u64* tw, hipStream_t s);
 hipError_t launch_ntt_inv(u64* polys, size_t count, const u64* tw, u64 ninv, hipStream_t s);
+
+// N = 2048 (P-FHEVM, pbs_n2048.hip): tables = [1024-point tables of psi^2 (4096) | combine
+// twiddles psi^(2j+1) (2048) | inverses (2048)]
+void make_ntt2048_tables(u64 psi, u64* tw);
+size_t ntt2048_tables_len();
+hipError_t launch_bsk_to_ntt_2048(const u64* bsk_std, u64* bsk_ntt, size_t polys, const u64* tw, u64 ninv,
+                                  hipStream_t s);
+hipError_t launch_blind_rotate_2048(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
+                                   int n_lut, const u64* bsk, const u64* tw, u64* out_big, u64* out_acc,
+                                   hipStream_t s);
+hipError_t launch_sample_extract_2048(const u64* acc, size_t B, u64* out, hipStream_t s);
+hipError_t launch_ntt2048_fwd(u64* polys, size_t count, const u64* tw, hipStream_t s);
+hipError_t launch_ntt2048_inv(u64* polys, size_t count, const u64* tw, u64 ninv, hipStream_t s);
 }  // namespace tfhe

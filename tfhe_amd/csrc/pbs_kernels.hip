@@ -17,15 +17,11 @@
 #include <hip/hip_runtime.h>
 
 #include "gl64.h"
+#include "ntt1024.h"
 #include "ntt16.h"
 #include "pbs_kernels.h"
 
 namespace tfhe {
-
-constexpr int N1K = 1024;
-constexpr int T1_STRIDE = 68;              // transpose-1 row stride (u64): conflict-free reads/writes
-constexpr int T_LDS = 16 * T1_STRIDE;      // u64 of LDS scratch per wavefront (>= 1024)
-constexpr int TW_U64 = 4 * N1K;            // twiddle tables: tw1 fwd, tw2 fwd, tw1 inv, tw2 inv
 
 // round(x * 2048 / 2^64) mod 2048  (modulus switch)
 __device__ __forceinline__ int ms2048(u64 x) { return (int)((((x >> 52) + 1) >> 1) & 2047u); }
@@ -57,48 +53,6 @@ __device__ __forceinline__ u32 decomp_7x3(u64 x) {
   return packed;
 }
 
-// Ordering of one wavefront's own LDS writes before its reads of another lane's data (LDS runs a
-// wave's operations in order; this stops the compiler moving them and retires the writes).
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// ---------------------------------------------------------------------------------------------
-// 1024-point negacyclic NTT of the wavefront's polynomial (ntt16.h for the factorization).
-// tw points at the 4 tables [tw1 fwd | tw2 fwd | tw1 inv | tw2 inv] (LDS or global).
-// Transpose 1: lane L, slot e -> T[e][L] (stride 68) -> lane (e1 = L >> 2, i3 = L & 3) reads
-//              T[e1][4 e2 + i3].  Transpose 2: lane L2, slot f -> T[f][L2 ^ (f >> 2 & 3)]
-//              (XOR swizzle) -> lane (e1, fhi = L & 3) reads element 4 flo + i3 from
-//              T[4 fhi + flo][(4 e1 + i3) ^ fhi].  Both are bank-conflict free.
-__device__ __forceinline__ void ntt1024_fwd_tail(u64 (&x)[16], u64* T, int lane, const u64* tw) {
-  const int e1 = lane >> 2, q = lane & 3;
-#pragma unroll
-  for (int e = 0; e < 16; e++) x[e] = gl_mul(x[e], tw[64 * e + lane]);
-#pragma unroll
-  for (int e = 0; e < 16; e++) T[e * T1_STRIDE + lane] = x[e];
-  wave_lds_sync();
-#pragma unroll
-  for (int e = 0; e < 16; e++) x[e] = T[e1 * T1_STRIDE + 4 * e + q];
-  wave_lds_sync();
-  cyc16_fwd(x);
-#pragma unroll
-  for (int f = 1; f < 16; f++) x[f] = gl_mul(x[f], tw[N1K + 64 * f + lane]);  // tw2 column f = 0 is 1
-#pragma unroll
-  for (int f = 0; f < 16; f++) T[f * 64 + (lane ^ ((f >> 2) & 3))] = x[f];
-  wave_lds_sync();
-#pragma unroll
-  for (int e = 0; e < 16; e++) x[e] = T[(4 * q + (e >> 2)) * 64 + ((4 * e1 + (e & 3)) ^ q)];
-  wave_lds_sync();
-  cyc4x4_fwd(x);
-}
-
-__device__ __forceinline__ void ntt1024_fwd(u64 (&x)[16], u64* T, int lane, const u64* tw) {
-  nega16_fwd(x);
-  ntt1024_fwd_tail(x, T, lane, tw);
-}
-
 // Forward NTT of a digit polynomial (|d| <= 64, byte l of dig[e] holds d + 64): the first
 // pass-1 stage (span 8, twiddle 2^48) is exact in int64 (|d + 2^48 d'| < 2^55): no reduction.
 __device__ __forceinline__ void ntt1024_fwd_digits(const u32 (&dig)[16], int l, u64 (&x)[16], u64* T, int lane,
@@ -113,30 +67,6 @@ __device__ __forceinline__ void ntt1024_fwd_digits(const u32 (&dig)[16], int l, 
   }
   nega16_fwd_from4(x);
   ntt1024_fwd_tail(x, T, lane, tw);
-}
-
-// Inverse, x 1024 (the 1/N is folded into the BSK): NTT layout in, natural layout out.
-__device__ __forceinline__ void ntt1024_inv(u64 (&x)[16], u64* T, int lane, const u64* tw) {
-  const int e1 = lane >> 2, q = lane & 3;
-  cyc4x4_inv(x);
-#pragma unroll
-  for (int e = 0; e < 16; e++) T[(4 * q + (e >> 2)) * 64 + ((4 * e1 + (e & 3)) ^ q)] = x[e];
-  wave_lds_sync();
-#pragma unroll
-  for (int f = 0; f < 16; f++) x[f] = T[f * 64 + (lane ^ ((f >> 2) & 3))];
-  wave_lds_sync();
-#pragma unroll
-  for (int f = 1; f < 16; f++) x[f] = gl_mul(x[f], tw[3 * N1K + 64 * f + lane]);  // f = 0 is 1
-  cyc16_inv(x);
-#pragma unroll
-  for (int e = 0; e < 16; e++) T[e1 * T1_STRIDE + 4 * e + q] = x[e];
-  wave_lds_sync();
-#pragma unroll
-  for (int e = 0; e < 16; e++) x[e] = T[e * T1_STRIDE + lane];
-  wave_lds_sync();
-#pragma unroll
-  for (int e = 0; e < 16; e++) x[e] = gl_mul(x[e], tw[2 * N1K + 64 * e + lane]);
-  nega16_inv(x);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -308,31 +238,34 @@ __global__ void sample_extract_kernel(const u64* __restrict__ acc, size_t B, u64
 }
 
 // ---------------------------------------------------------------------------------------------
-// Keyswitch kN -> n, base 2^2 x 8 levels (tfhe-rs SignedDecomposer digits in {-2..2}).
-// Workgroup = 64 output columns x 64 ciphertexts; wave w owns ciphertexts 16w..16w+15 of the tile.
-constexpr int KS_LEVELS = 8;
+// Keyswitch big -> n (tfhe-rs SignedDecomposer digits): P-GATE base 2^2 x 8 levels (digits in
+// {-2..2}), P-FHEVM base 2^4 x 4 (digits in [-8, 8]).  Workgroup = 64 output columns x 64
+// ciphertexts; wave w owns ciphertexts 16w..16w+15 of the tile; digits staged in LDS as bytes.
 constexpr int KS_TILE_CT = 64;
 constexpr int KS_JCHUNK = 32;
 
-__device__ __forceinline__ unsigned long long ks_digits_2x8(u64 x) {
-  // closest representable at 16 bits, then balanced base-4 digits; byte r = level r (0 = MSB)
-  u32 state = (u32)(((x >> 47) + 1) >> 1) & 0xFFFFu;
+// closest representable at BL*LV bits, then balanced base-2^BL digits; byte r = level r (0 = MSB)
+template <int BL, int LV>
+__device__ __forceinline__ unsigned long long ks_digits(u64 x) {
+  constexpr int P = BL * LV;
+  u32 state = (u32)(((x >> (63 - P)) + 1) >> 1) & (u32)((1ull << P) - 1);
   unsigned long long packed = 0;
 #pragma unroll
-  for (int l = KS_LEVELS - 1; l >= 0; l--) {
-    const u32 res = state & 3u;
-    state >>= 2;
-    const u32 carry = ((((res - 1u) | state) & res) >> 1) & 1u;
+  for (int l = LV - 1; l >= 0; l--) {
+    const u32 res = state & ((1u << BL) - 1);
+    state >>= BL;
+    const u32 carry = ((((res - 1u) | state) & res) >> (BL - 1)) & 1u;
     state += carry;
-    const int d = (int)res - (int)(carry << 2);
+    const int d = (int)res - (int)(carry << BL);
     packed |= (unsigned long long)(unsigned char)(signed char)d << (8 * l);
   }
   return packed;
 }
 
+template <int BL, int LV>
 __global__ __launch_bounds__(256) void keyswitch_kernel(const u64* __restrict__ in_big, int big_dim, int B,
                                                         const u64* __restrict__ ksk, int n, u64* __restrict__ out) {
-  __shared__ unsigned long long dig[KS_TILE_CT][KS_JCHUNK];  // 16 KB: 8 signed byte digits per (ct, j)
+  __shared__ unsigned long long dig[KS_TILE_CT][KS_JCHUNK];  // 16 KB: LV signed byte digits per (ct, j)
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int col = blockIdx.x * 64 + lane;
   const int ct0 = blockIdx.y * KS_TILE_CT;
@@ -343,19 +276,19 @@ __global__ __launch_bounds__(256) void keyswitch_kernel(const u64* __restrict__ 
     for (int q = tid; q < KS_TILE_CT * KS_JCHUNK; q += 256) {
       const int c = q / KS_JCHUNK, jj = q % KS_JCHUNK, b = ct0 + c;
       const u64 v = (b < B) ? in_big[(size_t)b * (big_dim + 1) + j0 + jj] : 0ull;
-      dig[c][jj] = ks_digits_2x8(v);
+      dig[c][jj] = ks_digits<BL, LV>(v);
     }
     __syncthreads();
     if (col <= n) {
       for (int jj = 0; jj < KS_JCHUNK; jj++) {
-        u64 kv[KS_LEVELS];
+        u64 kv[LV];
 #pragma unroll
-        for (int r = 0; r < KS_LEVELS; r++) kv[r] = ksk[((size_t)(j0 + jj) * KS_LEVELS + r) * (n + 1) + col];
+        for (int r = 0; r < LV; r++) kv[r] = ksk[((size_t)(j0 + jj) * LV + r) * (n + 1) + col];
 #pragma unroll
         for (int q = 0; q < 16; q++) {
           const unsigned long long dd = dig[w * 16 + q][jj];
 #pragma unroll
-          for (int r = 0; r < KS_LEVELS; r++) {
+          for (int r = 0; r < LV; r++) {
             const long long d = (long long)(signed char)(dd >> (8 * r));
             acc[q] -= (u64)d * kv[r];
           }
@@ -444,10 +377,17 @@ hipError_t launch_sample_extract(const u64* acc, size_t B, u64* out, hipStream_t
   return hipGetLastError();
 }
 
-hipError_t launch_keyswitch(const u64* in_big, size_t B, int big_dim, const u64* ksk, int n, u64* out, hipStream_t s) {
+hipError_t launch_keyswitch(const u64* in_big, size_t B, int big_dim, const u64* ksk, int n, int base_log, int levels,
+                           u64* out, hipStream_t s) {
   if (B == 0) return hipSuccess;
+  if (big_dim % KS_JCHUNK) return hipErrorInvalidValue;
   dim3 grid((unsigned)((n + 1 + 63) / 64), (unsigned)((B + KS_TILE_CT - 1) / KS_TILE_CT));
-  hipLaunchKernelGGL(keyswitch_kernel, grid, dim3(256), 0, s, in_big, big_dim, (int)B, ksk, n, out);
+  if (base_log == 2 && levels == 8)
+    hipLaunchKernelGGL((keyswitch_kernel<2, 8>), grid, dim3(256), 0, s, in_big, big_dim, (int)B, ksk, n, out);
+  else if (base_log == 4 && levels == 4)
+    hipLaunchKernelGGL((keyswitch_kernel<4, 4>), grid, dim3(256), 0, s, in_big, big_dim, (int)B, ksk, n, out);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
