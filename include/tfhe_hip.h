@@ -67,6 +67,12 @@ uint32_t tfhe_hip_io_dim(const tfhe_params* p);
  * Streams: LWE key 1, GLWE key 2, BSK_i 0x1000+i, KSK_j 0x100000+j (ChaCha20). */
 int tfhe_hip_keygen(const tfhe_params* p, uint64_t seed, uint64_t* lwe_key, uint64_t* glwe_key,
                     uint64_t* bsk /* nullable */, uint64_t* ksk /* nullable */);
+/* BSK / KSK (standard domain) for GIVEN binary secret keys — the server-key half of keygen, for key
+ * material ingested from tfhe-rs (the packages/kms loader role, SURVEY §8f f3: the ClientKey of
+ * sdk/relayer/src/test/keys/privateKey.bin; tfhe_amd/keyio.py parses it).  Same ChaCha streams as
+ * tfhe_hip_keygen.  EINVAL if a key word is not 0/1. */
+int tfhe_hip_server_keygen(const tfhe_params* p, uint64_t seed, const uint64_t* lwe_key, const uint64_t* glwe_key,
+                           uint64_t* bsk /* nullable */, uint64_t* ksk /* nullable */);
 /* Encrypt count torus messages; ciphertext q uses ChaCha stream (stream0 + q).
  * Replaces the encrypt path of packages/luxfhejs/src/index.ts:127-141 (server-side /encrypt). */
 int tfhe_hip_lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, uint64_t seed,

@@ -140,6 +140,21 @@ class Keys:
                     _p(self.bsk) if with_bsk else None, _p(self.ksk) if with_ksk else None)
         self._bsk_ntt = None
 
+    @classmethod
+    def from_secret(cls, prm: Params, seed: int, lwe_key: np.ndarray, glwe_key: np.ndarray) -> "Keys":
+        """Server keys for given secret keys (or_server_keygen; same streams as the seeded keygen)."""
+        k = cls.__new__(cls)
+        k.prm, k.seed = prm, seed
+        k.lwe_key = np.ascontiguousarray(lwe_key, dtype=np.uint64).copy()
+        k.glwe_key = np.ascontiguousarray(glwe_key, dtype=np.uint64).copy()
+        L = lib()
+        k.bsk = np.zeros(L.or_bsk_len(ctypes.byref(prm)), dtype=np.uint64)
+        k.ksk = np.zeros(L.or_ksk_len(ctypes.byref(prm)), dtype=np.uint64)
+        L.or_server_keygen(ctypes.byref(prm), ctypes.c_uint64(seed), _p(k.lwe_key), _p(k.glwe_key), _p(k.bsk),
+                           _p(k.ksk))
+        k._bsk_ntt = None
+        return k
+
     @property
     def bsk_ntt(self) -> np.ndarray:
         if self._bsk_ntt is None:

@@ -376,12 +376,18 @@ static void lwe_encrypt_one(uint32_t dim, const uint64_t* key, int32_t noise_log
 
 void or_keygen(const or_params* p, uint64_t seed, uint64_t* lwe_key, uint64_t* glwe_key, uint64_t* bsk,
                uint64_t* ksk) {
-  const uint32_t n = p->n, k = p->k, N = p->N, L = p->pbs_level;
   or_rng r;
   or_rng_init(&r, seed, 1);
-  for (uint32_t i = 0; i < n; i++) lwe_key[i] = or_rng_u64(&r) & 1;
+  for (uint32_t i = 0; i < p->n; i++) lwe_key[i] = or_rng_u64(&r) & 1;
   or_rng_init(&r, seed, 2);
-  for (uint32_t i = 0; i < k * N; i++) glwe_key[i] = or_rng_u64(&r) & 1;
+  for (uint32_t i = 0; i < p->k * p->N; i++) glwe_key[i] = or_rng_u64(&r) & 1;
+  or_server_keygen(p, seed, lwe_key, glwe_key, bsk, ksk);
+}
+
+/* server keys for given binary secret keys (ingested tfhe-rs ClientKey; same streams as or_keygen) */
+void or_server_keygen(const or_params* p, uint64_t seed, const uint64_t* lwe_key, const uint64_t* glwe_key,
+                      uint64_t* bsk, uint64_t* ksk) {
+  const uint32_t n = p->n, k = p->k, N = p->N, L = p->pbs_level;
   if (bsk) {
     const size_t row = (size_t)(k + 1) * N, per_i = (size_t)(k + 1) * L * row;
 #pragma omp parallel for schedule(dynamic, 4)

@@ -89,6 +89,8 @@ size_t or_ksk_len(const or_params* p); /* kN*l_ks*(n+1) u64, layout [j][r][0..n]
 /* ---- keys & encryption --------------------------------------------------------------- */
 void or_keygen(const or_params* p, uint64_t seed, uint64_t* lwe_key /*n*/, uint64_t* glwe_key /*kN*/,
                uint64_t* bsk /*nullable*/, uint64_t* ksk /*nullable*/);
+void or_server_keygen(const or_params* p, uint64_t seed, const uint64_t* lwe_key, const uint64_t* glwe_key,
+                      uint64_t* bsk, uint64_t* ksk);
 /* ct q of the batch uses ChaCha stream (stream0 + q). dim = LWE dimension of key. */
 void or_lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, uint64_t seed,
                     uint64_t stream0, const uint64_t* msgs, size_t count, uint64_t* out);

@@ -81,6 +81,7 @@ ABI_SYMBOLS = (
     "tfhe_hip_load_keys_device", "tfhe_hip_pbs", "tfhe_hip_pbs_async", "tfhe_hip_blind_rotate",
     "tfhe_hip_sample_extract", "tfhe_hip_keyswitch", "tfhe_hip_ntt_fwd", "tfhe_hip_ntt_inv", "tfhe_hip_nand",
     "tfhe_hip_sync", "tfhe_hip_timing_enable", "tfhe_hip_timing_reset", "tfhe_hip_timing_stats",
+    "tfhe_hip_server_keygen",
 )
 
 
@@ -111,6 +112,7 @@ def lib():
         L.tfhe_hip_io_dim.restype = ctypes.c_uint32
         L.tfhe_hip_destroy.restype = None
         L.tfhe_hip_keygen.argtypes = [ctypes.c_void_p, ctypes.c_uint64, _U64P, _U64P, _U64P, _U64P]
+        L.tfhe_hip_server_keygen.argtypes = [ctypes.c_void_p, ctypes.c_uint64, _U64P, _U64P, _U64P, _U64P]
         L.tfhe_hip_lwe_encrypt.argtypes = [ctypes.c_uint32, _U64P, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint64,
                                            _U64P, ctypes.c_size_t, _U64P]
         L.tfhe_hip_lwe_phase.argtypes = [ctypes.c_uint32, _U64P, _U64P, ctypes.c_size_t, _U64P]
@@ -236,6 +238,17 @@ def gen_keys(params: Optional[Params] = None, seed: int = 0x7F4E0001, with_serve
                              _u64(bsk) if bsk is not None else None, _u64(ksk) if ksk is not None else None))
     ck = ClientKey(params, seed, lwe, glwe)
     return ck, (ServerKey(params, bsk, ksk) if with_server_key else None)
+
+
+def server_keygen(ck: "ClientKey", seed: int = 0x7F4E0001) -> ServerKey:
+    """BSK / KSK for the secret keys of ``ck`` (e.g. a tfhe-rs ClientKey ingested by tfhe_amd.keyio)."""
+    p = ck.params
+    L = lib()
+    bsk = np.zeros(L.tfhe_hip_bsk_len(ctypes.byref(p)), dtype=np.uint64)
+    ksk = np.zeros(L.tfhe_hip_ksk_len(ctypes.byref(p)), dtype=np.uint64)
+    lwe, glwe = _c_u64(ck.lwe_key), _c_u64(ck.glwe_key)
+    _check(L.tfhe_hip_server_keygen(ctypes.byref(p), seed, _u64(lwe), _u64(glwe), _u64(bsk), _u64(ksk)))
+    return ServerKey(p, bsk, ksk)
 
 
 def lut_constant(N: int, torus_value: int) -> np.ndarray:

@@ -244,6 +244,17 @@ int tfhe_hip_keygen(const tfhe_params* p, uint64_t seed, uint64_t* lwe_key, uint
   return 0;
 }
 
+int tfhe_hip_server_keygen(const tfhe_params* p, uint64_t seed, const uint64_t* lwe_key, const uint64_t* glwe_key,
+                           uint64_t* bsk, uint64_t* ksk) {
+  if (!params_valid(p) || !lwe_key || !glwe_key) return fail(TFHE_HIP_EINVAL, "server_keygen: bad arguments");
+  for (uint32_t i = 0; i < p->n; i++)
+    if (lwe_key[i] > 1) return fail(TFHE_HIP_EINVAL, "server_keygen: lwe_key[%u] is not binary", i);
+  for (uint32_t i = 0; i < p->k * p->N; i++)
+    if (glwe_key[i] > 1) return fail(TFHE_HIP_EINVAL, "server_keygen: glwe_key[%u] is not binary", i);
+  tfhe::client::server_keygen(*p, seed, lwe_key, glwe_key, bsk, ksk);
+  return 0;
+}
+
 int tfhe_hip_lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, uint64_t seed, uint64_t stream0,
                          const uint64_t* msgs, size_t count, uint64_t* out) {
   if (!dim || !key || (count && (!msgs || !out))) return fail(TFHE_HIP_EINVAL, "lwe_encrypt: bad arguments");

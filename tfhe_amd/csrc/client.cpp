@@ -176,6 +176,11 @@ void keygen(const tfhe_params& p, uint64_t seed, uint64_t* lwe_key, uint64_t* gl
     ChaCha r(seed, 2);
     for (uint32_t i = 0; i < p.k * p.N; i++) glwe_key[i] = r.next() & 1;
   }
+  server_keygen(p, seed, lwe_key, glwe_key, bsk, ksk);
+}
+
+void server_keygen(const tfhe_params& p, uint64_t seed, const uint64_t* lwe_key, const uint64_t* glwe_key,
+                   uint64_t* bsk, uint64_t* ksk) {
   if (bsk) {
     const size_t row = (size_t)(p.k + 1) * p.N, per_i = (size_t)(p.k + 1) * p.pbs_level * row;
     parallel_for((int64_t)p.n, [&](int64_t i) {
