@@ -125,6 +125,12 @@ int tfhe_hip_ntt_inv(tfhe_ctx* ctx, uint64_t* polys, size_t count);
 int tfhe_hip_nand(tfhe_ctx* ctx, const uint64_t* c1, const uint64_t* c2, size_t B, uint64_t* out);
 
 /* Wait for all work on the ctx stream. */
+/* Batches of at most max_batch ciphertexts run the latency blind-rotate kernel (one ciphertext per
+ * workgroup, ~5x lower PBS latency: the lockstep levels of integer circuits, single /evaluate
+ * requests — packages/luxfhejs/src/index.ts:56-141 call patterns); larger batches the throughput
+ * kernel.  Default 1024 (the measured crossover on MI355X: 55 vs 61 ms at B = 1024, 69 vs 62 at 1280;
+ * tools/latency_sweep.py); 0 disables the latency kernel.  P-GATE only. */
+int tfhe_hip_set_latency_batch(tfhe_ctx* ctx, size_t max_batch);
 int tfhe_hip_sync(tfhe_ctx* ctx);
 /* Per-kernel device timing (HIP events recorded on the launch stream around every blind-rotate /
  * keyswitch launch).  reset clears the record; stats waits for the recorded events and returns the

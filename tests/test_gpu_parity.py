@@ -191,3 +191,27 @@ def test_device_resident_async_and_device_keys(engine, product_keys):
     torch.cuda.synchronize()
     assert np.array_equal(d_out.cpu().numpy().view(np.uint64), ref)
     eng2.close()
+
+
+@pytest.mark.parametrize("B", [1, 37, 300])
+def test_latency_and_batch_kernels_agree(engine, product_keys, oracle_mod, gate_params, oracle_keys, B):
+    """The latency kernel (one ciphertext per workgroup) and the batch kernel (8 per workgroup) are
+    bit-identical, and both equal the oracle on a sample."""
+    ck, _ = product_keys
+    rng = np.random.default_rng(B)
+    msgs = rng.integers(0, 8, B).astype(np.uint64) * np.uint64(1 << 60)
+    cts = ck.encrypt_torus(msgs, seed=0xC0FFEE30 + B)
+    lut = oracle_mod.lut_from_table(1024, 8, [(5 * m + 3) % 8 for m in range(8)], 1 << 60)
+    try:
+        engine.set_latency_batch(0)
+        acc_b = engine.blind_rotate(cts, lut)
+        out_b = engine.pbs(cts, lut)
+        engine.set_latency_batch(1 << 20)
+        acc_l = engine.blind_rotate(cts, lut)
+        out_l = engine.pbs(cts, lut)
+    finally:
+        engine.set_latency_batch(1024)
+    assert np.array_equal(acc_l, acc_b)
+    assert np.array_equal(out_l, out_b)
+    i = B // 2
+    assert np.array_equal(acc_l[i], oracle_mod.blind_rotate(gate_params, oracle_keys, cts[i], lut))

@@ -81,7 +81,7 @@ ABI_SYMBOLS = (
     "tfhe_hip_load_keys_device", "tfhe_hip_pbs", "tfhe_hip_pbs_async", "tfhe_hip_blind_rotate",
     "tfhe_hip_sample_extract", "tfhe_hip_keyswitch", "tfhe_hip_ntt_fwd", "tfhe_hip_ntt_inv", "tfhe_hip_nand",
     "tfhe_hip_sync", "tfhe_hip_timing_enable", "tfhe_hip_timing_reset", "tfhe_hip_timing_stats",
-    "tfhe_hip_server_keygen",
+    "tfhe_hip_server_keygen", "tfhe_hip_set_latency_batch",
 )
 
 
@@ -393,6 +393,10 @@ class Engine:
 
     def sync(self) -> None:
         _check(lib().tfhe_hip_sync(self._h))
+
+    def set_latency_batch(self, max_batch: int) -> None:
+        """Batches up to ``max_batch`` use the latency blind-rotate kernel (0: always the batch kernel)."""
+        _check(lib().tfhe_hip_set_latency_batch(self._h, ctypes.c_size_t(max_batch)))
 
     # -- timing (HIP events around each kernel launch) -----------------------------------------
     def timing(self, enable: bool = True) -> None:

@@ -81,6 +81,7 @@ struct tfhe_ctx {
   u64* d_tw = nullptr;  // 4 x 1024 twiddle tables of the device NTT layout
   u64 ninv = 0;
   bool keys = false;
+  size_t lat_max = 1024;  // batches up to this size use the latency blind-rotate kernel (P-GATE)
   // workspaces
   u64* d_big = nullptr;
   size_t big_cap = 0;  // u64 elements
@@ -156,7 +157,8 @@ hipError_t launch_br(tfhe_ctx* c, const u64* in, size_t B, const u64* luts, cons
   if (c->p.N == 2048)
     return tfhe::launch_blind_rotate_2048(in, B, (int)c->p.n, luts, idx, (int)n_lut, c->d_bsk, c->d_tw, out_big, out_acc,
                                           s);
-  return tfhe::launch_blind_rotate(in, B, (int)c->p.n, luts, idx, (int)n_lut, c->d_bsk, c->d_tw, out_big, out_acc, s);
+  return tfhe::launch_blind_rotate(in, B, (int)c->p.n, luts, idx, (int)n_lut, c->d_bsk, c->d_tw, out_big, out_acc, s,
+                                   c->lat_max);
 }
 
 hipError_t launch_ks(tfhe_ctx* c, const u64* in_big, size_t B, u64* out, hipStream_t s) {
@@ -507,6 +509,13 @@ int tfhe_hip_nand(tfhe_ctx* c, const uint64_t* c1, const uint64_t* c2, size_t B,
   }
   tfhe::client::lut_constant(c->p.N, mu, lut.data());
   return tfhe_hip_pbs(c, in.data(), B, lut.data(), 1, nullptr, out);
+}
+
+int tfhe_hip_set_latency_batch(tfhe_ctx* c, size_t max_batch) {
+  if (!c) return fail(TFHE_HIP_EINVAL, "set_latency_batch: null ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->lat_max = max_batch;
+  return 0;
 }
 
 int tfhe_hip_sync(tfhe_ctx* c) {

@@ -9,8 +9,11 @@ namespace tfhe {
 // 4 x 1024 twiddle tables of the device NTT layout, for the canonical psi (psi^32 = 8).
 void make_ntt_tables(u64 psi, u64* tw);
 hipError_t launch_bsk_to_ntt(const u64* bsk_std, u64* bsk_ntt, int n, const u64* tw, u64 ninv, hipStream_t s);
+// batches of at most latency_max_batch ciphertexts use the latency kernel (one ciphertext per
+// workgroup); larger ones the batch kernel (8 ciphertexts per workgroup)
 hipError_t launch_blind_rotate(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index, int n_lut,
-                               const u64* bsk, const u64* tw, u64* out_big, u64* out_acc, hipStream_t s);
+                               const u64* bsk, const u64* tw, u64* out_big, u64* out_acc, hipStream_t s,
+                               size_t latency_max_batch = 0);
 hipError_t launch_sample_extract(const u64* acc, size_t B, u64* out, hipStream_t s);
 hipError_t launch_keyswitch(const u64* in_big, size_t B, int big_dim, const u64* ksk, int n, int base_log, int levels,
                            u64* out, hipStream_t s);

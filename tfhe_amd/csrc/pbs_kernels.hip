@@ -224,6 +224,108 @@ __global__ __launch_bounds__(BR_THREADS, 1) void blind_rotate_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
+// Latency-mode blind rotation: ONE ciphertext per workgroup of 8 wavefronts (small batches: the
+// integer circuits' lockstep levels, single /evaluate requests).  Per CMUX:
+//   A  waves 0..5: wave w = (c, l) rotates + decomposes accumulator polynomial c (LDS), takes
+//      digit level l and runs its forward NTT -> F[w]                       (6 NTTs in parallel)
+//   B  all 8 waves: pointwise MAC out_j = sum_w F[w] (.) BSK_i[w][j] over a quarter of the slots
+//      each (j = wave >> 2), BSK read straight from L2 (each word once per workgroup) -> O[j]
+//   C  waves 0, 1: inverse NTT of O[j], acc_j += ..., written back to A[j]   (2 NTTs in parallel)
+// Three barriers per CMUX; the critical path is ~2 forward + 1 inverse NTT instead of 6 + 2, so a
+// PBS completes ~5x sooner than in the batch kernel (which is faster per PBS once >~1.3k
+// ciphertexts fill the GPU: the host picks the kernel by batch size).  LDS: A 16 KB, F 48 KB,
+// 6 NTT scratch areas 52 KB (O aliases scratch 2..3, dead after phase A), twiddles 32 KB = 148 KB.
+constexpr int LAT_THREADS = 512;
+
+struct LatShared {
+  u64 A[2][N1K];
+  u64 F[6][N1K];
+  u64 T[6][T_LDS];
+  u64 tw[TW_U64];
+};
+
+template <bool WRITE_ACC, bool WRITE_BIG>
+__global__ __launch_bounds__(LAT_THREADS, 1) void blind_rotate_lat_kernel(
+    const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
+    int n_lut, const u64* __restrict__ bsk, const u64* __restrict__ tw_g, u64* __restrict__ out_big,
+    u64* __restrict__ out_acc) {
+  __shared__ __attribute__((aligned(16))) LatShared sh;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t b = blockIdx.x;
+  const u64* ct = lwe_in + b * (size_t)(n + 1);
+  u64* O = sh.T[2];  // 2 x 1024 u64 alias of scratch areas 2 and 3
+
+  for (int q = threadIdx.x; q < TW_U64; q += LAT_THREADS) sh.tw[q] = tw_g[q];
+  {
+    int li = lut_index ? (int)lut_index[b] : 0;
+    li = (li < 0 || li >= n_lut) ? 0 : li;
+    const u64* lut = luts + (size_t)li * N1K;
+    const int s = (2048 - ms2048(ct[n])) & 2047;
+    for (int q = threadIdx.x; q < N1K; q += LAT_THREADS) {
+      sh.A[0][q] = 0;
+      sh.A[1][q] = rot_read(lut, q, s);
+    }
+  }
+  __syncthreads();
+
+  const int j = wave >> 2, e0 = (wave & 3) * 4;  // phase B: output j, slots e0 .. e0 + 3
+  for (int i = 0; i < n; i++) {
+    const int a = ms2048(ct[i]);
+    if (wave < 6) {  // phase A
+      const int c = wave / 3, l = wave % 3;
+      const u64* acc = sh.A[c];
+      u32 dig[16];
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        const int idx = 64 * e + lane;
+        dig[e] = decomp_7x3(gl_sub(rot_read(acc, idx, a), acc[idx]));
+      }
+      u64 x[16];
+      ntt1024_fwd_digits(dig, l, x, sh.T[wave], lane, sh.tw);
+#pragma unroll
+      for (int e = 0; e < 16; e++) sh.F[wave][64 * e + lane] = x[e];
+    }
+    __syncthreads();
+    {  // phase B
+      const u64* k = bsk + (size_t)i * 12 * N1K + (size_t)j * N1K + lane;
+      u64 o[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int r = 0; r < 6; r++)
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+          o[t] = gl_mac_lazy(o[t], sh.F[r][64 * (e0 + t) + lane], k[(size_t)r * 2 * N1K + 64 * (e0 + t)]);
+#pragma unroll
+      for (int t = 0; t < 4; t++) O[j * N1K + 64 * (e0 + t) + lane] = gl_canon(o[t]);
+    }
+    __syncthreads();
+    if (wave < 2) {  // phase C
+      u64 x[16];
+#pragma unroll
+      for (int e = 0; e < 16; e++) x[e] = O[wave * N1K + 64 * e + lane];
+      ntt1024_inv(x, sh.T[wave], lane, sh.tw);
+#pragma unroll
+      for (int e = 0; e < 16; e++) sh.A[wave][64 * e + lane] = gl_add(sh.A[wave][64 * e + lane], x[e]);
+    }
+    __syncthreads();
+  }
+
+  if (WRITE_ACC) {
+    u64* oa = out_acc + b * 2048;
+    for (int q = threadIdx.x; q < 2 * N1K; q += LAT_THREADS) oa[q] = sh.A[q >> 10][q & (N1K - 1)];
+  }
+  if (WRITE_BIG) {
+    u64* ob = out_big + b * (size_t)(N1K + 1);
+    for (int q = threadIdx.x; q <= N1K; q += LAT_THREADS) {
+      u64 v;
+      if (q == N1K) v = sh.A[1][0];
+      else if (q == 0) v = sh.A[0][0];
+      else v = gl_neg(sh.A[0][N1K - q]);
+      ob[q] = gl_to_torus(v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 __global__ void sample_extract_kernel(const u64* __restrict__ acc, size_t B, u64* __restrict__ out) {
   const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * (N1K + 1)) return;
@@ -355,8 +457,22 @@ hipError_t launch_bsk_to_ntt(const u64* bsk_std, u64* bsk_ntt, int n, const u64*
 }
 
 hipError_t launch_blind_rotate(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index, int n_lut,
-                               const u64* bsk, const u64* tw, u64* out_big, u64* out_acc, hipStream_t s) {
+                               const u64* bsk, const u64* tw, u64* out_big, u64* out_acc, hipStream_t s,
+                               size_t latency_max_batch) {
   if (B == 0) return hipSuccess;
+  if (B <= latency_max_batch) {
+    dim3 grid((unsigned)B), block(LAT_THREADS);
+    if (out_acc && out_big)
+      hipLaunchKernelGGL((blind_rotate_lat_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index, n_lut,
+                         bsk, tw, out_big, out_acc);
+    else if (out_acc)
+      hipLaunchKernelGGL((blind_rotate_lat_kernel<true, false>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                         n_lut, bsk, tw, out_big, out_acc);
+    else
+      hipLaunchKernelGGL((blind_rotate_lat_kernel<false, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                         n_lut, bsk, tw, out_big, out_acc);
+    return hipGetLastError();
+  }
   dim3 grid((unsigned)((B + BR_WAVES - 1) / BR_WAVES)), block(BR_THREADS);
   if (out_acc && out_big)
     hipLaunchKernelGGL((blind_rotate_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index, n_lut, bsk,
