@@ -55,3 +55,20 @@ def load_golden(name):
     path = os.path.join(ROOT, "tests", "golden", name)
     with np.load(path, allow_pickle=False) as z:
         return {k: z[k] for k in z.files}
+
+
+# ---- P-FHEVM (N=2048, KS->PBS) fixtures shared by the gpu tests --------------------------------
+@pytest.fixture(scope="session")
+def fhevm_keys():
+    import tfhe_amd
+    return tfhe_amd.gen_keys(tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM), KEY_SEED)
+
+
+@pytest.fixture(scope="session")
+def fhevm_engine(fhevm_keys):
+    import tfhe_amd
+    ck, sk = fhevm_keys
+    eng = tfhe_amd.Engine(ck.params, 0)
+    eng.load_keys(sk)
+    yield eng
+    eng.close()

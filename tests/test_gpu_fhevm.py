@@ -27,19 +27,13 @@ def fkeys_oracle(oracle_mod, fprm):
 
 
 @pytest.fixture(scope="module")
-def fkeys():
-    import tfhe_amd
-    return tfhe_amd.gen_keys(tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM), KEY_SEED)
+def fkeys(fhevm_keys):
+    return fhevm_keys
 
 
 @pytest.fixture(scope="module")
-def fengine(fkeys):
-    import tfhe_amd
-    ck, sk = fkeys
-    eng = tfhe_amd.Engine(ck.params, 0)
-    eng.load_keys(sk)
-    yield eng
-    eng.close()
+def fengine(fhevm_engine):
+    return fhevm_engine
 
 
 def test_ntt2048_vs_oracle(fengine, oracle_mod):

@@ -16,6 +16,15 @@ constexpr int TW_U64 = 4 * N1K;            // twiddle tables: tw1 fwd, tw2 fwd, 
 
 // Ordering of one wavefront's own LDS writes before its reads of another lane's data (LDS runs a
 // wave's operations in order; this stops the compiler moving them and retires the writes).
+// Barrier that also publishes LDS written by global_load_lds (LDS DMA): the DMA completes on the
+// VECTOR memory counter, which the compiler does not wait for before s_barrier on its own (it
+// does not model the LDS write), so every wave drains vmcnt(0) first — otherwise a wave can read a
+// BSK chunk slice another wave's DMA has not finished writing.
+__device__ __forceinline__ void glds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __syncthreads();
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)

@@ -134,9 +134,9 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int a, 
 #pragma unroll 1
   for (int l = 0; l < 3; l++) {
     const int g = i * 6 + c * 3 + l;
-    // chunk g has landed (every wave drained its glds: __syncthreads waits vmcnt(0)) and every wave
-    // is done reading buffer (g+1)&1 (step g-1): refill it with chunk g+1
-    __syncthreads();
+    // chunk g has landed (every wave drains its own LDS DMA, then the barrier) and every wave is
+    // done reading buffer (g+1)&1 (step g-1): refill it with chunk g+1
+    glds_barrier();
     if (g + 1 < n_steps) load_chunk(bsk, g + 1, sh.K[(g + 1) & 1], wave, lane);
     u64 x[16];
     ntt1024_fwd_digits(dig, l, x, T, lane, sh.tw);

@@ -199,7 +199,7 @@ __device__ __forceinline__ void ext_prod_2048(const u64 (&acc)[16], int a, int c
 #pragma unroll 1
   for (int j = 0; j < 2; j++) {
     const int g = i * 4 + c * 2 + j;
-    __syncthreads();  // chunk g landed everywhere; buffer (g+1)&1 free; exchange reads done
+    glds_barrier();  // chunk g landed everywhere; buffer (g+1)&1 free; exchange reads done
     if (g + 1 < n_steps) load_chunk2(bsk, g + 1, sh.K[(g + 1) & 1], wave, lane);
     const u64* k = sh.K[g & 1] + h * N1K + lane;
     if (j == 0) {
