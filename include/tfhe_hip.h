@@ -126,10 +126,11 @@ int tfhe_hip_nand(tfhe_ctx* ctx, const uint64_t* c1, const uint64_t* c2, size_t 
 
 /* Wait for all work on the ctx stream. */
 /* Batches of at most max_batch ciphertexts run the latency blind-rotate kernel (one ciphertext per
- * workgroup, ~5x lower PBS latency: the lockstep levels of integer circuits, single /evaluate
- * requests — packages/luxfhejs/src/index.ts:56-141 call patterns); larger batches the throughput
- * kernel.  Default 1024 (the measured crossover on MI355X: 55 vs 61 ms at B = 1024, 69 vs 62 at 1280;
- * tools/latency_sweep.py); 0 disables the latency kernel.  P-GATE only. */
+ * workgroup: 4.5x (N=1024) / 2.5x (N=2048) lower PBS latency — the lockstep levels of integer
+ * circuits, single /evaluate requests, packages/luxfhejs/src/index.ts:56-141 call patterns); larger
+ * batches the throughput kernel.  Defaults = the measured crossovers on MI355X (tools/latency_sweep.py):
+ * 1024 for N=1024 (55 vs 61 ms at B=1024, 69 vs 62 at 1280), 512 for N=2048 (42 vs 53 ms at 512,
+ * 63 vs 53 at 768); 0 disables the latency kernel. */
 int tfhe_hip_set_latency_batch(tfhe_ctx* ctx, size_t max_batch);
 int tfhe_hip_sync(tfhe_ctx* ctx);
 /* Per-kernel device timing (HIP events recorded on the launch stream around every blind-rotate /

@@ -97,3 +97,27 @@ def test_pbs2048_all_messages_and_batch(fengine, fkeys):
     # chained: f(f(m))
     out2 = fengine.pbs(out, acc)
     assert np.array_equal(ck.decrypt(out2, MM), np.array([f(f(int(m))) for m in msgs], dtype=np.uint64))
+
+
+@pytest.mark.parametrize("B", [1, 6, 130])
+def test_latency_and_batch_kernels_agree_2048(fengine, fkeys, oracle_mod, fprm, fkeys_oracle, B):
+    ck, _ = fkeys
+    rng = np.random.default_rng(B + 2048)
+    msgs = rng.integers(0, MM, B).astype(np.uint64)
+    cts = ck.encrypt(msgs, MM, seed=0xC0FFEE40 + B)
+    lut = oracle_mod.lut_from_table(2048, MM, [(7 * m + 2) % MM for m in range(MM)], DELTA)
+    small = fengine.keyswitch(cts)
+    try:
+        fengine.set_latency_batch(0)
+        acc_b = fengine.blind_rotate(small, lut)
+        out_b = fengine.pbs(cts, lut)
+        fengine.set_latency_batch(1 << 20)
+        acc_l = fengine.blind_rotate(small, lut)
+        out_l = fengine.pbs(cts, lut)
+    finally:
+        fengine.set_latency_batch(512)
+    assert np.array_equal(acc_l, acc_b)
+    assert np.array_equal(out_l, out_b)
+    i = B // 2
+    assert np.array_equal(acc_l[i], oracle_mod.blind_rotate(fprm, fkeys_oracle, small[i], lut))
+    assert np.array_equal(ck.decrypt(out_l, MM), (7 * msgs + 2) % MM)

@@ -81,7 +81,7 @@ struct tfhe_ctx {
   u64* d_tw = nullptr;  // 4 x 1024 twiddle tables of the device NTT layout
   u64 ninv = 0;
   bool keys = false;
-  size_t lat_max = 1024;  // batches up to this size use the latency blind-rotate kernel (P-GATE)
+  size_t lat_max = 1024;  // batches up to this size use the latency blind-rotate kernel
   // workspaces
   u64* d_big = nullptr;
   size_t big_cap = 0;  // u64 elements
@@ -156,7 +156,7 @@ hipError_t launch_br(tfhe_ctx* c, const u64* in, size_t B, const u64* luts, cons
                      u64* out_acc, hipStream_t s) {
   if (c->p.N == 2048)
     return tfhe::launch_blind_rotate_2048(in, B, (int)c->p.n, luts, idx, (int)n_lut, c->d_bsk, c->d_tw, out_big, out_acc,
-                                          s);
+                                          s, c->lat_max);
   return tfhe::launch_blind_rotate(in, B, (int)c->p.n, luts, idx, (int)n_lut, c->d_bsk, c->d_tw, out_big, out_acc, s,
                                    c->lat_max);
 }
@@ -302,6 +302,7 @@ int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out) {
   tfhe_ctx* c = new tfhe_ctx();
   c->p = *p;
   c->device = device;
+  c->lat_max = p->N == 2048 ? 512 : 1024;  // measured crossovers (tools/latency_sweep.py)
   auto cleanup = [&](int rc) {
     tfhe_hip_destroy(c);
     return rc;

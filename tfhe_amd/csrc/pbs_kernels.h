@@ -28,7 +28,7 @@ hipError_t launch_bsk_to_ntt_2048(const u64* bsk_std, u64* bsk_ntt, size_t polys
                                   hipStream_t s);
 hipError_t launch_blind_rotate_2048(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
                                    int n_lut, const u64* bsk, const u64* tw, u64* out_big, u64* out_acc,
-                                   hipStream_t s);
+                                   hipStream_t s, size_t latency_max_batch = 0);
 hipError_t launch_sample_extract_2048(const u64* acc, size_t B, u64* out, hipStream_t s);
 hipError_t launch_ntt2048_fwd(u64* polys, size_t count, const u64* tw, hipStream_t s);
 hipError_t launch_ntt2048_inv(u64* polys, size_t count, const u64* tw, u64 ninv, hipStream_t s);

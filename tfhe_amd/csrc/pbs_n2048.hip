@@ -307,6 +307,139 @@ __global__ __launch_bounds__(B2_THREADS, 1) void blind_rotate2048_kernel(
     br2048_body<0, WRITE_ACC, WRITE_BIG>(sh, lwe_in, n, B, luts, lut_index, n_lut, bsk, tw_g, out_big, out_acc);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Latency-mode blind rotation, N = 2048: ONE ciphertext per workgroup of 8 waves (radix circuits'
+// lockstep levels).  Per CMUX:
+//   A   waves 0..3 = (c, h): rotate/decompose half h of accumulator polynomial c, ntt1024_fwd,
+//       send the partner's combine slots through LDS;   A2: combine -> F[c] (device layout)
+//   B   all 8 waves: pointwise MAC over 256 positions each, both outputs j, in place in F
+//   C   waves 0..3 = (j, h): inverse combine (exchange), ntt1024_inv, acc_j half += ...
+// Five barriers per CMUX, executed by all waves.  LDS: accumulator 32 KB (split layout), F 32 KB,
+// 4 NTT scratch areas 35 KB, 4 exchange areas 16 KB, twiddles 32 KB = 147 KB.
+struct Lat2Shared {
+  u64 A[2][N2K];          // accumulator polynomials, split layout [h][m]
+  u64 F[2][N2K];          // NTT(digits_c), then MAC outputs out_j, device layout [h][s][L]
+  u64 T[4][T_LDS];        // NTT scratch of waves 0..3
+  u64 X[4][8 * 64];       // combine exchange areas
+  u64 tw[TW_U64];
+};
+
+template <bool WRITE_ACC, bool WRITE_BIG>
+__global__ __launch_bounds__(512, 1) void blind_rotate2048_lat_kernel(
+    const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
+    int n_lut, const u64* __restrict__ bsk, const u64* __restrict__ tw_g, u64* __restrict__ out_big,
+    u64* __restrict__ out_acc) {
+  __shared__ __attribute__((aligned(16))) Lat2Shared sh;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t b = blockIdx.x;
+  const u64* ct = lwe_in + b * (size_t)(n + 1);
+  const bool act = wave < 4;
+  const int hi = wave >> 1, h = wave & 1;  // (c or j, half) of the active waves
+  const u64* twc = tw_g + TWC_FWD;
+  const u64* twci = tw_g + TWC_INV;
+
+  for (int q = threadIdx.x; q < TW_U64; q += 512) sh.tw[q] = tw_g[q];
+  {
+    int li = lut_index ? (int)lut_index[b] : 0;
+    li = (li < 0 || li >= n_lut) ? 0 : li;
+    const u64* lut = luts + (size_t)li * N2K;
+    const int s0 = (4096 - ms4096(ct[n])) & 4095;
+    for (int i = threadIdx.x; i < N2K; i += 512) {
+      sh.A[0][(i & 1) * N1K + (i >> 1)] = 0;
+      sh.A[1][(i & 1) * N1K + (i >> 1)] = rot_read_2048(lut, i, s0);
+    }
+  }
+
+  for (int i = 0; i < n; i++) {
+    const int a = ms4096(ct[i]);
+    __syncthreads();  // B0: accumulator (and twiddles, first time) visible
+    u64 x[16];
+    if (act) {  // A: digits of half h of polynomial c = hi, forward transform
+      const u64* acc = sh.A[hi];
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        const int m = 64 * e + lane;
+        x[e] = gl_from_i32(decomp_23x1(gl_sub(rot_read_split(acc, 2 * m + h, a), acc[h * N1K + m])));
+      }
+      ntt1024_fwd(x, sh.T[wave], lane, sh.tw);
+#pragma unroll
+      for (int p = 0; p < 8; p++) sh.X[wave][64 * p + lane] = x[8 * (1 - h) + p];
+    }
+    __syncthreads();  // B1
+    if (act) {  // A2: combine with the partner's slots
+      const u64* P = sh.X[wave ^ 1];
+#pragma unroll
+      for (int p = 0; p < 8; p++) {
+        const u64 r = P[64 * p + lane];
+        const u64 E = h ? r : x[p];
+        const u64 O = h ? x[8 + p] : r;
+        const u64 t = gl_mul(O, twc[(8 * h + p) * 64 + lane]);
+        sh.F[hi][h * N1K + 64 * p + lane] = gl_add(E, t);
+        sh.F[hi][h * N1K + 64 * (8 + p) + lane] = gl_sub(E, t);
+      }
+    }
+    __syncthreads();  // B2
+    {  // B: out_j[pos] = F0[pos] BSK[i][0][j][pos] + F1[pos] BSK[i][1][j][pos], in place
+      const u64* k = bsk + (size_t)i * 4 * N2K;
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const int pos = wave * 256 + 64 * t + lane;
+        const u64 f0 = sh.F[0][pos], f1 = sh.F[1][pos];
+        u64 o0 = gl_mac_lazy(0, f0, k[pos]);
+        o0 = gl_mac_lazy(o0, f1, k[2 * N2K + pos]);
+        u64 o1 = gl_mac_lazy(0, f0, k[N2K + pos]);
+        o1 = gl_mac_lazy(o1, f1, k[3 * N2K + pos]);
+        sh.F[0][pos] = gl_canon(o0);
+        sh.F[1][pos] = gl_canon(o1);
+      }
+    }
+    __syncthreads();  // B3
+    u64 keep[8];
+    if (act) {  // C: inverse combine of out_j (j = hi), own slots p, send the partner's
+#pragma unroll
+      for (int p = 0; p < 8; p++) {
+        const u64 y0 = sh.F[hi][h * N1K + 64 * p + lane], y1 = sh.F[hi][h * N1K + 64 * (8 + p) + lane];
+        const u64 Ep = gl_add(y0, y1);
+        const u64 Op = gl_mul(gl_sub(y0, y1), twci[(8 * h + p) * 64 + lane]);
+        sh.X[wave][64 * p + lane] = h ? Ep : Op;
+        keep[p] = h ? Op : Ep;
+      }
+    }
+    __syncthreads();  // B4
+    if (act) {  // C2: assemble the half, inverse transform, accumulate
+      const u64* P = sh.X[wave ^ 1];
+#pragma unroll
+      for (int p = 0; p < 8; p++) {
+        x[h ? p : 8 + p] = P[64 * p + lane];
+        x[h ? 8 + p : p] = keep[p];
+      }
+      ntt1024_inv(x, sh.T[wave], lane, sh.tw);
+      u64* acc = sh.A[hi] + h * N1K;
+#pragma unroll
+      for (int e = 0; e < 16; e++) acc[64 * e + lane] = gl_add(acc[64 * e + lane], x[e]);
+    }
+  }
+  __syncthreads();
+
+  if (WRITE_ACC) {
+    u64* oa = out_acc + b * (2 * N2K);
+    for (int i = threadIdx.x; i < N2K; i += 512) {
+      oa[i] = sh.A[0][(i & 1) * N1K + (i >> 1)];
+      oa[N2K + i] = sh.A[1][(i & 1) * N1K + (i >> 1)];
+    }
+  }
+  if (WRITE_BIG) {
+    u64* ob = out_big + b * (size_t)(N2K + 1);
+    for (int q = threadIdx.x; q <= N2K; q += 512) {
+      u64 v;
+      if (q == N2K) v = sh.A[1][0];
+      else if (q == 0) v = sh.A[0][0];
+      else v = gl_neg(sh.A[0][((N2K - q) & 1) * N1K + ((N2K - q) >> 1)]);
+      ob[q] = gl_to_torus(v);
+    }
+  }
+}
+
 __global__ void sample_extract2048_kernel(const u64* __restrict__ acc, size_t B, u64* __restrict__ out) {
   const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * (N2K + 1)) return;
@@ -344,8 +477,21 @@ hipError_t launch_bsk_to_ntt_2048(const u64* bsk_std, u64* bsk_ntt, size_t polys
 
 hipError_t launch_blind_rotate_2048(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
                                    int n_lut, const u64* bsk, const u64* tw, u64* out_big, u64* out_acc,
-                                   hipStream_t s) {
+                                   hipStream_t s, size_t latency_max_batch) {
   if (B == 0) return hipSuccess;
+  if (B <= latency_max_batch) {
+    dim3 grid((unsigned)B), block(512);
+    if (out_acc && out_big)
+      hipLaunchKernelGGL((blind_rotate2048_lat_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                         n_lut, bsk, tw, out_big, out_acc);
+    else if (out_acc)
+      hipLaunchKernelGGL((blind_rotate2048_lat_kernel<true, false>), grid, block, 0, s, lwe_in, n, B, luts,
+                         lut_index, n_lut, bsk, tw, out_big, out_acc);
+    else
+      hipLaunchKernelGGL((blind_rotate2048_lat_kernel<false, true>), grid, block, 0, s, lwe_in, n, B, luts,
+                         lut_index, n_lut, bsk, tw, out_big, out_acc);
+    return hipGetLastError();
+  }
   dim3 grid((unsigned)((B + B2_CTS - 1) / B2_CTS)), block(B2_THREADS);
   if (out_acc && out_big)
     hipLaunchKernelGGL((blind_rotate2048_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index, n_lut,

@@ -1,6 +1,6 @@
-"""Blind-rotate kernel time vs batch size for the latency kernel and the batch kernel (P-GATE),
-measured with the library's HIP events; prints one JSON object.  Picks the crossover used as the
-default of tfhe_hip_set_latency_batch.   python tools/latency_sweep.py"""
+"""Blind-rotate kernel time vs batch size for the latency kernel and the batch kernel, measured with
+the library's HIP events; prints one JSON object.  Picks the crossover used as the default of
+tfhe_hip_set_latency_batch.   python tools/latency_sweep.py [gate|fhevm]"""
 import json
 import os
 import sys
@@ -13,15 +13,18 @@ import tfhe_amd  # noqa: E402
 
 def main():
     import torch
-    params = tfhe_amd.Params.preset(tfhe_amd.PRESET_GATE)
+    fhevm = len(sys.argv) > 1 and sys.argv[1] == "fhevm"
+    params = tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM if fhevm else tfhe_amd.PRESET_GATE)
     ck, sk = tfhe_amd.gen_keys(params, 0x7F4E0001)
     eng = tfhe_amd.Engine(params, 0).load_keys(sk)
     dev = torch.device("cuda", 0)
     res = {}
     for B in [1, 8, 64, 256, 257, 512, 768, 1024, 1280, 1536, 2048, 4096]:
-        cts = ck.encrypt_bool(np.arange(B) % 2 == 0, seed=9)
+        want = np.arange(B) % (16 if fhevm else 2)
+        cts = ck.encrypt(want, 16, seed=9) if fhevm else ck.encrypt_bool(want == 0, seed=9)
+        lut = eng.generate_accumulator(lambda m: m, 16) if fhevm else eng.gate_lut()
         d_in = torch.from_numpy(cts.view(np.int64)).to(dev)
-        d_lut = torch.from_numpy(eng.gate_lut().view(np.int64)).to(dev)
+        d_lut = torch.from_numpy(lut.view(np.int64)).to(dev)
         d_out = torch.empty_like(d_in)
         row = {}
         for name, thr in (("latency", 1 << 30), ("batch", 0)):
@@ -39,7 +42,8 @@ def main():
             eng.timing(False)
             ms, n = eng.timing_stats(0)
             row[name] = round(ms / max(n, 1), 3)
-            ok = np.array_equal(ck.decrypt_bool(d_out.cpu().numpy().view(np.uint64)), np.arange(B) % 2 == 0)
+            o = d_out.cpu().numpy().view(np.uint64)
+            ok = np.array_equal(ck.decrypt(o, 16), want) if fhevm else np.array_equal(ck.decrypt_bool(o), want == 0)
             assert ok, (B, name)
         res[B] = row
         print(B, row, file=sys.stderr, flush=True)
