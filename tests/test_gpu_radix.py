@@ -41,7 +41,7 @@ def test_radix_kats_gpu(fhevm_engine, fhevm_keys):
         if not ok:
             bad.append((k["source"], k["op"], k["types"], k["args"], k["expect"], got))
     assert not bad, f"{len(bad)} of {len(kats)} failed: {bad[:5]}"
-    assert c.launches <= 12
+    assert c.launches <= 40
 
 
 def test_radix_batch_gpu(fhevm_engine, fhevm_keys):

@@ -12,8 +12,10 @@ Operators (fhEVM semantics, as tfhe_amd.integer): add/sub/neg with parallel-pref
 propagation over block states {0: none, 1: propagate, 2: generate} (log2(blocks) levels),
 bitwise and/or/xor (1 level), not (free: 3 - v), eq/ne (per-block equality + AND tree),
 lt/le/gt/ge (per-block {<, =, >} + MSB-first merge tree), min/max (compare + 2-PBS select),
-shl/shr/rotl/rotr by a plaintext amount (block moves + one bivariate level for odd shifts),
-plaintext right operands, mixed widths zero-extended.
+shl/shr/rotl/rotr by a plaintext amount (block moves + one bivariate level for odd shifts) or an
+encrypted one (barrel shifter over the amount's bits), mul (block products by bivariate low/high
+digit tables, carry-save reduction rounds of up to 5 blocks, final prefix add; plaintext factors by
+univariate tables), plaintext right operands, mixed widths zero-extended.
 """
 from __future__ import annotations
 
@@ -326,7 +328,96 @@ def g_shift(c, a, k: int, kind: str):
     return out
 
 
-RADIX_OPS = ("add", "sub", "and", "or", "xor", "eq", "ne", "lt", "le", "gt", "ge", "min", "max",
+T_MUL_LO = _biv(lambda x, y: (x * y) % MSG)
+T_MUL_HI = _biv(lambda x, y: (x * y) // MSG)
+T_CARRY = _table(lambda v: v // MSG)
+
+
+def g_sum_columns(c, cols: List[List[np.ndarray]], B: int):
+    """Sum per-position lists of clean blocks (position k has weight 4^k, positions >= nb dropped)
+    into one clean radix value: carry-save rounds add up to 5 blocks (<= 15, the block capacity) and
+    split each sum into message (stays) and carry (moves up) in one PBS level, until every position
+    holds at most two blocks; then one carry-propagating add."""
+    nb = len(cols)
+    while max(len(col) for col in cols) > 2:
+        reqs, plan = [], []
+        new_cols: List[List[np.ndarray]] = [[] for _ in range(nb)]
+        for k, col in enumerate(cols):
+            if len(col) <= 2:
+                new_cols[k].extend(col)
+                continue
+            for g in range(0, len(col), 5):
+                grp = col[g:g + 5]
+                if len(grp) == 1:
+                    new_cols[k].append(grp[0])
+                    continue
+                ssum = _add(*grp)
+                reqs += [(ssum, T_MSG), (ssum, T_CARRY)]
+                plan.append(k)
+        outs = yield reqs
+        for t, k in enumerate(plan):
+            new_cols[k].append(outs[2 * t])
+            if k + 1 < nb:
+                new_cols[k + 1].append(outs[2 * t + 1])
+        cols = new_cols
+    zero = _const(c, (B,), 0)
+    a = np.stack([col[0] if len(col) > 0 else zero for col in cols], axis=1)
+    b = np.stack([col[1] if len(col) > 1 else zero for col in cols], axis=1)
+    return (yield from g_add(c, a, b))
+
+
+def g_mul(c, a, b):
+    """a * b mod 2^w.  b: blocks (B, nb, dim) or a plaintext int.  Block products: two bivariate
+    PBS (low / high digit of x*y) per pair i + j < nb (plaintext: univariate per a-block and digit)."""
+    B, nb = a.shape[:2]
+    reqs, pos = [], []
+    if isinstance(b, (int, np.integer)):
+        digs = [(int(b) >> (2 * j)) & 3 for j in range(nb)]
+        for i in range(nb):
+            for j in range(nb - i):
+                d = digs[j]
+                if d == 0:
+                    continue
+                reqs.append((a[:, i], _table(lambda v, d=d: (v * d) % MSG)))
+                pos.append(i + j)
+                if i + j + 1 < nb:
+                    reqs.append((a[:, i], _table(lambda v, d=d: (v * d) // MSG)))
+                    pos.append(i + j + 1)
+    else:
+        for i in range(nb):
+            for j in range(nb - i):
+                packed = _pack(a[:, i], b[:, j])
+                reqs.append((packed, T_MUL_LO))
+                pos.append(i + j)
+                if i + j + 1 < nb:
+                    reqs.append((packed, T_MUL_HI))
+                    pos.append(i + j + 1)
+    cols: List[List[np.ndarray]] = [[] for _ in range(nb)]
+    if reqs:
+        outs = yield reqs
+        for o, k in zip(outs, pos):
+            cols[k].append(o)
+    return (yield from g_sum_columns(c, cols, B))
+
+
+T_BIT = {k: _table(lambda v, k=k: (v >> k) & 1) for k in (0, 1)}
+
+
+def g_shift_enc(c, a, amount, kind: str):
+    """Shift / rotate by an encrypted amount (mod w): barrel shifter, one select per amount bit."""
+    B, nb = a.shape[:2]
+    w = 2 * nb
+    nbits = max(1, (w - 1).bit_length())
+    reqs = [(amount[:, k // 2], T_BIT[k % 2]) for k in range(nbits)]
+    bits = yield reqs
+    cur = a
+    for k in range(nbits):
+        moved = yield from g_shift(c, cur, 1 << k, kind)
+        cur = yield from g_select(c, bits[k], moved, cur)
+    return cur
+
+
+RADIX_OPS = ("add", "sub", "mul", "and", "or", "xor", "eq", "ne", "lt", "le", "gt", "ge", "min", "max",
              "neg", "not", "shl", "shr", "rotl", "rotr")
 
 
@@ -344,8 +435,10 @@ def fhevm_op(c: RadixCircuit, op: str, lhs, rhs=None):
     if not (lenc or renc):
         raise ValueError("at least one operand must be encrypted")
     if op in ("shl", "shr", "rotl", "rotr"):
-        if not lenc or renc:
-            raise ValueError("radix shifts take an encrypted value and a plaintext amount")
+        if not lenc:
+            raise ValueError("shift of a plaintext by an encrypted amount is not an fhEVM overload")
+        if renc:
+            return RadixUint(c, (yield from g_shift_enc(c, lhs.blocks, rhs.blocks, op)))
         return RadixUint(c, (yield from g_shift(c, lhs.blocks, int(rhs), op)))
     w = max(x.width for x in (lhs, rhs) if isinstance(x, RadixUint))
     B = (lhs if lenc else rhs).batch
@@ -355,6 +448,12 @@ def fhevm_op(c: RadixCircuit, op: str, lhs, rhs=None):
             return x.cast(w).blocks
         return c.trivial(np.broadcast_to(RadixUint._digits([int(x) % (1 << w)], w), (B, w // 2)))
 
+    if op == "mul":
+        if not lenc:
+            return RadixUint(c, (yield from g_mul(c, rhs.cast(w).blocks, int(lhs) % (1 << w))))
+        if not renc:
+            return RadixUint(c, (yield from g_mul(c, lhs.cast(w).blocks, int(rhs) % (1 << w))))
+        return RadixUint(c, (yield from g_mul(c, blocks(lhs), blocks(rhs))))
     a, b = blocks(lhs), blocks(rhs)
     if op == "add":
         return RadixUint(c, (yield from g_add(c, a, b)))
