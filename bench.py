@@ -71,6 +71,27 @@ def pmc_traffic(B: int):
     return None
 
 
+def valu_profile(B: int, kernel_ms: float):
+    """VALU roofline of the blind-rotate kernel from the committed SQ counter pass
+    (profiles/*_pmc_sq.csv: rocprofv3 --pmc SQ_INSTS_VALU ... of this bench at B = 4096): wave64 VALU
+    instructions per launch (scaled per PBS to B) x 4 cycles on a 16-lane SIMD, over the SIMD-cycles of
+    the measured launch (1024 SIMDs at 2.4 GHz, MI355X_MICROARCH.md)."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_sq.csv")))
+    if not files:
+        return None
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(files[-1]))
+            if r["Counter_Name"] == "SQ_INSTS_VALU" and "blind_rotate_kernel" in r["Kernel_Name"]]
+    if not vals:
+        return None
+    insts = sum(vals) / len(vals) / 4096 * B
+    frac = insts * 4 / (1024 * 2.4e9 * kernel_ms * 1e-3)
+    return {"bound": "valu", "insts_per_launch": round(insts), "insts_per_pbs": round(insts / B),
+            "issue_frac": round(frac, 3), "model": "4 cycles per wave64 VALU instruction per SIMD, 1024 SIMDs, 2.4 GHz",
+            "source": os.path.relpath(files[-1], ROOT)}
+
+
 def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int, preset: int = 0,
                  lut_host: np.ndarray = None):
     """Oracle PBS on host cores over `sample` ciphertexts of the same batch (same keys)."""
@@ -246,6 +267,7 @@ def main() -> int:
                 "kernel_ms": round(br_avg, 3),
                 "launches": br_n,
             },
+            "valu_roofline": None if fhevm else valu_profile(B, br_avg),
             "keyswitch_ms": round(ks_ms / max(ks_n, 1), 3),
             "key_broadcast_ms": round(bcast_ms, 3),
             "decrypt_ok": bool(ok.item()),
