@@ -29,6 +29,7 @@ export class Engine {
   destroy(): void;
   gateLut(): BigUint64Array;
   generateAccumulator(f: (m: number) => number | bigint, msgModulus?: number, deltaOut?: bigint | null): BigUint64Array;
+  lutFromTable(table: ArrayLike<number | bigint>, msgModulus?: number): BigUint64Array;
   pbs(cts: BigUint64Array, luts: BigUint64Array, lutIndex?: Uint32Array | null): Promise<BigUint64Array>;
   keyswitchProgrammableBootstrap(ct: BigUint64Array, acc: BigUint64Array): Promise<BigUint64Array>;
   nand(c1: BigUint64Array, c2: BigUint64Array): Promise<BigUint64Array>;
@@ -77,12 +78,14 @@ export class FheUint32 extends FheUintN { static encrypt(v: number | bigint | Ar
 export class FheUint64 extends FheUintN { static encrypt(v: number | bigint | Array<number | bigint>, ck: ClientKey, e: Engine, seed?: bigint, stream0?: bigint): FheUint64; }
 
 /** ciphertext bytes: 'TFA1' | u8 kind | u8 0 | u16 width | u32 lwe_dim | u32 count | u64[] (LE) */
-export function serializeCiphertext(kind: 0 | 1, width: number, lweDim: number, count: number, words: BigUint64Array): Uint8Array;
+/** kind: 0 ebool / 1 euint (P-GATE bits), 2 radix euint / 3 radix ebool (P-FHEVM blocks) */
+export function serializeCiphertext(kind: 0 | 1 | 2 | 3, width: number, lweDim: number, count: number, words: BigUint64Array): Uint8Array;
 export function parseCiphertext(bytes: Uint8Array | number[]): { kind: number; width: number; lweDim: number; count: number; words: BigUint64Array };
 
 export interface EvaluateRequest { op: FheOp; left: Uint8Array; right?: Uint8Array | number | bigint | null; bitWidth?: number; }
 export class LuxFHELocalClient {
-  constructor(config?: { params?: TfheParams; seed?: bigint; device?: number });
+  constructor(config?: { params?: TfheParams | 'gate' | 'fhevm'; seed?: bigint; device?: number; engine?: Engine });
+  readonly radix: boolean;
   initialize(): Promise<void>;
   getPublicKey(): Promise<Uint8Array>;
   encryptValue(value: number | bigint | string, bitWidth: number): Uint8Array;

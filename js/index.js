@@ -16,6 +16,7 @@
 const path = require('path');
 const native = require(path.join(__dirname, 'build', 'tfhe_napi.node'));
 const integer = require('./integer.js');
+const radix = require('./radix.js');
 
 const PRESET_GATE = 0;
 const PRESET_FHEVM = 1;
@@ -89,6 +90,11 @@ class Engine {
     const table = BigUint64Array.from({ length: msgModulus }, (_, m) => mod64(BigInt(f(m)) % mm));
     return native.lutFromTable(this.params.N, msgModulus, table, delta);
   }
+  /** LUT for a lookup table of msgModulus entries (radix blocks: 16 = message x carry, padding bit kept) */
+  lutFromTable(table, msgModulus = table.length) {
+    const t = BigUint64Array.from(table, (v) => BigInt(v));
+    return native.lutFromTable(this.params.N, msgModulus, t, (1n << 63n) / BigInt(msgModulus));
+  }
   /** batched PBS (blind rotate + sample extract + keyswitch) on the GPU; resolves to ciphertexts */
   pbs(cts, luts, lutIndex = null) { return native.pbs(this.handle, cts, luts, lutIndex); }
   keyswitchProgrammableBootstrap(ct, acc) { return this.pbs(ct, acc); }
@@ -124,10 +130,14 @@ class FheBool {
 
 /**
  * Ciphertext bytes (the opaque Uint8Array of the HTTP API and LuxFHEClient): a 16-byte header
- *   'TFA1' | u8 kind (0 = ebool, 1 = euint) | u8 0 | u16 width | u32 lwe_dim | u32 count
- * then count x width x (lwe_dim + 1) u64 little-endian (value-major, LSB bit first).
+ *   'TFA1' | u8 kind | u8 0 | u16 width | u32 lwe_dim | u32 count
+ * then count x cts(kind, width) x (lwe_dim + 1) u64 little-endian (value-major, LSB first).
+ * kind 0 = ebool, 1 = euint (one gate ciphertext per bit, P-GATE); kind 2 = radix euint (width/2
+ * blocks of 2 message bits, P-FHEVM), 3 = radix ebool (one block holding 0/1).
  */
 const CT_MAGIC = 0x31414654; // 'TFA1'
+const KIND = { BOOL: 0, UINT: 1, RADIX_UINT: 2, RADIX_BOOL: 3 };
+const ctsPerValue = (kind, width) => (kind === KIND.RADIX_UINT ? width / 2 : kind === KIND.RADIX_BOOL ? 1 : width);
 function serializeCiphertext(kind, width, lweDim, count, words) {
   const out = new Uint8Array(16 + words.byteLength);
   const dv = new DataView(out.buffer);
@@ -145,7 +155,8 @@ function parseCiphertext(bytes) {
   const dv = new DataView(u8.buffer, u8.byteOffset, u8.byteLength);
   if (dv.getUint32(0, true) !== CT_MAGIC) throw new Error('not a tfhe_amd ciphertext (bad magic)');
   const kind = dv.getUint8(4), width = dv.getUint16(6, true), lweDim = dv.getUint32(8, true), count = dv.getUint32(12, true);
-  const nWords = count * width * (lweDim + 1);
+  if (kind > 3 || (kind === KIND.RADIX_UINT && width % 2)) throw new Error(`bad ciphertext kind ${kind} / width ${width}`);
+  const nWords = count * ctsPerValue(kind, width) * (lweDim + 1);
   if (u8.length !== 16 + 8 * nWords) throw new Error(`ciphertext length ${u8.length} != header size ${16 + 8 * nWords}`);
   const words = new BigUint64Array(u8.buffer.slice(u8.byteOffset + 16, u8.byteOffset + u8.byteLength));
   return { kind, width, lweDim, count, words };
@@ -215,10 +226,15 @@ const FheUint64 = UINT_CLASSES[64];
  * encrypt_* return serialized ciphertext bytes (Uint8Array) like the HTTP client; evaluate() takes
  * the POST /evaluate shape (e2e/test/fhe.test.ts:105-175) and runs every fhEVM operator on the GPU.
  * Requests submitted concurrently are evaluated in lockstep (one PBS launch per circuit level).
+ * config.params: a params object, or 'gate' (default: boolean gates, js/integer.js) or 'fhevm'
+ * (P-FHEVM radix blocks, js/radix.js — fhEVM's own representation; div/rem only in 'gate').
  */
 class LuxFHELocalClient {
   constructor(config = {}) {
-    this.params = config.params || paramsPreset(PRESET_GATE);
+    const pr = config.params;
+    this.params = pr === 'fhevm' ? paramsPreset(PRESET_FHEVM) : (!pr || pr === 'gate') ? paramsPreset(PRESET_GATE) : pr;
+    this.radix = this.params.order === 1;
+    this.dim = this.radix ? this.params.k * this.params.N : this.params.n;
     this.seed = BigInt(config.seed || 0x7F4E0001n);
     this.device = config.device || 0;
     this.engine = config.engine || null;
@@ -249,6 +265,14 @@ class LuxFHELocalClient {
     const w = Number(bitWidth);
     if (!(w >= 1 && w <= 256)) throw new Error(`Encryption failed: bitWidth ${bitWidth} not supported`);
     const v = BigInt.asUintN(w, BigInt(value));
+    if (this.radix) {
+      if (w > 1 && w % 2) throw new Error(`Encryption failed: radix bitWidth ${w} must be even`);
+      const nb = w === 1 ? 1 : w / 2;
+      const digits = Array.from({ length: nb }, (_, j) => (v >> BigInt(2 * j)) & 3n);
+      const ct = this.clientKey.encrypt(digits, radix.SPACE, this.seed + 1n, this.stream);
+      this.stream += BigInt(nb);
+      return serializeCiphertext(w === 1 ? KIND.RADIX_BOOL : KIND.RADIX_UINT, w, this.dim, 1, ct);
+    }
     const flat = [];
     for (let j = 0; j < w; j++) flat.push(((v >> BigInt(j)) & 1n) === 1n);
     const ct = this.clientKey.encryptBool(flat, this.seed + 1n, this.stream);
@@ -268,8 +292,19 @@ class LuxFHELocalClient {
     if (x === null || x === undefined) return null;
     if (typeof x === 'number' || typeof x === 'bigint' || typeof x === 'string') return BigInt(x);
     const ct = parseCiphertext(x);
-    if (ct.lweDim !== this.params.n) throw new Error(`ciphertext lwe_dim ${ct.lweDim} != engine n ${this.params.n}`);
+    if (ct.lweDim !== this.dim) throw new Error(`ciphertext lwe_dim ${ct.lweDim} != engine ${this.dim}`);
+    if (this.radix !== (ct.kind >= KIND.RADIX_UINT)) throw new Error(`ciphertext kind ${ct.kind} does not match the engine parameters`);
+    if (this.radix) return radix.RadixVec.fromValueMajor(circuit, ct.words, ct.count, ctsPerValue(ct.kind, ct.width));
     return integer.FheUintVec.fromValueMajor(circuit, ct.words, ct.count, ct.width);
+  }
+  _radixGen(c, op, l, r) {
+    // ebool operands are one-block radix values holding 0/1; logical not is 1 - x on them
+    if (op === 'not' && l.blocks.length === 1 && l.isBool) {
+      const one = c.const(l.B, 1);
+      for (let i = 0; i < one.length; i++) one[i] = BigInt.asUintN(64, one[i] - l.blocks[0][i]);
+      return (function* () { return one; }());
+    }
+    return radix.fhevmOp(c, op, l, r);
   }
   /** POST /evaluate: { op, left, right?, bitWidth } -> ciphertext bytes (ebool for comparisons) */
   evaluate(req) {
@@ -282,20 +317,33 @@ class LuxFHELocalClient {
     if (this.busy || !this.queue.length) return;
     this.busy = true;
     const jobs = this.queue.splice(0);
-    const c = new integer.Circuit(this.engine);
+    const c = this.radix ? new radix.RadixCircuit(this.engine) : new integer.Circuit(this.engine);
     const live = [];
     for (const j of jobs) {
       try {
         const { op, left, right } = j.req;
-        live.push({ j, gen: integer.fhevmOp(c, op, this._operand(left, j.req.bitWidth, c), this._operand(right, j.req.bitWidth, c)) });
+        const l = this._operand(left, j.req.bitWidth, c), r = this._operand(right, j.req.bitWidth, c);
+        if (this.radix) {
+          const isB = (x) => x !== null && x !== undefined && typeof x === 'object' && parseCiphertext(x).kind === KIND.RADIX_BOOL;
+          l.isBool = isB(left);
+          if (r instanceof radix.RadixVec) r.isBool = isB(right);
+          live.push({ j, gen: this._radixGen(c, op, l, r), bool: l.isBool && (!(r instanceof radix.RadixVec) || r.isBool) });
+        } else {
+          live.push({ j, gen: integer.fhevmOp(c, op, l, r) });
+        }
       } catch (e) { j.reject(e); }
     }
     try {
       const res = await c.runMany(live.map((x) => x.gen));
       this.launches += c.launches;
+      const d = this.dim + 1;
       res.forEach((r, i) => {
-        if (r instanceof integer.FheUintVec) live[i].j.resolve(serializeCiphertext(1, r.width, this.params.n, r.B, r.toValueMajor()));
-        else live[i].j.resolve(serializeCiphertext(0, 1, this.params.n, r.length / (this.params.n + 1), r));
+        if (r instanceof integer.FheUintVec) live[i].j.resolve(serializeCiphertext(KIND.UINT, r.width, this.dim, r.B, r.toValueMajor()));
+        else if (r instanceof radix.RadixVec) {
+          // and/or/xor on ebool operands stay ebool (one block)
+          if (live[i].bool && r.blocks.length === 1) live[i].j.resolve(serializeCiphertext(KIND.RADIX_BOOL, 1, this.dim, r.B, r.toValueMajor()));
+          else live[i].j.resolve(serializeCiphertext(KIND.RADIX_UINT, r.width, this.dim, r.B, r.toValueMajor()));
+        } else live[i].j.resolve(serializeCiphertext(this.radix ? KIND.RADIX_BOOL : KIND.BOOL, 1, this.dim, r.length / d, r));
       });
     } catch (e) {
       live.forEach((x) => x.j.reject(e));
@@ -306,7 +354,11 @@ class LuxFHELocalClient {
   /** -> bigint (first value of the ciphertext) */
   async decrypt(bytes) {
     const ct = parseCiphertext(bytes);
-    const c = { dim: this.params.n + 1 };
+    const c = { dim: ct.lweDim + 1 };
+    if (ct.kind >= KIND.RADIX_UINT) {
+      const vec = radix.RadixVec.fromValueMajor(c, ct.words, ct.count, ctsPerValue(ct.kind, ct.width));
+      return radix.decryptRadix(this.clientKey, vec)[0];
+    }
     const vec = integer.FheUintVec.fromValueMajor(c, ct.words, ct.count, ct.width);
     return integer.decryptColumns(this.clientKey, vec.cols, ct.count)[0];
   }
@@ -315,7 +367,7 @@ class LuxFHELocalClient {
 }
 
 module.exports = {
-  native, integer, PRESET_GATE, PRESET_FHEVM, MU, paramsPreset, genKeys, ClientKey, ServerKey, Engine,
+  native, integer, radix, KIND, PRESET_GATE, PRESET_FHEVM, MU, paramsPreset, genKeys, ClientKey, ServerKey, Engine,
   FheBool, FheUint8, FheUint16, FheUint32, FheUint64, UINT_CLASSES, LuxFHELocalClient,
   serializeCiphertext, parseCiphertext,
 };

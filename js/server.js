@@ -15,7 +15,10 @@
  * for all of them).  Single-party: this process holds the client key (like the reference's local
  * dev server); /verify checks ciphertext framing only — there is no ZK proof system on this path.
  *
- *   node js/server.js [--port 8448] [--host 127.0.0.1] [--device 0] [--seed 0x7F4E0001]
+ * --params fhevm serves fhEVM's own representation instead (P-FHEVM radix blocks, js/radix.js:
+ * KS -> PBS at N = 2048, every operator but div/rem).
+ *
+ *   node js/server.js [--port 8448] [--host 127.0.0.1] [--device 0] [--seed 0x7F4E0001] [--params gate|fhevm]
  */
 const http = require('http');
 
@@ -116,11 +119,12 @@ if (require.main === module) {
   const args = process.argv.slice(2);
   const opt = (name, dflt) => { const i = args.indexOf(`--${name}`); return i >= 0 ? args[i + 1] : dflt; };
   const { LuxFHELocalClient } = require('./index.js');
-  const client = new LuxFHELocalClient({ device: Number(opt('device', 0)), seed: BigInt(opt('seed', '0x7F4E0001')) });
+  const params = opt('params', 'gate');
+  const client = new LuxFHELocalClient({ device: Number(opt('device', 0)), seed: BigInt(opt('seed', '0x7F4E0001')), params });
   client.initialize().then(() => {
     const port = Number(opt('port', 8448)), host = opt('host', '127.0.0.1');
-    createServer(client, { device: Number(opt('device', 0)) }).listen(port, host, () => {
-      console.log(`tfhe_amd FHE server on http://${host}:${port}`);
+    createServer(client, { device: Number(opt('device', 0)), params }).listen(port, host, () => {
+      console.log(`tfhe_amd FHE server (${params}) on http://${host}:${port}`);
     });
   }).catch((e) => { console.error(e); process.exit(1); });
 }

@@ -3,13 +3,17 @@
 // (e2e/test/fhe.test.ts) and hardhat plugin.  argv[2] === 'gpu': the real MI355X engine;
 // otherwise a key-holding test double stands in for the gate bootstrap (CPU: phase -> sign ->
 // trivial ciphertext), so the host logic (routes, framing, coalescing, circuits) runs without a GPU.
+// argv[2] === 'fhevm' / 'fhevm-gpu': the same requests on P-FHEVM radix blocks (js/radix.js); the
+// CPU double decrypts each block and applies the bootstrap's table.
 const path = require('path');
 const http = require('http');
 const assert = require('assert');
 const tfhe = require(path.join(__dirname, '..', '..', 'js', 'index.js'));
 const { createServer } = require(path.join(__dirname, '..', '..', 'js', 'server.js'));
 
-const useGpu = process.argv[2] === 'gpu';
+const mode = process.argv[2] || 'cpu';
+const useGpu = mode === 'gpu' || mode === 'fhevm-gpu';
+const fhevm = mode.startsWith('fhevm');
 const HALF = 1n << 63n;
 
 function request(port, method, url, body, headers = {}) {
@@ -41,7 +45,23 @@ function request(port, method, url, body, headers = {}) {
       return out;
     },
   };
-  client = new tfhe.LuxFHELocalClient(useGpu ? {} : { engine: dbl });
+  const rdbl = {
+    params: tfhe.paramsPreset(tfhe.PRESET_FHEVM),
+    lutFromTable(t) { return BigUint64Array.from(t, BigInt); },
+    calls: 0,
+    async pbs(cts, luts, idx) {
+      this.calls++;
+      const d = this.params.k * this.params.N + 1;
+      const v = client.clientKey.decrypt(cts, 16);
+      const out = new BigUint64Array(cts.length);
+      for (let i = 0; i < v.length; i++) out[(i + 1) * d - 1] = luts[idx[i] * this.params.N + v[i]] * tfhe.radix.DELTA;
+      return out;
+    },
+  };
+  const cfg = fhevm ? { params: 'fhevm' } : {};
+  if (!useGpu) cfg.engine = fhevm ? rdbl : dbl;
+  client = new tfhe.LuxFHELocalClient(cfg);
+  const ctBytes = (w) => 16 + 8 * (fhevm ? (w / 2) * 2049 : w * 631);
   await client.initialize();
   const server = createServer(client).listen(0, '127.0.0.1');
   await new Promise((r) => server.on('listening', r));
@@ -56,7 +76,7 @@ function request(port, method, url, body, headers = {}) {
     for (const w of [8, 16, 32, 64]) {
       r = await request(port, 'POST', '/encrypt', { value: 123, bitWidth: w });
       assert.strictEqual(r.status, 200);
-      assert.strictEqual(r.body.length, 16 + 8 * w * 631);
+      assert.strictEqual(r.body.length, ctBytes(w));
     }
     const encA = (await request(port, 'POST', '/encrypt', { value: 42, bitWidth: 32 })).body;
     const encB = (await request(port, 'POST', '/encrypt', { value: 17, bitWidth: 32 })).body;
@@ -80,11 +100,32 @@ function request(port, method, url, body, headers = {}) {
     // verify + errors
     r = await request(port, 'POST', '/verify', Buffer.from([1, 2, 3]));
     assert.strictEqual(JSON.parse(r.body).verified, true);
+    // shifts / rotations (plaintext and encrypted amounts), neg, bitwise, max
+    const enc5 = (await request(port, 'POST', '/encrypt', { value: 5, bitWidth: 8 })).body;
+    const [shl, rotr, shlE, neg, xor, mx] = await Promise.all([
+      request(port, 'POST', '/evaluate', { op: 'shl', left: Array.from(encA), right: 3, bitWidth: 32 }),
+      request(port, 'POST', '/evaluate', { op: 'rotr', left: Array.from(encB), right: 4, bitWidth: 32 }),
+      ev('shl', encB, enc5), request(port, 'POST', '/evaluate', { op: 'neg', left: Array.from(encB), bitWidth: 32 }),
+      ev('xor', encA, encB), ev('max', encA, encB)]);
+    assert.strictEqual(await dec(shl.body), 42n << 3n);
+    assert.strictEqual(await dec(rotr.body), ((17n >> 4n) | (17n << 28n)) & 0xFFFFFFFFn);
+    assert.strictEqual(await dec(shlE.body), 17n << 5n);
+    assert.strictEqual(await dec(neg.body), (1n << 32n) - 17n);
+    assert.strictEqual(await dec(xor.body), 42n ^ 17n);
+    assert.strictEqual(await dec(mx.body), 42n);
+    // ebool
+    const t = (await request(port, 'POST', '/encrypt', { value: 1, bitWidth: 1 })).body;
+    const f = (await request(port, 'POST', '/encrypt', { value: 0, bitWidth: 1 })).body;
+    const [band, bor, bnot] = await Promise.all([ev('and', t, f), ev('or', t, f),
+      request(port, 'POST', '/evaluate', { op: 'not', left: Array.from(f), bitWidth: 1 })]);
+    assert.strictEqual(await dec(band.body), 0n);
+    assert.strictEqual(await dec(bor.body), 1n);
+    assert.strictEqual(await dec(bnot.body), 1n);
     r = await request(port, 'POST', '/evaluate', { op: 'pow', left: Array.from(encA), right: Array.from(encB), bitWidth: 32 });
     assert.strictEqual(r.status, 400);
     r = await request(port, 'POST', '/decrypt', { ciphertext: [1, 2, 3] });
     assert.strictEqual(r.status, 400);
-    console.log(`OK server (${useGpu ? 'gpu' : 'cpu double'}), evaluate launches ${client.launches}`);
+    console.log(`OK server (${useGpu ? 'gpu' : 'cpu double'}${fhevm ? ', fhevm radix' : ''}), evaluate launches ${client.launches}`);
   } finally {
     server.close();
     client.close();

@@ -64,9 +64,32 @@ def test_js_integer_kats_cpu():
     assert _run_plain("integer_check.js").startswith("OK 936 KATs, 27 launches")
 
 
+def test_js_radix_kats_cpu():
+    """js/radix.js replays the 912 radix-layer fhEVM KATs with the same launch and PBS counts as
+    tfhe_amd/radix.py (tests/test_radix.py) — the two layers build identical circuits."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_radix import GOLDEN, CleartextRadixCircuit, kat_op, supported
+    with open(GOLDEN) as f:
+        kats = [k for k in json.load(f) if supported(k)]
+    c = CleartextRadixCircuit()
+    c.run_many([kat_op(c, k) for k in kats])
+    assert _run_plain("radix_check.js") == f"OK {len(kats)} {c.launches} {c.pbs_count}"
+
+
 def test_js_server_cpu():
     """js/server.js over HTTP with the reference's request shapes (fhe.test.ts, hardhat plugin)."""
     assert _run_plain("server_check.js").startswith("OK server")
+
+
+def test_js_server_fhevm_cpu():
+    """The same requests on P-FHEVM radix blocks (server --params fhevm)."""
+    assert _run_plain("server_check.js", "fhevm").startswith("OK server (cpu double, fhevm radix)")
+
+
+@pytest.mark.gpu
+def test_js_server_fhevm_gpu():
+    assert _run_plain("server_check.js", "fhevm-gpu", timeout=900).startswith("OK server (gpu, fhevm radix)")
 
 
 @pytest.mark.gpu
