@@ -227,7 +227,7 @@ const FheUint64 = UINT_CLASSES[64];
  * the POST /evaluate shape (e2e/test/fhe.test.ts:105-175) and runs every fhEVM operator on the GPU.
  * Requests submitted concurrently are evaluated in lockstep (one PBS launch per circuit level).
  * config.params: a params object, or 'gate' (default: boolean gates, js/integer.js) or 'fhevm'
- * (P-FHEVM radix blocks, js/radix.js — fhEVM's own representation; div/rem only in 'gate').
+ * (P-FHEVM radix blocks, js/radix.js — fhEVM's own representation).
  */
 class LuxFHELocalClient {
   constructor(config = {}) {

@@ -285,7 +285,39 @@ function* gShiftEnc(c, a, amount, kind, B) {
   return cur;
 }
 
-const RADIX_OPS = ['add', 'sub', 'mul', 'and', 'or', 'xor', 'eq', 'ne', 'lt', 'le', 'gt', 'ge', 'min', 'max', 'neg', 'not', 'shl', 'shr', 'rotl', 'rotr'];
+const T_LOW_BIT = table((v) => v & 1);
+
+/** (a / d, a % d) for a plaintext divisor by multiply-high (radix.py g_div_rem_scalar) */
+function* gDivRemScalar(c, a, d, B) {
+  const nb = a.length;
+  const w = 2 * nb;
+  d = BigInt.asUintN(w, BigInt(d));
+  if (d === 0n) return [a.map(() => c.const(B, MSG - 1)), a];
+  if ((d & (d - 1n)) === 0n) {
+    const s = d.toString(2).length - 1;
+    const q = s ? yield* gShift(c, a, s, 'shr', B) : a;
+    const keep = Math.floor(s / 2);
+    const rem = a.slice(0, keep);
+    if (s % 2) rem.push((yield [[a[keep], T_LOW_BIT]])[0]);
+    while (rem.length < nb) rem.push(c.const(B, 0));
+    return [q, rem];
+  }
+  const l = BigInt((d - 1n).toString(2).length);
+  const W = BigInt(w);
+  const m = ((1n << (W + l)) + d - 1n) / d;
+  const nbw = w + 1;
+  const aExt = a.concat(Array.from({ length: nbw - nb }, () => c.const(B, 0)));
+  const prod = yield* gMul(c, aExt, m, B);
+  const k = w + Number(l);
+  let sub = prod.slice(Math.floor(k / 2), Math.floor(k / 2) + nb + 1);
+  while (sub.length < nb + 1) sub.push(c.const(B, 0));
+  const q = (k % 2 ? yield* gShift(c, sub, 1, 'shr', B) : sub).slice(0, nb);
+  const qd = yield* gMul(c, q, d, B);
+  const r = yield* gPropagate(c, a.map((x, i) => c.add(x, c.not(qd[i]))), B, true);
+  return [q, r];
+}
+
+const RADIX_OPS = ['add', 'sub', 'mul', 'div', 'rem', 'and', 'or', 'xor', 'eq', 'ne', 'lt', 'le', 'gt', 'ge', 'min', 'max', 'neg', 'not', 'shl', 'shr', 'rotl', 'rotr'];
 
 /** one fhEVM operator on radix values (lhs/rhs: RadixVec or plaintext bigint); bool results are a block column */
 function* fhevmOp(c, op, lhs, rhs = null) {
@@ -302,6 +334,11 @@ function* fhevmOp(c, op, lhs, rhs = null) {
     if (!lE) throw new Error('shift of a plaintext by an encrypted amount is not an fhEVM overload');
     if (rE) return new RadixVec(c, yield* gShiftEnc(c, lhs.blocks, rhs.blocks, op, lhs.B), lhs.B);
     return new RadixVec(c, yield* gShift(c, lhs.blocks, Number(BigInt(rhs) % BigInt(lhs.width)), op, lhs.B), lhs.B);
+  }
+  if (op === 'div' || op === 'rem') {
+    if (!lE || rE) throw new Error('fhEVM div / rem take an encrypted numerator and a plaintext divisor');
+    const [q, r] = yield* gDivRemScalar(c, lhs.blocks, rhs, lhs.B);
+    return new RadixVec(c, op === 'div' ? q : r, lhs.B);
   }
   const w = Math.max(...[lhs, rhs].filter(isV).map((x) => x.width));
   const B = (lE ? lhs : rhs).B;

@@ -1,7 +1,7 @@
 'use strict';
-// CPU check of js/radix.js: every radix-layer fhEVM KAT (tests/golden/fhevm_kats.json, all ops
-// but div/rem) with a cleartext double of the multi-LUT PBS on trivial blocks (asserts no block
-// ever reaches the padding bit), all KATs in lockstep; then a random batch per operator.
+// CPU check of js/radix.js: every fhEVM KAT (tests/golden/fhevm_kats.json) with a cleartext
+// double of the multi-LUT PBS on trivial blocks (asserts no block ever reaches the padding bit),
+// all KATs in lockstep; then a random batch per operator (div/rem over several divisors).
 // Prints "OK <kats> <launches> <pbs>" — tests/test_js.py compares the counts with tfhe_amd/radix.py.
 const path = require('path');
 const assert = require('assert');
@@ -76,6 +76,11 @@ const width = (t) => (t === 'ebool' ? 1 : Number(t.replace('euint', '').replace(
   assert.deepStrictEqual(R.decryptRadix(clearKey, neg), a.map((x) => (0n - x) & m));
   assert.deepStrictEqual(R.decryptRadix(clearKey, not), a.map((x) => x ^ m));
   assert.deepStrictEqual(R.decryptRadix(clearKey, shl5), a.map((x) => (x << 5n) & m));
+  for (const d of [0n, 1n, 4n, 7n, 8n, 1000n, 65535n]) {
+    const [q, r] = await c2.runMany([R.fhevmOp(c2, 'div', A, d), R.fhevmOp(c2, 'rem', A, d)]);
+    assert.deepStrictEqual(R.decryptRadix(clearKey, q), a.map((x) => (d === 0n ? m : x / d)), `div ${d}`);
+    assert.deepStrictEqual(R.decryptRadix(clearKey, r), a.map((x) => (d === 0n ? x : x % d)), `rem ${d}`);
+  }
   const rt = R.RadixVec.fromValueMajor(c2, A.toValueMajor(), B, 8);
   assert.deepStrictEqual(R.decryptRadix(clearKey, rt), a);
   console.log(`OK ${kats.length} ${katLaunches} ${katPbs}`);

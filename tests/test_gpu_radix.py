@@ -1,5 +1,5 @@
 """Radix integers (tfhe_amd/radix.py) on the MI355X at the production fhEVM parameters: every
-reference fhEVM operator KAT the radix layer supports, encrypted under the P-FHEVM key, evaluated
+reference fhEVM operator KAT (all 936, div/rem included), encrypted under the P-FHEVM key, evaluated
 in lockstep (one multi-LUT PBS launch per circuit level) and decrypted."""
 import json
 import os
@@ -58,3 +58,22 @@ def test_radix_batch_gpu(fhevm_engine, fhevm_keys):
     np.testing.assert_array_equal(add.decrypt(ck), (a + b) & m)
     np.testing.assert_array_equal(ck.decrypt(lt, R.SPACE).astype(bool), a < b)
     np.testing.assert_array_equal(mx.decrypt(ck), np.maximum(a, b))
+
+
+def test_radix_div_rem_gpu(fhevm_engine, fhevm_keys):
+    """division / remainder by plaintext divisors (multiply-high, power-of-two and d = 0 paths)."""
+    ck, _ = fhevm_keys
+    rng = np.random.default_rng(77)
+    B, w = 64, 32
+    a = rng.integers(0, 1 << w, B, dtype=np.uint64)
+    a[:2] = [0, (1 << w) - 1]
+    c = R.RadixCircuit(fhevm_engine)
+    A = R.RadixUint.encrypt(c, ck, a, w, seed=3, stream0=0)
+    cases = [("div", 7), ("rem", 1000), ("div", 32), ("rem", 32), ("rem", 550954323), ("div", 0)]
+    res = c.run_many([R.fhevm_op(c, op, A, d) for op, d in cases])
+    for (op, d), r in zip(cases, res):
+        if d == 0:
+            want = np.full_like(a, (1 << w) - 1)
+        else:
+            want = a // np.uint64(d) if op == "div" else a % np.uint64(d)
+        np.testing.assert_array_equal(r.decrypt(ck), want, err_msg=f"{op} {d}")

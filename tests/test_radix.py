@@ -53,7 +53,7 @@ def check(ck, k, r):
 
 
 def supported(k):
-    return k["op"] in R.RADIX_OPS         # everything but div / rem (boolean layer)
+    return k["op"] in R.RADIX_OPS         # every fhEVM operator
 
 
 @pytest.fixture(scope="module")
@@ -63,7 +63,7 @@ def kats():
 
 
 def test_radix_kats_cleartext(kats):
-    assert len(kats) == 912
+    assert len(kats) == 936
     c = CleartextRadixCircuit()
     ck = ClearKey()
     res = c.run_many([kat_op(c, k) for k in kats])
@@ -101,3 +101,25 @@ def test_radix_random_batch(w):
                    "rotl": [((x << kk) | (x >> (w - kk))) & m for x in v],
                    "rotr": [((x >> kk) | (x << (w - kk))) & m for x in v]}[kind]
             np.testing.assert_array_equal(r.decrypt(ck), np.array(exp, dtype=np.uint64), err_msg=f"{kind} {k}")
+
+
+@pytest.mark.parametrize("w,divisors", [(8, [0, 1, 2, 3, 7, 8, 76, 128, 180, 255]),
+                                         (32, [5, 550954323, 1 << 31, (1 << 32) - 1])])
+def test_radix_div_rem_scalar(w, divisors):
+    """multiply-high division against // and % (exhaustive numerators at w=8, edge values at w=32);
+    d = 0 gives quotient all ones and remainder = numerator (tfhe-rs / fhEVM)."""
+    rng = np.random.default_rng(w)
+    m = (1 << w) - 1
+    a = np.arange(256, dtype=np.uint64) if w == 8 else np.concatenate(
+        [np.array([0, 1, m, m - 1, 550954323, 550954322], dtype=np.uint64), rng.integers(0, 1 << w, 40, dtype=np.uint64)])
+    c = CleartextRadixCircuit()
+    ck = ClearKey()
+    A = R.RadixUint.trivial(c, a, w)
+    res = c.run_many([R.fhevm_op(c, op, A, d) for d in divisors for op in ("div", "rem")])
+    for t, d in enumerate(divisors):
+        q, r = res[2 * t].decrypt(ck), res[2 * t + 1].decrypt(ck)
+        wq = np.full_like(a, m) if d == 0 else a // np.uint64(d)
+        wr = a if d == 0 else a % np.uint64(d)
+        np.testing.assert_array_equal(q, wq, err_msg=f"div {d}")
+        np.testing.assert_array_equal(r, wr, err_msg=f"rem {d}")
+    assert c.max_seen <= 15

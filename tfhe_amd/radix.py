@@ -15,7 +15,8 @@ lt/le/gt/ge (per-block {<, =, >} + MSB-first merge tree), min/max (compare + 2-P
 shl/shr/rotl/rotr by a plaintext amount (block moves + one bivariate level for odd shifts) or an
 encrypted one (barrel shifter over the amount's bits), mul (block products by bivariate low/high
 digit tables, carry-save reduction rounds of up to 5 blocks, final prefix add; plaintext factors by
-univariate tables), plaintext right operands, mixed widths zero-extended.
+univariate tables), div/rem by a plaintext divisor (multiply-high by a (w+1)-bit reciprocal),
+plaintext right operands, mixed widths zero-extended.
 """
 from __future__ import annotations
 
@@ -417,7 +418,48 @@ def g_shift_enc(c, a, amount, kind: str):
     return cur
 
 
-RADIX_OPS = ("add", "sub", "mul", "and", "or", "xor", "eq", "ne", "lt", "le", "gt", "ge", "min", "max",
+T_LOW_BIT = _table(lambda v: v & 1)
+
+
+def g_div_rem_scalar(c, a, d: int):
+    """(a // d, a % d) for a plaintext divisor by multiply-high: with l = ceil(log2 d) and
+    m = ceil(2^(w+l) / d) (w + 1 bits), floor(a * m / 2^(w+l)) = floor(a / d) for every a < 2^w
+    (m*d - 2^(w+l) < d, so the error term a*(m*d - 2^(w+l)) / d < 2^(w+l) never crosses an integer).
+    One constant multiply at width 2w + 2, a block shift, one constant multiply and one subtract.
+    d = 0 follows tfhe-rs / fhEVM: quotient all ones, remainder = numerator.  Powers of two are a
+    block shift and a mask."""
+    B, nb = a.shape[:2]
+    w = 2 * nb
+    d = int(d) % (1 << w)
+    if d == 0:
+        return _const(c, (B, nb), MSG - 1), a
+    if d & (d - 1) == 0:
+        s = d.bit_length() - 1
+        q = (yield from g_shift(c, a, s, "shr")) if s else a
+        keep = s // 2
+        parts = [a[:, :keep]]
+        if s % 2:
+            (lowbit,) = yield [(a[:, keep], T_LOW_BIT)]
+            parts.append(lowbit[:, None])
+        done = keep + s % 2
+        parts.append(_const(c, (B, nb - done), 0))
+        return q, np.concatenate(parts, axis=1)
+    l = (d - 1).bit_length()
+    m = -(-(1 << (w + l)) // d)
+    nbw = w + 1                                             # width 2w + 2 holds a * m < 2^(2w+1)
+    a_ext = np.concatenate([a, _const(c, (B, nbw - nb), 0)], axis=1)
+    prod = yield from g_mul(c, a_ext, m)
+    k = w + l
+    sub = prod[:, k // 2:k // 2 + nb + 1]
+    if sub.shape[1] < nb + 1:
+        sub = np.concatenate([sub, _const(c, (B, nb + 1 - sub.shape[1]), 0)], axis=1)
+    q = (yield from g_shift(c, sub, k % 2, "shr"))[:, :nb] if k % 2 else sub[:, :nb]
+    qd = yield from g_mul(c, q, d)
+    r = yield from g_sub(c, a, qd)
+    return q, r
+
+
+RADIX_OPS = ("add", "sub", "mul", "div", "rem", "and", "or", "xor", "eq", "ne", "lt", "le", "gt", "ge", "min", "max",
              "neg", "not", "shl", "shr", "rotl", "rotr")
 
 
@@ -448,6 +490,11 @@ def fhevm_op(c: RadixCircuit, op: str, lhs, rhs=None):
             return x.cast(w).blocks
         return c.trivial(np.broadcast_to(RadixUint._digits([int(x) % (1 << w)], w), (B, w // 2)))
 
+    if op in ("div", "rem"):
+        if not lenc or renc:
+            raise ValueError("fhEVM div / rem take an encrypted numerator and a plaintext divisor")
+        q, r = yield from g_div_rem_scalar(c, lhs.blocks, int(rhs))
+        return RadixUint(c, q if op == "div" else r)
     if op == "mul":
         if not lenc:
             return RadixUint(c, (yield from g_mul(c, rhs.cast(w).blocks, int(lhs) % (1 << w))))
