@@ -73,6 +73,17 @@ int tfhe_hip_keygen(const tfhe_params* p, uint64_t seed, uint64_t* lwe_key, uint
  * tfhe_hip_keygen.  EINVAL if a key word is not 0/1. */
 int tfhe_hip_server_keygen(const tfhe_params* p, uint64_t seed, const uint64_t* lwe_key, const uint64_t* glwe_key,
                            uint64_t* bsk /* nullable */, uint64_t* ksk /* nullable */);
+/* Modulus-switch noise reduction key of the P-FHEVM server key (the
+ * reference's parameter block carries modulus_switch_zeros_count 1449, ms_bound 2^58,
+ * ms_r_sigma_factor 13.179852282053789, ms_input_variance 2.63039184094559e-07 —
+ * sdk/relayer/src/test/keys/privateKey.bin @0x5e04..0x5e30).  count LWE encryptions of 0 under
+ * the small key, count x (n+1) u64; zero z on ChaCha stream 0x200000 + z. */
+#define TFHE_HIP_MS_FHEVM_ZEROS 1449u
+#define TFHE_HIP_MS_FHEVM_BOUND 0x1p58
+#define TFHE_HIP_MS_FHEVM_R_SIGMA 13.179852282053789
+#define TFHE_HIP_MS_FHEVM_INPUT_VARIANCE 2.63039184094559e-07
+int tfhe_hip_ms_zeros_keygen(const tfhe_params* p, uint64_t seed, const uint64_t* lwe_key, uint32_t count,
+                             uint64_t* zeros);
 /* Encrypt count torus messages; ciphertext q uses ChaCha stream (stream0 + q).
  * Replaces the encrypt path of packages/luxfhejs/src/index.ts:127-141 (server-side /encrypt). */
 int tfhe_hip_lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, uint64_t seed,
@@ -97,6 +108,17 @@ int tfhe_hip_load_keys(tfhe_ctx* ctx, const uint64_t* bsk, size_t bsk_len, const
 /* Same, from DEVICE buffers on this ctx's device (e.g. after an RCCL broadcast of the keys). */
 int tfhe_hip_load_keys_device(tfhe_ctx* ctx, const uint64_t* d_bsk, size_t bsk_len, const uint64_t* d_ksk,
                               size_t ksk_len);
+
+/* Enable the modulus-switch noise reduction between keyswitch and blind rotation (order 1 only;
+ * count = 0 disables).  Before each blind rotation the ciphertext gets the one zero whose
+ * measure |E[err]| + r_sigma * sd(err) of the switch to 2N is best (tfhe-rs 1.x
+ * improve_lwe_ciphertext_modulus_switch_noise_for_binary_key; exact rule in oracle/tfhe_oracle.h).
+ * EUNSUPPORTED for order 0 parameter sets. */
+int tfhe_hip_load_ms_key(tfhe_ctx* ctx, const uint64_t* zeros, uint32_t count, double bound, double r_sigma,
+                         double input_variance);
+/* Stage-level: the reduction alone on B small-key ciphertexts (B x (n+1)); picks (nullable, B
+ * entries) receives the chosen zero index or -1. */
+int tfhe_hip_ms_reduce(tfhe_ctx* ctx, const uint64_t* lwe_small, size_t B, uint64_t* out, int32_t* picks);
 
 /* Full PBS of B ciphertexts: order 0 = blind-rotate -> sample-extract -> keyswitch.
  * luts: n_lut LUTs of N values; lut_index (nullable, B entries) picks the LUT per ciphertext.
@@ -135,7 +157,8 @@ int tfhe_hip_set_latency_batch(tfhe_ctx* ctx, size_t max_batch);
 int tfhe_hip_sync(tfhe_ctx* ctx);
 /* Per-kernel device timing (HIP events recorded on the launch stream around every blind-rotate /
  * keyswitch launch).  reset clears the record; stats waits for the recorded events and returns the
- * summed milliseconds and the launch count.  which: 0 = blind rotate (+sample extract), 1 = keyswitch.
+ * summed milliseconds and the launch count.  which: 0 = blind rotate (+sample extract), 1 = keyswitch,
+ * 2 = modulus-switch noise reduction.
  * Used by bench.py for the roofline figure. */
 int tfhe_hip_timing_enable(tfhe_ctx* ctx, int enable);
 int tfhe_hip_timing_reset(tfhe_ctx* ctx);

@@ -20,7 +20,7 @@ export class ClientKey {
   encrypt(values: Iterable<number | bigint>, msgModulus: number, seed?: bigint, stream0?: bigint): BigUint64Array;
   decrypt(cts: BigUint64Array, msgModulus: number): number[];
 }
-export class ServerKey { readonly params: TfheParams; readonly bsk: BigUint64Array; readonly ksk: BigUint64Array; }
+export class ServerKey { readonly params: TfheParams; readonly bsk: BigUint64Array; readonly ksk: BigUint64Array; readonly msZeros: BigUint64Array | null; }
 export function genKeys(params?: TfheParams, seed?: bigint): [ClientKey, ServerKey];
 
 export class Engine {

@@ -67,13 +67,14 @@ class ClientKey {
 }
 
 class ServerKey {
-  constructor(params, bsk, ksk) { this.params = params; this.bsk = bsk; this.ksk = ksk; }
+  // msZeros: P-FHEVM modulus-switch noise-reduction zeros (KS -> PBS parameter sets only)
+  constructor(params, bsk, ksk, msZeros = null) { this.params = params; this.bsk = bsk; this.ksk = ksk; this.msZeros = msZeros; }
 }
 
 /** tfhe-rs gen_keys analogue: deterministic ChaCha20-seeded key set -> [ClientKey, ServerKey] */
 function genKeys(params = paramsPreset(), seed = 0x7F4E0001n) {
   const k = native.keygen(params, BigInt(seed), true);
-  return [new ClientKey(k.params, seed, k.lweKey, k.glweKey), new ServerKey(k.params, k.bsk, k.ksk)];
+  return [new ClientKey(k.params, seed, k.lweKey, k.glweKey), new ServerKey(k.params, k.bsk, k.ksk, k.msZeros || null)];
 }
 
 class Engine {
@@ -81,7 +82,7 @@ class Engine {
     this.params = params;
     this.handle = native.createEngine(params, device);
   }
-  loadKeys(serverKey) { native.loadKeys(this.handle, serverKey.bsk, serverKey.ksk); return this; }
+  loadKeys(serverKey) { native.loadKeys(this.handle, serverKey.bsk, serverKey.ksk, serverKey.msZeros || null); return this; }
   destroy() { if (this.handle) { native.destroyEngine(this.handle); this.handle = null; } }
   gateLut() { return native.lutConstant(this.params.N, MU); }
   generateAccumulator(f, msgModulus = 4, deltaOut = null) {

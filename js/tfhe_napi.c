@@ -137,8 +137,8 @@ static napi_value js_keygen(napi_env env, napi_callback_info info) {
   }
   bool with_sk = true;
   if (argc > 2) napi_get_value_bool(env, argv[2], &with_sk);
-  uint64_t *lwe, *glwe, *bsk = NULL, *ksk = NULL;
-  napi_value o, a_lwe, a_glwe, a_bsk = NULL, a_ksk = NULL;
+  uint64_t *lwe, *glwe, *bsk = NULL, *ksk = NULL, *zeros = NULL;
+  napi_value o, a_lwe, a_glwe, a_bsk = NULL, a_ksk = NULL, a_zeros = NULL;
   a_lwe = new_u64_array(env, p.n, &lwe);
   a_glwe = new_u64_array(env, (size_t)p.k * p.N, &glwe);
   if (!a_lwe || !a_glwe) return throw_tfhe(env, TFHE_HIP_ENOMEM);
@@ -149,12 +149,19 @@ static napi_value js_keygen(napi_env env, napi_callback_info info) {
   }
   int rc = tfhe_hip_keygen(&p, seed, lwe, glwe, bsk, ksk);
   if (rc) return throw_tfhe(env, rc);
+  if (with_sk && p.order == 1) { /* KS -> PBS server keys carry the modulus-switch zeros */
+    a_zeros = new_u64_array(env, (size_t)TFHE_HIP_MS_FHEVM_ZEROS * (p.n + 1), &zeros);
+    if (!a_zeros) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+    rc = tfhe_hip_ms_zeros_keygen(&p, seed, lwe, TFHE_HIP_MS_FHEVM_ZEROS, zeros);
+    if (rc) return throw_tfhe(env, rc);
+  }
   napi_create_object(env, &o);
   napi_set_named_property(env, o, "lweKey", a_lwe);
   napi_set_named_property(env, o, "glweKey", a_glwe);
   if (with_sk) {
     napi_set_named_property(env, o, "bsk", a_bsk);
     napi_set_named_property(env, o, "ksk", a_ksk);
+    if (a_zeros) napi_set_named_property(env, o, "msZeros", a_zeros);
   }
   napi_set_named_property(env, o, "params", params_to_js(env, &p));
   return o;
@@ -296,20 +303,36 @@ static napi_value js_destroy(napi_env env, napi_callback_info info) {
 }
 
 /* loadKeys(handle, bsk, ksk) */
+/* loadKeys(engine, bsk, ksk[, msZeros]) — msZeros enables the P-FHEVM modulus-switch noise reduction */
 static napi_value js_load_keys(napi_env env, napi_callback_info info) {
-  size_t argc = 3;
-  napi_value argv[3];
+  size_t argc = 4;
+  napi_value argv[4];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   ctx_box* b = argc ? get_box(env, argv[0]) : NULL;
   uint64_t *bsk, *ksk;
   size_t bl, kl;
   if (!b || !b->ctx || argc < 3 || !get_typed(env, argv[1], napi_biguint64_array, (void**)&bsk, &bl) ||
       !get_typed(env, argv[2], napi_biguint64_array, (void**)&ksk, &kl)) {
-    napi_throw_type_error(env, "EINVAL", "loadKeys(engine, bsk, ksk)");
+    napi_throw_type_error(env, "EINVAL", "loadKeys(engine, bsk, ksk[, msZeros])");
     return NULL;
+  }
+  uint64_t* zeros = NULL;
+  size_t zl = 0;
+  if (argc > 3) {
+    napi_valuetype t;
+    napi_typeof(env, argv[3], &t);
+    if (t != napi_undefined && t != napi_null && !get_typed(env, argv[3], napi_biguint64_array, (void**)&zeros, &zl)) {
+      napi_throw_type_error(env, "EINVAL", "loadKeys: msZeros must be a BigUint64Array");
+      return NULL;
+    }
   }
   int rc = tfhe_hip_load_keys(b->ctx, bsk, bl, ksk, kl);
   if (rc) return throw_tfhe(env, rc);
+  if (zeros) {
+    rc = tfhe_hip_load_ms_key(b->ctx, zeros, (uint32_t)(zl / (b->p.n + 1)), TFHE_HIP_MS_FHEVM_BOUND,
+                              TFHE_HIP_MS_FHEVM_R_SIGMA, TFHE_HIP_MS_FHEVM_INPUT_VARIANCE);
+    if (rc) return throw_tfhe(env, rc);
+  }
   return NULL;
 }
 

@@ -30,6 +30,15 @@ class Params(ctypes.Structure):
     ]
 
 
+class MsKey(ctypes.Structure):
+    _fields_ = [("zeros", ctypes.c_void_p), ("count", ctypes.c_uint32), ("bound", ctypes.c_double),
+                ("r_sigma", ctypes.c_double), ("input_variance", ctypes.c_double)]
+
+
+# P-FHEVM modulus-switch noise reduction (tfhe_oracle.h: or_ms_key)
+MS_FHEVM = dict(count=1449, bound=2.0 ** 58, r_sigma=13.179852282053789, input_variance=2.63039184094559e-07)
+
+
 def build() -> str:
     """Compile liboracle.so with the committed Makefile (gcc)."""
     import subprocess
@@ -60,6 +69,9 @@ def lib():
         L.or_p_to_tor.argtypes = [ctypes.c_uint64]
         L.or_mod_switch.restype = ctypes.c_uint32
         L.or_mod_switch.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
+        L.or_ms_measure.restype = ctypes.c_double
+        L.or_ms_measure.argtypes = [ctypes.c_void_p, ctypes.c_void_p, U64P, U64P]
+        L.or_ms_reduce.restype = ctypes.c_int
         L.or_bsk_len.restype = ctypes.c_size_t
         L.or_ksk_len.restype = ctypes.c_size_t
         _LIB = L
@@ -139,6 +151,23 @@ class Keys:
         L.or_keygen(ctypes.byref(prm), ctypes.c_uint64(seed), _p(self.lwe_key), _p(self.glwe_key),
                     _p(self.bsk) if with_bsk else None, _p(self.ksk) if with_ksk else None)
         self._bsk_ntt = None
+        self._ms_zeros_keygen()
+
+    def _ms_zeros_keygen(self):
+        """P-FHEVM (KS -> PBS) server keys carry the modulus-switch zeros; P-GATE none."""
+        self.ms_zeros = None
+        if self.prm.order == 1:
+            self.ms_zeros = np.zeros((MS_FHEVM["count"], self.prm.n + 1), dtype=np.uint64)
+            lib().or_ms_zeros_keygen(ctypes.byref(self.prm), ctypes.c_uint64(self.seed), _p(self.lwe_key),
+                                     ctypes.c_uint32(MS_FHEVM["count"]), _p(self.ms_zeros))
+
+    def ms_key(self, enabled: bool = True):
+        if not enabled or self.ms_zeros is None:
+            return None
+        k = MsKey(self.ms_zeros.ctypes.data, self.ms_zeros.shape[0], MS_FHEVM["bound"], MS_FHEVM["r_sigma"],
+                  MS_FHEVM["input_variance"])
+        k._keep = self.ms_zeros
+        return k
 
     @classmethod
     def from_secret(cls, prm: Params, seed: int, lwe_key: np.ndarray, glwe_key: np.ndarray) -> "Keys":
@@ -153,6 +182,7 @@ class Keys:
         L.or_server_keygen(ctypes.byref(prm), ctypes.c_uint64(seed), _p(k.lwe_key), _p(k.glwe_key), _p(k.bsk),
                            _p(k.ksk))
         k._bsk_ntt = None
+        k._ms_zeros_keygen()
         return k
 
     @property
@@ -208,8 +238,24 @@ def keyswitch(prm: Params, keys: Keys, lwe_big: np.ndarray) -> np.ndarray:
     return out
 
 
+def ms_measure(prm: Params, keys: Keys, ct: np.ndarray, zero_index=None) -> float:
+    ms = keys.ms_key()
+    ct = np.ascontiguousarray(ct, dtype=np.uint64)
+    z = None if zero_index is None else _p(np.ascontiguousarray(keys.ms_zeros[zero_index]))
+    return lib().or_ms_measure(ctypes.byref(prm), ctypes.byref(ms), _p(ct), z)
+
+
+def ms_reduce(prm: Params, keys: Keys, small: np.ndarray):
+    """-> (reduced ciphertexts, chosen zero index per ciphertext or -1)"""
+    ms = keys.ms_key()
+    out = np.ascontiguousarray(small, dtype=np.uint64).reshape(-1, prm.n + 1).copy()
+    picks = np.array([lib().or_ms_reduce(ctypes.byref(prm), ctypes.byref(ms), _p(out[i])) for i in range(out.shape[0])],
+                     dtype=np.int64)
+    return out, picks
+
+
 def pbs_batch(prm: Params, keys: Keys, lwe_in: np.ndarray, luts: np.ndarray, lut_index=None,
-              threads: int = 0) -> np.ndarray:
+              threads: int = 0, ms: bool = True) -> np.ndarray:
     lwe_in = np.ascontiguousarray(lwe_in, dtype=np.uint64)
     luts = np.ascontiguousarray(luts, dtype=np.uint64).reshape(-1, prm.N)
     B = lwe_in.shape[0]
@@ -218,7 +264,9 @@ def pbs_batch(prm: Params, keys: Keys, lwe_in: np.ndarray, luts: np.ndarray, lut
     li = None
     if lut_index is not None:
         li = np.ascontiguousarray(lut_index, dtype=np.uint32)
-    lib().or_pbs_batch(ctypes.byref(prm), _p(keys.bsk_ntt), _p(keys.ksk), _p(lwe_in), ctypes.c_size_t(B),
+    msk = keys.ms_key(ms)
+    lib().or_pbs_batch_ex(ctypes.byref(prm), _p(keys.bsk_ntt), _p(keys.ksk), ctypes.byref(msk) if msk else None,
+                       _p(lwe_in), ctypes.c_size_t(B),
                        _p(luts), ctypes.c_size_t(luts.shape[0]), _p(li, U32P) if li is not None else None,
                        _p(out), ctypes.c_int(threads))
     return out

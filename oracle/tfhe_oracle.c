@@ -534,8 +534,80 @@ void or_keyswitch(const or_params* p, const uint64_t* ksk, const uint64_t* in, u
   }
 }
 
+/* ======================================================================================
+ * Modulus-switch noise reduction (header: or_ms_key).
+ * ==================================================================================== */
+void or_ms_zeros_keygen(const or_params* p, uint64_t seed, const uint64_t* lwe_key, uint32_t count,
+                        uint64_t* zeros) {
+#pragma omp parallel for schedule(static)
+  for (uint32_t z = 0; z < count; z++) {
+    or_rng rr;
+    or_rng_init(&rr, seed, 0x200000 + z);
+    lwe_encrypt_one(p->n, lwe_key, p->lwe_noise_log2, &rr, 0, zeros + (size_t)z * (p->n + 1));
+  }
+}
+
+static uint32_t log2u(uint32_t x) {
+  uint32_t l = 0;
+  while ((1u << l) < x) l++;
+  return l;
+}
+
+/* signed error of the switch to 2N (tfhe-rs modulus_switch: ((x >> (s-1)) + 1) >> 1) */
+static inline int64_t ms_err(uint64_t x, uint32_t shift) {
+  uint64_t r = ((x >> (shift - 1)) + 1) >> 1;
+  return (int64_t)((r << shift) - x);
+}
+
+static double ms_measure_sums(const or_ms_key* ms, int64_t s1, unsigned __int128 s2, int64_t eb) {
+  const double mean = (double)(2 * eb - s1) * 0.5;
+  const double sq = (double)(uint64_t)(s2 >> 64) * 0x1p64 + (double)(uint64_t)s2;
+  const double var = sq * 0.25 + ms->input_variance * 0x1p128;
+  const double sd = sqrt(var);
+  const double dev = ms->r_sigma * sd;
+  return fabs(mean) + dev;
+}
+
+double or_ms_measure(const or_params* p, const or_ms_key* ms, const uint64_t* ct, const uint64_t* zero) {
+  const uint32_t shift = 64 - log2u(2 * p->N);
+  int64_t s1 = 0;
+  unsigned __int128 s2 = 0;
+  for (uint32_t i = 0; i < p->n; i++) {
+    const int64_t e = ms_err(ct[i] + (zero ? zero[i] : 0), shift);
+    s1 += e;
+    s2 += (unsigned __int128)((__int128)e * e);
+  }
+  const int64_t eb = ms_err(ct[p->n] + (zero ? zero[p->n] : 0), shift);
+  return ms_measure_sums(ms, s1, s2, eb);
+}
+
+int or_ms_reduce(const or_params* p, const or_ms_key* ms, uint64_t* ct) {
+  if (!ms || !ms->count) return -1;
+  double best = or_ms_measure(p, ms, ct, NULL);
+  if (best <= ms->bound) return -1;
+  int pick = -1;
+  for (uint32_t z = 0; z < ms->count; z++) {
+    const double m = or_ms_measure(p, ms, ct, ms->zeros + (size_t)z * (p->n + 1));
+    if (m < best) {
+      best = m;
+      pick = (int)z;
+      if (best <= ms->bound) break;
+    }
+  }
+  if (pick >= 0) {
+    const uint64_t* zr = ms->zeros + (size_t)pick * (p->n + 1);
+    for (uint32_t i = 0; i <= p->n; i++) ct[i] += zr[i];
+  }
+  return pick;
+}
+
 void or_pbs(const or_params* p, const uint64_t* bsk_ntt, const uint64_t* ksk, const uint64_t* lwe_in,
             const uint64_t* lut, uint64_t* lwe_out) {
+  or_pbs_ex(p, bsk_ntt, ksk, NULL, lwe_in, lut, lwe_out);
+}
+
+void or_pbs_ex(const or_params* p, const uint64_t* bsk_ntt, const uint64_t* ksk, const or_ms_key* ms,
+               const uint64_t* lwe_in, const uint64_t* lut, uint64_t* lwe_out) {
   const size_t row = (size_t)(p->k + 1) * p->N;
   uint64_t* acc = (uint64_t*)malloc(row * 8);
   uint64_t* big = (uint64_t*)malloc(((size_t)p->k * p->N + 1) * 8);
@@ -546,6 +618,7 @@ void or_pbs(const or_params* p, const uint64_t* bsk_ntt, const uint64_t* ksk, co
   } else {
     uint64_t* small = (uint64_t*)malloc(((size_t)p->n + 1) * 8);
     or_keyswitch(p, ksk, lwe_in, small);
+    or_ms_reduce(p, ms, small);
     or_blind_rotate(p, bsk_ntt, 0, small, lut, acc);
     or_sample_extract(p, acc, lwe_out);
     free(small);
@@ -556,6 +629,12 @@ void or_pbs(const or_params* p, const uint64_t* bsk_ntt, const uint64_t* ksk, co
 void or_pbs_batch(const or_params* p, const uint64_t* bsk_ntt, const uint64_t* ksk, const uint64_t* lwe_in,
                   size_t B, const uint64_t* luts, size_t n_lut, const uint32_t* lut_index, uint64_t* lwe_out,
                   int threads) {
+  or_pbs_batch_ex(p, bsk_ntt, ksk, NULL, lwe_in, B, luts, n_lut, lut_index, lwe_out, threads);
+}
+
+void or_pbs_batch_ex(const or_params* p, const uint64_t* bsk_ntt, const uint64_t* ksk, const or_ms_key* ms,
+                     const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
+                     const uint32_t* lut_index, uint64_t* lwe_out, int threads) {
   const size_t din = (p->order == 0 ? p->n : p->k * p->N) + 1;
   const size_t dout = (p->order == 0 ? p->n : p->k * p->N) + 1;
 #ifdef _OPENMP
@@ -565,7 +644,7 @@ void or_pbs_batch(const or_params* p, const uint64_t* bsk_ntt, const uint64_t* k
   for (size_t q = 0; q < B; q++) {
     size_t li = lut_index ? lut_index[q] : 0;
     if (li >= n_lut) li = 0;
-    or_pbs(p, bsk_ntt, ksk, lwe_in + q * din, luts + li * p->N, lwe_out + q * dout);
+    or_pbs_ex(p, bsk_ntt, ksk, ms, lwe_in + q * din, luts + li * p->N, lwe_out + q * dout);
   }
   (void)threads;
 }

@@ -114,6 +114,45 @@ void or_pbs_batch(const or_params* p, const uint64_t* bsk_ntt, const uint64_t* k
                   size_t B, const uint64_t* luts, size_t n_lut, const uint32_t* lut_index,
                   uint64_t* lwe_out, int threads);
 
+/* ---- modulus-switch noise reduction (P-FHEVM) ------------------------
+ * The P-FHEVM server key carries `count` LWE encryptions of zero under the small key (1449 in the
+ * reference's parameter block, privateKey.bin @0x5e04, with ms_bound = 2^58, ms_r_sigma_factor =
+ * 13.179852282053789, ms_input_variance = 2.63039184094559e-07).  Before the
+ * blind rotation (after the keyswitch) the ciphertext may get ONE of them added, chosen to shrink
+ * the modulus-switch error (tfhe-rs 1.x `improve_lwe_ciphertext_modulus_switch_noise_for_binary_key`,
+ * absent from /root/reference; restated from its published description, parity unpinned):
+ *   err(x)   = (round(x * 2N / 2^64) * 2^64/2N) - x           (signed, |err| <= 2^(63-log2 2N))
+ *   measure  = |err(b) - sum_i err(a_i) / 2| + r * sqrt(sum_i err(a_i)^2 / 4 + var * 2^128)
+ *              (mean and r-sigma of the switched phase error for a uniform binary key)
+ *   if measure(ct) <= bound: unchanged; else add the zero with the lowest index whose measure is
+ *   <= bound, or failing that the lowest-index minimiser if it beats measure(ct).
+ * Sums are exact integers (i64 / u128); the double evaluation order above is fixed so the GPU
+ * kernel reproduces every comparison bit-for-bit. */
+#define OR_MS_FHEVM_ZEROS 1449u
+#define OR_MS_FHEVM_BOUND 0x1p58
+#define OR_MS_FHEVM_R_SIGMA 13.179852282053789
+#define OR_MS_FHEVM_INPUT_VARIANCE 2.63039184094559e-07
+
+typedef struct or_ms_key {
+  const uint64_t* zeros; /* count x (n+1) */
+  uint32_t count;
+  double bound, r_sigma, input_variance;
+} or_ms_key;
+
+/* encryptions of zero under the small key: zero z uses ChaCha stream 0x200000 + z of `seed` */
+void or_ms_zeros_keygen(const or_params* p, uint64_t seed, const uint64_t* lwe_key, uint32_t count,
+                        uint64_t* zeros /* count x (n+1) */);
+/* measure of ct (+ zero when zero != NULL); dim = p->n */
+double or_ms_measure(const or_params* p, const or_ms_key* ms, const uint64_t* ct, const uint64_t* zero);
+/* returns the chosen zero index or -1 and applies it to ct in place */
+int or_ms_reduce(const or_params* p, const or_ms_key* ms, uint64_t* ct /* n+1 */);
+/* or_pbs / or_pbs_batch with the reduction between keyswitch and blind rotation (order 1; ms nullable) */
+void or_pbs_ex(const or_params* p, const uint64_t* bsk_ntt, const uint64_t* ksk, const or_ms_key* ms,
+               const uint64_t* lwe_in, const uint64_t* lut, uint64_t* lwe_out);
+void or_pbs_batch_ex(const or_params* p, const uint64_t* bsk_ntt, const uint64_t* ksk, const or_ms_key* ms,
+                     const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
+                     const uint32_t* lut_index, uint64_t* lwe_out, int threads);
+
 /* ---- LUT helpers --------------------------------------------------------------------- */
 void or_lut_constant(uint32_t N, uint64_t torus_value, uint64_t* lut); /* gate LUT: every coef = v */
 /* tfhe-rs generate_accumulator: box = N/msg_modulus, v[i] = f(i/box)*delta_out, half-box rotation.

@@ -121,3 +121,49 @@ def test_latency_and_batch_kernels_agree_2048(fengine, fkeys, oracle_mod, fprm, 
     i = B // 2
     assert np.array_equal(acc_l[i], oracle_mod.blind_rotate(fprm, fkeys_oracle, small[i], lut))
     assert np.array_equal(ck.decrypt(out_l, MM), (7 * msgs + 2) % MM)
+
+
+@pytest.mark.parametrize("B", [1, 9, 300])
+def test_ms_noise_reduction_vs_oracle(fengine, fkeys, oracle_mod, fprm, fkeys_oracle, B):
+    """Modulus-switch noise reduction kernel (ms_reduce.hip) == oracle: same zero chosen, same
+    ciphertext, on real keyswitch outputs (early exit after 1-2 tiles of zeros) and on uniformly
+    random ciphertexts (no zero reaches the bound: full scan of all 1449 + argmin)."""
+    ck, _ = fkeys
+    rng = np.random.default_rng(B + 31)
+    msgs = rng.integers(0, MM, B).astype(np.uint64)
+    small = fengine.keyswitch(ck.encrypt(msgs, MM, seed=0xC0FFEE50 + B))
+    small[: max(1, B // 10)] = rng.integers(0, 2 ** 64 - 1, size=(max(1, B // 10), 919), dtype=np.uint64)
+    out, picks = fengine.ms_reduce(small)
+    ref, rpicks = oracle_mod.ms_reduce(fprm, fkeys_oracle, small)
+    assert np.array_equal(picks, rpicks)
+    assert np.array_equal(out, ref)
+    if B >= 9:
+        assert (picks >= 0).mean() > 0.5
+
+
+def test_ms_noise_reduction_in_pbs(fengine, fkeys, oracle_mod, fprm, fkeys_oracle):
+    """The full P-FHEVM PBS applies the reduction (KS -> MS -> BR): bit-exact with the oracle with it,
+    different from the oracle without it, and decrypting correctly either way."""
+    ck, _ = fkeys
+    B = 40
+    msgs = (np.arange(B) % MM).astype(np.uint64)
+    cts = ck.encrypt(msgs, MM, seed=0xC0FFEE60)
+    lut = oracle_mod.lut_from_table(2048, MM, [(5 * m + 3) % MM for m in range(MM)], DELTA)
+    out = fengine.pbs(cts, lut)
+    assert np.array_equal(out, oracle_mod.pbs_batch(fprm, fkeys_oracle, cts, lut))
+    plain = oracle_mod.pbs_batch(fprm, fkeys_oracle, cts, lut, ms=False)
+    assert not np.array_equal(out, plain)
+    want = (5 * msgs + 3) % MM
+    assert np.array_equal(ck.decrypt(out, MM), want) and np.array_equal(ck.decrypt(plain, MM), want)
+    try:
+        fengine.load_ms_key(None)                     # disabled: the plain path
+        assert np.array_equal(fengine.pbs(cts, lut), plain)
+    finally:
+        fengine.load_ms_key(fkeys[1].ms_zeros)
+
+
+def test_ms_key_refused_for_pbs_ks_order(engine):
+    import tfhe_amd
+    z = np.zeros((4, 631), dtype=np.uint64)
+    with pytest.raises(tfhe_amd.TfheError, match="EUNSUPPORTED"):
+        engine.load_ms_key(z)

@@ -56,6 +56,9 @@ def test_keygen_and_encrypt_match_oracle_fhevm(oracle_mod):
     ck, sk = tfhe_amd.gen_keys(tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM), KEY_SEED)
     assert np.array_equal(ck.lwe_key, ok.lwe_key) and np.array_equal(ck.glwe_key, ok.glwe_key)
     assert np.array_equal(sk.bsk, ok.bsk) and np.array_equal(sk.ksk, ok.ksk)
+    assert sk.ms_zeros.shape == (1449, 919) and np.array_equal(sk.ms_zeros, ok.ms_zeros)
+    zph = ok.phase(sk.ms_zeros, ok.lwe_key, prm.n).view(np.int64)
+    assert np.abs(zph).max() < 2 ** 50                       # encryptions of zero under the small key
     msgs = (np.arange(16, dtype=np.uint64) * np.uint64((1 << 63) // 16))
     a = ck.encrypt_torus(msgs, seed=0xC0FFEE03)
     assert a.shape == (16, 2049)
@@ -126,3 +129,35 @@ def test_gl64_primitives_exact(tmp_path):
                    check=True, capture_output=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout
+
+
+def test_ms_noise_reduction_rule_oracle(oracle_mod):
+    """The oracle's modulus-switch noise reduction follows its stated rule (tfhe_oracle.h or_ms_key):
+    brute-force every zero's measure and replay the sequential choice; the phase moves only by the
+    zero's noise; the measure never grows."""
+    prm = oracle_mod.params(1)
+    ok = oracle_mod.Keys(prm, KEY_SEED, with_bsk=False)
+    bound = oracle_mod.MS_FHEVM["bound"]
+    msgs = (np.arange(24, dtype=np.uint64) % 16) * np.uint64((1 << 63) // 16)
+    big = ok.encrypt(msgs, seed=0xC0FFEE31)
+    small = np.stack([oracle_mod.keyswitch(prm, ok, c) for c in big])
+    rng = np.random.default_rng(3)
+    small[-2:] = rng.integers(0, 2 ** 64 - 1, size=(2, prm.n + 1), dtype=np.uint64)   # no zero reaches the bound
+    red, picks = oracle_mod.ms_reduce(prm, ok, small)
+    for q in range(small.shape[0]):
+        best = oracle_mod.ms_measure(prm, ok, small[q])
+        want = -1
+        if best > bound:
+            for z in range(ok.ms_zeros.shape[0]):
+                m = oracle_mod.ms_measure(prm, ok, small[q], z)
+                if m < best:
+                    best, want = m, z
+                    if best <= bound:
+                        break
+        assert picks[q] == want, q
+        assert oracle_mod.ms_measure(prm, ok, red[q]) == best
+        if want >= 0:
+            assert np.array_equal(red[q], small[q] + ok.ms_zeros[want])
+    assert (picks[:-2] >= 0).mean() > 0.5 and (picks[-2:] >= 0).all()
+    d = (ok.phase(red[:-2], ok.lwe_key, prm.n) - ok.phase(small[:-2], ok.lwe_key, prm.n)).view(np.int64)
+    assert np.abs(d).max() < 2 ** 50

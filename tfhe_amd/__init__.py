@@ -81,8 +81,12 @@ ABI_SYMBOLS = (
     "tfhe_hip_load_keys_device", "tfhe_hip_pbs", "tfhe_hip_pbs_async", "tfhe_hip_blind_rotate",
     "tfhe_hip_sample_extract", "tfhe_hip_keyswitch", "tfhe_hip_ntt_fwd", "tfhe_hip_ntt_inv", "tfhe_hip_nand",
     "tfhe_hip_sync", "tfhe_hip_timing_enable", "tfhe_hip_timing_reset", "tfhe_hip_timing_stats",
-    "tfhe_hip_server_keygen", "tfhe_hip_set_latency_batch",
+    "tfhe_hip_server_keygen", "tfhe_hip_set_latency_batch", "tfhe_hip_ms_zeros_keygen", "tfhe_hip_load_ms_key",
+    "tfhe_hip_ms_reduce",
 )
+
+# P-FHEVM modulus-switch noise reduction key (include/tfhe_hip.h TFHE_HIP_MS_FHEVM_*)
+MS_FHEVM = dict(count=1449, bound=2.0 ** 58, r_sigma=13.179852282053789, input_variance=2.63039184094559e-07)
 
 
 def _share_hip_runtime_with_torch() -> None:
@@ -113,6 +117,11 @@ def lib():
         L.tfhe_hip_destroy.restype = None
         L.tfhe_hip_keygen.argtypes = [ctypes.c_void_p, ctypes.c_uint64, _U64P, _U64P, _U64P, _U64P]
         L.tfhe_hip_server_keygen.argtypes = [ctypes.c_void_p, ctypes.c_uint64, _U64P, _U64P, _U64P, _U64P]
+        L.tfhe_hip_ms_zeros_keygen.argtypes = [ctypes.c_void_p, ctypes.c_uint64, _U64P, ctypes.c_uint32, _U64P]
+        L.tfhe_hip_load_ms_key.argtypes = [ctypes.c_void_p, _U64P, ctypes.c_uint32, ctypes.c_double, ctypes.c_double,
+                                           ctypes.c_double]
+        L.tfhe_hip_ms_reduce.argtypes = [ctypes.c_void_p, _U64P, ctypes.c_size_t, _U64P,
+                                         ctypes.POINTER(ctypes.c_int32)]
         L.tfhe_hip_lwe_encrypt.argtypes = [ctypes.c_uint32, _U64P, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint64,
                                            _U64P, ctypes.c_size_t, _U64P]
         L.tfhe_hip_lwe_phase.argtypes = [ctypes.c_uint32, _U64P, _U64P, ctypes.c_size_t, _U64P]
@@ -218,10 +227,19 @@ class ClientKey:
 
 
 class ServerKey:
-    """Public evaluation keys in the standard domain: BSK over Z_p and KSK over Z_2^64."""
+    """Public evaluation keys in the standard domain: BSK over Z_p and KSK over Z_2^64; for KS -> PBS
+    parameter sets (P-FHEVM) also the modulus-switch noise-reduction zeros (count x (n+1))."""
 
-    def __init__(self, params: Params, bsk: np.ndarray, ksk: np.ndarray):
-        self.params, self.bsk, self.ksk = params, bsk, ksk
+    def __init__(self, params: Params, bsk: np.ndarray, ksk: np.ndarray, ms_zeros: Optional[np.ndarray] = None):
+        self.params, self.bsk, self.ksk, self.ms_zeros = params, bsk, ksk, ms_zeros
+
+
+def ms_zeros_keygen(params: Params, seed: int, lwe_key: np.ndarray, count: int = MS_FHEVM["count"]) -> np.ndarray:
+    """Encryptions of zero under the small key for the modulus-switch noise reduction."""
+    z = np.zeros((count, params.n + 1), dtype=np.uint64)
+    lwe = _c_u64(lwe_key)
+    _check(lib().tfhe_hip_ms_zeros_keygen(ctypes.byref(params), seed, _u64(lwe), count, _u64(z)))
+    return z
 
 
 def gen_keys(params: Optional[Params] = None, seed: int = 0x7F4E0001, with_server_key: bool = True):
@@ -237,7 +255,10 @@ def gen_keys(params: Optional[Params] = None, seed: int = 0x7F4E0001, with_serve
     _check(L.tfhe_hip_keygen(ctypes.byref(params), seed, _u64(lwe), _u64(glwe),
                              _u64(bsk) if bsk is not None else None, _u64(ksk) if ksk is not None else None))
     ck = ClientKey(params, seed, lwe, glwe)
-    return ck, (ServerKey(params, bsk, ksk) if with_server_key else None)
+    if not with_server_key:
+        return ck, None
+    zeros = ms_zeros_keygen(params, seed, lwe) if params.order == 1 else None
+    return ck, ServerKey(params, bsk, ksk, zeros)
 
 
 def server_keygen(ck: "ClientKey", seed: int = 0x7F4E0001) -> ServerKey:
@@ -248,7 +269,7 @@ def server_keygen(ck: "ClientKey", seed: int = 0x7F4E0001) -> ServerKey:
     ksk = np.zeros(L.tfhe_hip_ksk_len(ctypes.byref(p)), dtype=np.uint64)
     lwe, glwe = _c_u64(ck.lwe_key), _c_u64(ck.glwe_key)
     _check(L.tfhe_hip_server_keygen(ctypes.byref(p), seed, _u64(lwe), _u64(glwe), _u64(bsk), _u64(ksk)))
-    return ServerKey(p, bsk, ksk)
+    return ServerKey(p, bsk, ksk, ms_zeros_keygen(p, seed, lwe) if p.order == 1 else None)
 
 
 def lut_constant(N: int, torus_value: int) -> np.ndarray:
@@ -296,7 +317,28 @@ class Engine:
     def load_keys(self, sk: ServerKey) -> "Engine":
         bsk, ksk = _c_u64(sk.bsk), _c_u64(sk.ksk)
         _check(lib().tfhe_hip_load_keys(self._h, _u64(bsk), bsk.size, _u64(ksk), ksk.size))
+        if getattr(sk, "ms_zeros", None) is not None:
+            self.load_ms_key(sk.ms_zeros)
         return self
+
+    def load_ms_key(self, zeros: Optional[np.ndarray], bound: float = MS_FHEVM["bound"],
+                    r_sigma: float = MS_FHEVM["r_sigma"], input_variance: float = MS_FHEVM["input_variance"]):
+        """Modulus-switch noise reduction between keyswitch and blind rotation (None: disable)."""
+        if zeros is None:
+            _check(lib().tfhe_hip_load_ms_key(self._h, None, 0, 0.0, 0.0, 0.0))
+            return self
+        z = _c_u64(zeros).reshape(-1, self.params.n + 1)
+        _check(lib().tfhe_hip_load_ms_key(self._h, _u64(z), z.shape[0], bound, r_sigma, input_variance))
+        return self
+
+    def ms_reduce(self, small: np.ndarray):
+        """Stage-level noise reduction on small-key ciphertexts -> (ciphertexts, chosen zero index or -1)."""
+        x = _c_u64(small).reshape(-1, self.params.n + 1)
+        out = np.zeros_like(x)
+        picks = np.zeros(x.shape[0], dtype=np.int32)
+        _check(lib().tfhe_hip_ms_reduce(self._h, _u64(x), x.shape[0], _u64(out),
+                                        picks.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return out, picks
 
     def load_keys_device(self, d_bsk, d_ksk) -> "Engine":
         """Keys already in HBM on this device (torch tensors of dtype int64/uint64, e.g. after an

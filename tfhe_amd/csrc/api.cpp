@@ -82,6 +82,10 @@ struct tfhe_ctx {
   u64 ninv = 0;
   bool keys = false;
   size_t lat_max = 1024;  // batches up to this size use the latency blind-rotate kernel
+  // modulus-switch noise reduction (order 1): zeros resident in HBM
+  u64* d_ms_zeros = nullptr;
+  uint32_t ms_count = 0;
+  double ms_bound = 0, ms_r_sigma = 0, ms_var128 = 0;
   // workspaces
   u64* d_big = nullptr;
   size_t big_cap = 0;  // u64 elements
@@ -90,7 +94,7 @@ struct tfhe_ctx {
   std::mutex mu;
   // timing
   bool timing = false;
-  std::vector<hipEvent_t> ev[2];  // start/stop pairs, flattened
+  std::vector<hipEvent_t> ev[3];  // start/stop pairs, flattened
   std::vector<hipEvent_t> ev_pool;
 };
 
@@ -161,13 +165,25 @@ hipError_t launch_br(tfhe_ctx* c, const u64* in, size_t B, const u64* luts, cons
                                    c->lat_max);
 }
 
+uint32_t log2u(uint32_t x) {
+  uint32_t l = 0;
+  while ((1u << l) < x) l++;
+  return l;
+}
+
+hipError_t launch_ms(tfhe_ctx* c, u64* small, size_t B, int* picks, hipStream_t s) {
+  return tfhe::launch_ms_reduce(small, B, (int)c->p.n, c->d_ms_zeros, (int)c->ms_count, (int)log2u(2 * c->p.N),
+                                c->ms_bound, c->ms_r_sigma, c->ms_var128, picks, s);
+}
+
 hipError_t launch_ks(tfhe_ctx* c, const u64* in_big, size_t B, u64* out, hipStream_t s) {
   return tfhe::launch_keyswitch(in_big, B, (int)(c->p.k * c->p.N), c->d_ksk, (int)c->p.n, (int)c->p.ks_base_log,
                                 (int)c->p.ks_level, out, s);
 }
 
 // PBS on device buffers (caller holds c->mu, device set).  Order 0 (P-GATE): BR + SE -> KS;
-// order 1 (P-FHEVM): KS -> BR + SE.  Timing slot 0 = blind rotate, 1 = keyswitch.
+// order 1 (P-FHEVM): KS -> [MS noise reduction] -> BR + SE.  Timing slots 0 = blind rotate,
+// 1 = keyswitch, 2 = modulus-switch noise reduction.
 int pbs_device(tfhe_ctx* c, const u64* d_in, size_t B, const u64* d_luts, size_t n_lut, const u32* d_idx, u64* d_out,
                hipStream_t s) {
   const size_t big = (size_t)c->p.k * c->p.N + 1, small = (size_t)c->p.n + 1;
@@ -184,6 +200,11 @@ int pbs_device(tfhe_ctx* c, const u64* d_in, size_t B, const u64* d_luts, size_t
     timed_begin(c, 1, s);
     HIP_TRY(launch_ks(c, d_in, B, c->d_big, s));
     timed_end(c, 1, s);
+    if (c->ms_count) {
+      timed_begin(c, 2, s);
+      HIP_TRY(launch_ms(c, c->d_big, B, nullptr, s));
+      timed_end(c, 2, s);
+    }
     timed_begin(c, 0, s);
     HIP_TRY(launch_br(c, c->d_big, B, d_luts, d_idx, n_lut, d_out, nullptr, s));
     timed_end(c, 0, s);
@@ -254,6 +275,13 @@ int tfhe_hip_server_keygen(const tfhe_params* p, uint64_t seed, const uint64_t* 
   for (uint32_t i = 0; i < p->k * p->N; i++)
     if (glwe_key[i] > 1) return fail(TFHE_HIP_EINVAL, "server_keygen: glwe_key[%u] is not binary", i);
   tfhe::client::server_keygen(*p, seed, lwe_key, glwe_key, bsk, ksk);
+  return 0;
+}
+
+int tfhe_hip_ms_zeros_keygen(const tfhe_params* p, uint64_t seed, const uint64_t* lwe_key, uint32_t count,
+                             uint64_t* zeros) {
+  if (!params_valid(p) || !lwe_key || (count && !zeros)) return fail(TFHE_HIP_EINVAL, "ms_zeros_keygen: bad arguments");
+  tfhe::client::ms_zeros_keygen(*p, seed, lwe_key, count, zeros);
   return 0;
 }
 
@@ -329,12 +357,13 @@ void tfhe_hip_destroy(tfhe_ctx* c) {
   {
     DeviceGuard g(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (int w = 0; w < 2; w++)
+    for (int w = 0; w < 3; w++)
       for (auto e : c->ev[w]) (void)hipEventDestroy(e);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     (void)hipFree(c->d_bsk);
     (void)hipFree(c->d_ksk);
     (void)hipFree(c->d_tw);
+    (void)hipFree(c->d_ms_zeros);
     (void)hipFree(c->d_big);
     (void)hipFree(c->d_stage);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -383,6 +412,49 @@ int tfhe_hip_load_keys(tfhe_ctx* c, const uint64_t* bsk, size_t bsk_len, const u
 int tfhe_hip_load_keys_device(tfhe_ctx* c, const uint64_t* d_bsk, size_t bsk_len, const uint64_t* d_ksk,
                               size_t ksk_len) {
   return load_keys_impl(c, d_bsk, bsk_len, d_ksk, ksk_len, hipMemcpyDeviceToDevice);
+}
+
+int tfhe_hip_load_ms_key(tfhe_ctx* c, const uint64_t* zeros, uint32_t count, double bound, double r_sigma,
+                         double input_variance) {
+  if (!c || (count && !zeros)) return fail(TFHE_HIP_EINVAL, "load_ms_key: bad arguments");
+  if (c->p.order != 1 && count)
+    return fail(TFHE_HIP_EUNSUPPORTED, "load_ms_key: the noise reduction runs between keyswitch and blind rotation "
+                                       "(KS -> PBS parameter sets only)");
+  if (count > 0x7FFFFFFF || !(bound >= 0) || !(r_sigma >= 0) || !(input_variance >= 0))
+    return fail(TFHE_HIP_EINVAL, "load_ms_key: count %u / bound / r_sigma / variance out of range", count);
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  (void)hipFree(c->d_ms_zeros);
+  c->d_ms_zeros = nullptr;
+  c->ms_count = 0;
+  if (!count) return 0;
+  const size_t bytes = (size_t)count * (c->p.n + 1) * 8;
+  HIP_TRY(hipMalloc(&c->d_ms_zeros, bytes));
+  HIP_TRY(hipMemcpy(c->d_ms_zeros, zeros, bytes, hipMemcpyHostToDevice));
+  c->ms_count = count;
+  c->ms_bound = bound;
+  c->ms_r_sigma = r_sigma;
+  c->ms_var128 = input_variance * 0x1p128;
+  return 0;
+}
+
+int tfhe_hip_ms_reduce(tfhe_ctx* c, const uint64_t* in, size_t B, uint64_t* out, int32_t* picks) {
+  if (!c || (B && (!in || !out))) return fail(TFHE_HIP_EINVAL, "ms_reduce: bad arguments");
+  if (c->p.order != 1) return fail(TFHE_HIP_EUNSUPPORTED, "ms_reduce: KS -> PBS parameter sets only");
+  if (B == 0) return 0;
+  if (B > 0x7FFFFFFF) return fail(TFHE_HIP_EINVAL, "ms_reduce: batch too large");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  const size_t small = (size_t)c->p.n + 1;
+  std::vector<void*> d;
+  int rc = stage(c, {{in, B * small * 8}}, d, B * 4);
+  if (rc) return rc;
+  HIP_TRY(launch_ms(c, (u64*)d[0], B, (int*)d[1], c->stream));
+  HIP_TRY(hipMemcpyAsync(out, d[0], B * small * 8, hipMemcpyDeviceToHost, c->stream));
+  if (picks) HIP_TRY(hipMemcpyAsync(picks, d[1], B * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
 }
 
 int tfhe_hip_pbs_async(tfhe_ctx* c, const uint64_t* d_in, size_t B, const uint64_t* d_luts, size_t n_lut,
@@ -535,7 +607,7 @@ int tfhe_hip_timing_enable(tfhe_ctx* c, int enable) {
 int tfhe_hip_timing_reset(tfhe_ctx* c) {
   if (!c) return fail(TFHE_HIP_EINVAL, "timing: null ctx");
   std::lock_guard<std::mutex> lk(c->mu);
-  for (int w = 0; w < 2; w++) {
+  for (int w = 0; w < 3; w++) {
     for (auto e : c->ev[w]) c->ev_pool.push_back(e);
     c->ev[w].clear();
   }
@@ -543,7 +615,7 @@ int tfhe_hip_timing_reset(tfhe_ctx* c) {
 }
 
 int tfhe_hip_timing_stats(tfhe_ctx* c, int which, double* total_ms, int* launches) {
-  if (!c || which < 0 || which > 1 || !total_ms || !launches) return fail(TFHE_HIP_EINVAL, "timing: bad arguments");
+  if (!c || which < 0 || which > 2 || !total_ms || !launches) return fail(TFHE_HIP_EINVAL, "timing: bad arguments");
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   double tot = 0;

@@ -207,6 +207,14 @@ void server_keygen(const tfhe_params& p, uint64_t seed, const uint64_t* lwe_key,
   }
 }
 
+// modulus-switch zeros of the P-FHEVM server key: zero z on ChaCha stream 0x200000 + z
+void ms_zeros_keygen(const tfhe_params& p, uint64_t seed, const uint64_t* lwe_key, uint32_t count, uint64_t* zeros) {
+  parallel_for((int64_t)count, [&](int64_t z) {
+    ChaCha r(seed, 0x200000 + (uint64_t)z);
+    lwe_one(p.n, lwe_key, p.lwe_noise_log2, r, 0, zeros + (size_t)z * (p.n + 1));
+  });
+}
+
 void lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, uint64_t seed, uint64_t stream0,
                  const uint64_t* msgs, size_t count, uint64_t* out) {
   auto one = [&](int64_t q) {

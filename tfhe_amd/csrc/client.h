@@ -13,6 +13,8 @@ void keygen(const tfhe_params& p, uint64_t seed, uint64_t* lwe_key, uint64_t* gl
 // BSK / KSK for given binary secret keys (e.g. an ingested tfhe-rs ClientKey); same streams as keygen
 void server_keygen(const tfhe_params& p, uint64_t seed, const uint64_t* lwe_key, const uint64_t* glwe_key,
                    uint64_t* bsk, uint64_t* ksk);
+// P-FHEVM modulus-switch zeros: count LWE encryptions of 0 under the small key, count x (n+1)
+void ms_zeros_keygen(const tfhe_params& p, uint64_t seed, const uint64_t* lwe_key, uint32_t count, uint64_t* zeros);
 void lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, uint64_t seed, uint64_t stream0,
                  const uint64_t* msgs, size_t count, uint64_t* out);
 void lwe_phase(uint32_t dim, const uint64_t* key, const uint64_t* ct, size_t count, uint64_t* out);

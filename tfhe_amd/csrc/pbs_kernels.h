@@ -31,5 +31,8 @@ hipError_t launch_blind_rotate_2048(const u64* lwe_in, size_t B, int n, const u6
                                    hipStream_t s, size_t latency_max_batch = 0);
 hipError_t launch_sample_extract_2048(const u64* acc, size_t B, u64* out, hipStream_t s);
 hipError_t launch_ntt2048_fwd(u64* polys, size_t count, const u64* tw, hipStream_t s);
+// modulus-switch noise reduction (ms_reduce.hip), in place on B x (n+1); picks (device, nullable)
+hipError_t launch_ms_reduce(u64* lwe, size_t B, int n, const u64* zeros, int count, int log2_2N, double bound,
+                            double r_sigma, double var128, int* picks, hipStream_t s);
 hipError_t launch_ntt2048_inv(u64* polys, size_t count, const u64* tw, u64 ninv, hipStream_t s);
 }  // namespace tfhe
