@@ -164,6 +164,41 @@ int tfhe_hip_timing_enable(tfhe_ctx* ctx, int enable);
 int tfhe_hip_timing_reset(tfhe_ctx* ctx);
 int tfhe_hip_timing_stats(tfhe_ctx* ctx, int which, double* total_ms, int* launches);
 
+/* ---- LWE -> GLWE packing keyswitch and ciphertext compression ---------------
+ * Replaces the reference's compression of result ciphertexts (ml/extensions/rust/src/compression.rs:
+ * cpu_compress_ciphertexts_into_list :246-291 / cuda_compress_ciphertexts_into_single_glwe :190-240 ->
+ * tfhe-rs par_keyswitch_lwe_ciphertext_list_and_pack_in_glwe_ciphertext, then
+ * CompressedModulusSwitchedGlweCiphertext::compress; extract :134-156).  Up to lwe_per_glwe LWEs
+ * (dimension in_dim, native 2^64) are keyswitched into the coefficients 0, 1, ... of one GLWE
+ * (k = out_k, N = out_N) under a fresh binary GLWE key; compression switches every stored coefficient
+ * to storage_log bits and bit-packs them.  Exact rule: oracle/tfhe_oracle.h (or_pks_params). */
+typedef struct tfhe_pks_params {
+  uint32_t in_dim, out_k, out_N, base_log, level, lwe_per_glwe, storage_log;
+  int32_t noise_log2;
+} tfhe_pks_params;
+/* PARAMS_8B_2048_NEW (ml/extensions/rust/src/fhext_classes.rs:98-112): in 2048, pks 2 x 2^14,
+ * out k=1 N=2048, lwe_per_glwe 2048, storage 26 bits, noise 2^-48 */
+#define TFHE_HIP_PKS_PRESET_ML2048 0
+int tfhe_hip_pks_params_preset(int preset, tfhe_pks_params* out);
+size_t tfhe_hip_pksk_len(const tfhe_pks_params* pp); /* in_dim * level * (out_k+1) * out_N u64 */
+/* output GLWE key (out_k*out_N bits, ChaCha stream 4) and PKSK [j][l][(k+1)N] (stream 0x300000+j) */
+int tfhe_hip_pks_keygen(const tfhe_pks_params* pp, uint64_t seed, const uint64_t* in_key, uint64_t* out_key,
+                        uint64_t* pksk /* nullable */);
+typedef struct tfhe_pks_ctx tfhe_pks_ctx;
+int tfhe_hip_pks_create(const tfhe_pks_params* pp, int device, tfhe_pks_ctx** out);
+void tfhe_hip_pks_destroy(tfhe_pks_ctx* ctx);
+int tfhe_hip_pks_load_key(tfhe_pks_ctx* ctx, const uint64_t* pksk, size_t len);
+/* count LWEs (count x (in_dim+1)) -> ceil(count / lwe_per_glwe) GLWEs ((k+1) x N each); GLWE g holds
+ * LWEs g*lwe_per_glwe ... in coefficients 0, 1, ...  Host buffers, synchronous. */
+int tfhe_hip_pks_pack(tfhe_pks_ctx* ctx, const uint64_t* lwes, size_t count, uint64_t* glwes);
+/* Device buffers, enqueued on `stream` (NULL = the ctx stream). */
+int tfhe_hip_pks_pack_async(tfhe_pks_ctx* ctx, const uint64_t* d_lwes, size_t count, uint64_t* d_glwes, void* stream);
+size_t tfhe_hip_pks_packed_words(const tfhe_pks_params* pp, uint32_t bodies);
+int tfhe_hip_pks_compress(const tfhe_pks_params* pp, const uint64_t* glwe, uint32_t bodies, uint64_t* packed);
+int tfhe_hip_pks_extract(const tfhe_pks_params* pp, const uint64_t* packed, uint32_t bodies, uint64_t* glwe);
+/* client-side decryption of a native GLWE: body - sum_c mask_c * S_c (N values) */
+int tfhe_hip_glwe_phase(uint32_t k, uint32_t N, const uint64_t* key, const uint64_t* glwe, uint64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

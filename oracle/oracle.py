@@ -301,3 +301,57 @@ def encode_bit(b: int) -> int:
 
 def decode_bit(phase: int) -> int:
     return 1 if phase < (1 << 63) else 0
+
+
+# ---- packing keyswitch + compression (tfhe_oracle.h: or_pks_params) ----------------------------
+class PksParams(ctypes.Structure):
+    _fields_ = [("in_dim", ctypes.c_uint32), ("out_k", ctypes.c_uint32), ("out_N", ctypes.c_uint32),
+                ("base_log", ctypes.c_uint32), ("level", ctypes.c_uint32), ("lwe_per_glwe", ctypes.c_uint32),
+                ("storage_log", ctypes.c_uint32), ("noise_log2", ctypes.c_int32)]
+
+
+def pks_params(preset: int = 0) -> PksParams:
+    p = PksParams()
+    assert lib().or_pks_params_preset(preset, ctypes.byref(p)) == 0
+    return p
+
+
+class PksKeys:
+    def __init__(self, pp: PksParams, seed: int, in_key: np.ndarray, with_pksk: bool = True):
+        L = lib()
+        L.or_pksk_len.restype = ctypes.c_size_t
+        self.pp, self.seed = pp, seed
+        self.in_key = np.ascontiguousarray(in_key, dtype=np.uint64)
+        self.out_key = np.zeros(pp.out_k * pp.out_N, dtype=np.uint64)
+        self.pksk = np.zeros(L.or_pksk_len(ctypes.byref(pp)), dtype=np.uint64) if with_pksk else None
+        L.or_pks_keygen(ctypes.byref(pp), ctypes.c_uint64(seed), _p(self.in_key), _p(self.out_key),
+                        _p(self.pksk) if with_pksk else None)
+
+
+def pks_pack(pp: PksParams, keys: PksKeys, lwes: np.ndarray) -> np.ndarray:
+    lwes = np.ascontiguousarray(lwes, dtype=np.uint64).reshape(-1, pp.in_dim + 1)
+    out = np.zeros((pp.out_k + 1) * pp.out_N, dtype=np.uint64)
+    lib().or_pks_pack(ctypes.byref(pp), _p(keys.pksk), _p(lwes), ctypes.c_uint32(lwes.shape[0]), _p(out))
+    return out
+
+
+def glwe_phase_native(k: int, N: int, key: np.ndarray, glwe: np.ndarray) -> np.ndarray:
+    out = np.zeros(N, dtype=np.uint64)
+    lib().or_glwe_phase_native(ctypes.c_uint32(k), ctypes.c_uint32(N), _p(np.ascontiguousarray(key, dtype=np.uint64)),
+                               _p(np.ascontiguousarray(glwe, dtype=np.uint64)), _p(out))
+    return out
+
+
+def pks_compress(pp: PksParams, glwe: np.ndarray, bodies: int) -> np.ndarray:
+    L = lib()
+    L.or_pks_packed_words.restype = ctypes.c_size_t
+    out = np.zeros(L.or_pks_packed_words(ctypes.byref(pp), ctypes.c_uint32(bodies)), dtype=np.uint64)
+    L.or_pks_compress(ctypes.byref(pp), _p(np.ascontiguousarray(glwe, dtype=np.uint64)), ctypes.c_uint32(bodies), _p(out))
+    return out
+
+
+def pks_extract(pp: PksParams, packed: np.ndarray, bodies: int) -> np.ndarray:
+    out = np.zeros((pp.out_k + 1) * pp.out_N, dtype=np.uint64)
+    lib().or_pks_extract(ctypes.byref(pp), _p(np.ascontiguousarray(packed, dtype=np.uint64)), ctypes.c_uint32(bodies),
+                         _p(out))
+    return out

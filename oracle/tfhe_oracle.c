@@ -678,3 +678,139 @@ void or_nand(const or_params* p, const uint64_t* bsk_ntt, const uint64_t* ksk, c
   or_pbs(p, bsk_ntt, ksk, c, lut, out);
   free(c); free(lut);
 }
+
+/* ======================================================================================
+ * Packing keyswitch + compression (header: or_pks_params).
+ * ==================================================================================== */
+int or_pks_params_preset(int preset, or_pks_params* o) {
+  if (preset != 0) return -1;
+  o->in_dim = 2048; o->out_k = 1; o->out_N = 2048; o->base_log = 14; o->level = 2;
+  o->lwe_per_glwe = 2048; o->storage_log = 26; o->noise_log2 = -48;
+  return 0;
+}
+
+size_t or_pksk_len(const or_pks_params* pp) {
+  return (size_t)pp->in_dim * pp->level * (pp->out_k + 1) * pp->out_N;
+}
+
+/* native (2^64) GLWE encryption of the plaintext polynomial m (N values, nullable = 0) */
+static void glwe_encrypt_native(uint32_t k, uint32_t N, const uint64_t* key, int32_t noise_log2, or_rng* r,
+                                const uint64_t* m, uint64_t* out) {
+  uint64_t* body = out + (size_t)k * N;
+  for (size_t i = 0; i < (size_t)k * N; i++) out[i] = or_rng_u64(r);
+  for (uint32_t i = 0; i < N; i++) body[i] = (uint64_t)or_rng_gauss(r, noise_log2) + (m ? m[i] : 0);
+  for (uint32_t c = 0; c < k; c++) {
+    const uint64_t* A = out + (size_t)c * N;
+    const uint64_t* S = key + (size_t)c * N;
+    for (uint32_t j = 0; j < N; j++) {
+      if (!S[j]) continue;
+      for (uint32_t i = 0; i < N; i++) {
+        const uint32_t d = i + j;
+        if (d < N) body[d] += A[i];
+        else body[d - N] -= A[i];
+      }
+    }
+  }
+}
+
+void or_pks_keygen(const or_pks_params* pp, uint64_t seed, const uint64_t* in_key, uint64_t* out_key,
+                   uint64_t* pksk) {
+  const uint32_t k = pp->out_k, N = pp->out_N;
+  or_rng r;
+  or_rng_init(&r, seed, 4);
+  for (uint32_t i = 0; i < k * N; i++) out_key[i] = or_rng_u64(&r) & 1;
+  if (!pksk) return;
+  const size_t row = (size_t)(k + 1) * N;
+#pragma omp parallel for schedule(dynamic, 8)
+  for (uint32_t j = 0; j < pp->in_dim; j++) {
+    or_rng rr;
+    or_rng_init(&rr, seed, 0x300000 + j);
+    uint64_t* m = (uint64_t*)calloc(N, 8);
+    for (uint32_t l = 0; l < pp->level; l++) {
+      m[0] = in_key[j] << (64 - pp->base_log * (l + 1));
+      glwe_encrypt_native(k, N, out_key, pp->noise_log2, &rr, m, pksk + ((size_t)j * pp->level + l) * row);
+    }
+    free(m);
+  }
+}
+
+void or_pks_pack(const or_pks_params* pp, const uint64_t* pksk, const uint64_t* lwes, uint32_t count,
+                 uint64_t* glwe) {
+  const uint32_t k = pp->out_k, N = pp->out_N, L = pp->level;
+  const size_t row = (size_t)(k + 1) * N;
+  uint64_t* buf = (uint64_t*)malloc(row * 8);
+  int64_t dig[64];
+  memset(glwe, 0, row * 8);
+  for (uint32_t d = 0; d < count; d++) {
+    const uint64_t* a = lwes + (size_t)d * (pp->in_dim + 1);
+    memset(buf, 0, row * 8);
+    buf[(size_t)k * N] = a[pp->in_dim];
+    for (uint32_t j = 0; j < pp->in_dim; j++) {
+      or_decompose(a[j], pp->base_log, L, dig);
+      for (uint32_t l = 0; l < L; l++) {
+        if (!dig[l]) continue;
+        const uint64_t* key = pksk + ((size_t)j * L + l) * row;
+        const uint64_t dv = (uint64_t)dig[l];
+        for (size_t t = 0; t < row; t++) buf[t] -= dv * key[t];
+      }
+    }
+    /* out += X^d * buf, each polynomial */
+    for (uint32_t c = 0; c <= k; c++) {
+      const uint64_t* src = buf + (size_t)c * N;
+      uint64_t* dst = glwe + (size_t)c * N;
+      for (uint32_t i = 0; i < N; i++) {
+        const uint32_t t = i + d;
+        if (t < N) dst[t] += src[i];
+        else dst[t - N] -= src[i];
+      }
+    }
+  }
+  free(buf);
+}
+
+void or_glwe_phase_native(uint32_t k, uint32_t N, const uint64_t* key, const uint64_t* glwe, uint64_t* out) {
+  memcpy(out, glwe + (size_t)k * N, (size_t)N * 8);
+  for (uint32_t c = 0; c < k; c++) {
+    const uint64_t* A = glwe + (size_t)c * N;
+    const uint64_t* S = key + (size_t)c * N;
+    for (uint32_t j = 0; j < N; j++) {
+      if (!S[j]) continue;
+      for (uint32_t i = 0; i < N; i++) {
+        const uint32_t d = i + j;
+        if (d < N) out[d] -= A[i];
+        else out[d - N] += A[i];
+      }
+    }
+  }
+}
+
+size_t or_pks_packed_words(const or_pks_params* pp, uint32_t bodies) {
+  const size_t vals = (size_t)pp->out_k * pp->out_N + bodies;
+  return (vals * pp->storage_log + 63) / 64;
+}
+
+void or_pks_compress(const or_pks_params* pp, const uint64_t* glwe, uint32_t bodies, uint64_t* packed) {
+  const uint32_t w = pp->storage_log;
+  const size_t vals = (size_t)pp->out_k * pp->out_N + bodies;
+  memset(packed, 0, or_pks_packed_words(pp, bodies) * 8);
+  for (size_t v = 0; v < vals; v++) {
+    const uint64_t x = glwe[v];     /* mask polys then the body, contiguous */
+    const uint64_t ms = (((x >> (64 - w - 1)) + 1) >> 1) & ((1ull << w) - 1);
+    const size_t bit = v * w, word = bit / 64, off = bit % 64;
+    packed[word] |= ms << off;
+    if (off + w > 64) packed[word + 1] |= ms >> (64 - off);
+  }
+}
+
+void or_pks_extract(const or_pks_params* pp, const uint64_t* packed, uint32_t bodies, uint64_t* glwe) {
+  const uint32_t w = pp->storage_log;
+  const size_t vals = (size_t)pp->out_k * pp->out_N + bodies;
+  memset(glwe, 0, (size_t)(pp->out_k + 1) * pp->out_N * 8);
+  for (size_t v = 0; v < vals; v++) {
+    const size_t bit = v * w, word = bit / 64, off = bit % 64;
+    uint64_t ms = packed[word] >> off;
+    if (off + w > 64) ms |= packed[word + 1] << (64 - off);
+    ms &= (1ull << w) - 1;
+    glwe[v] = ms << (64 - w);
+  }
+}

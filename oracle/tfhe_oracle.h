@@ -153,6 +153,39 @@ void or_pbs_batch_ex(const or_params* p, const uint64_t* bsk_ntt, const uint64_t
                      const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
                      const uint32_t* lut_index, uint64_t* lwe_out, int threads);
 
+/* ---- LWE -> GLWE packing keyswitch + modulus-switched compression --------------
+ * Restates the reference's ciphertext compression (ml/extensions/rust/src/compression.rs:246-291,
+ * cpu_compress_ciphertexts_into_list -> tfhe-rs par_keyswitch_lwe_ciphertext_list_and_pack_in_glwe_
+ * ciphertext, then CompressedModulusSwitchedGlweCiphertext::compress; extract :134-156):
+ *   for LWE d of a chunk of <= lwe_per_glwe:  buf = (0,..,0 | b_d at coefficient 0);
+ *     for each mask element a_j, digits d_l of closest_representable(a_j) (SignedDecomposer):
+ *       buf -= d_l * PKSK[j][l]      (PKSK[j][l] = GLWE_S'(s_j * 2^(64 - base_log*(l+1))), native q)
+ *     out += X^d * buf               (negacyclic monomial product per polynomial)
+ *   compress: every mask coefficient and the first `bodies` body coefficients switched to
+ *   storage_log bits (round(x / 2^(64-w))) and bit-packed LSB-first into u64 words; extract: unpack,
+ *   << (64 - w), missing body coefficients 0.
+ * Parameters: the reference's own PARAMS_8B_2048_NEW (ml/extensions/rust/src/fhext_classes.rs:98-112:
+ * input GLWE k=1,N=2048 read as an LWE of dim 2048, pks 2 x 2^14, output k=1,N=2048, storage 26 bits,
+ * pks noise stdev 2.845e-15 ~ 2^-48, lwe_per_glwe = N (fhext_classes.rs:130)).  PKSK layout
+ * [j][l][(k+1)N] u64; the output GLWE key is binary from ChaCha stream 4 of the seed, PKSK row j from
+ * stream 0x300000 + j.  Parity unpinned at ciphertext level (no fixture in the reference). */
+typedef struct or_pks_params {
+  uint32_t in_dim, out_k, out_N, base_log, level, lwe_per_glwe, storage_log;
+  int32_t noise_log2;
+} or_pks_params;
+int or_pks_params_preset(int preset, or_pks_params* out); /* 0 = PARAMS_8B_2048_NEW */
+size_t or_pksk_len(const or_pks_params* pp);              /* in_dim * level * (k+1) * N */
+void or_pks_keygen(const or_pks_params* pp, uint64_t seed, const uint64_t* in_key, uint64_t* out_key /* k*N */,
+                   uint64_t* pksk);
+/* count <= lwe_per_glwe LWEs (count x (in_dim+1)) -> one GLWE ((k+1) x N) */
+void or_pks_pack(const or_pks_params* pp, const uint64_t* pksk, const uint64_t* lwes, uint32_t count,
+                 uint64_t* glwe);
+/* phase polynomial body - sum_c mask_c * S_c over Z_2^64 (N values) */
+void or_glwe_phase_native(uint32_t k, uint32_t N, const uint64_t* key, const uint64_t* glwe, uint64_t* out);
+size_t or_pks_packed_words(const or_pks_params* pp, uint32_t bodies);
+void or_pks_compress(const or_pks_params* pp, const uint64_t* glwe, uint32_t bodies, uint64_t* packed);
+void or_pks_extract(const or_pks_params* pp, const uint64_t* packed, uint32_t bodies, uint64_t* glwe);
+
 /* ---- LUT helpers --------------------------------------------------------------------- */
 void or_lut_constant(uint32_t N, uint64_t torus_value, uint64_t* lut); /* gate LUT: every coef = v */
 /* tfhe-rs generate_accumulator: box = N/msg_modulus, v[i] = f(i/box)*delta_out, half-box rotation.

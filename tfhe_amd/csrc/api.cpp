@@ -238,6 +238,12 @@ int stage(tfhe_ctx* c, std::initializer_list<std::pair<const void*, size_t>> in,
 
 }  // namespace
 
+// error slot shared with pks_api.cpp
+int tfhe_hip_set_error(int code, const char* msg) {
+  g_err = msg;
+  return code;
+}
+
 extern "C" {
 
 const char* tfhe_hip_last_error(void) { return g_err.c_str(); }

@@ -255,5 +255,95 @@ void lut_from_table(uint32_t N, uint32_t msg_modulus, const uint64_t* table, uin
   }
 }
 
+// ------------------------------------------------------------ packing keyswitch key / compression
+size_t pksk_len(const tfhe_pks_params& pp) { return (size_t)pp.in_dim * pp.level * (pp.out_k + 1) * pp.out_N; }
+
+// native (2^64) GLWE encryption of the plaintext polynomial m (binary key: rotated-copy products)
+static void glwe_native(uint32_t k, uint32_t N, const uint64_t* key, int32_t noise_log2, ChaCha& r, const uint64_t* m,
+                        uint64_t* out) {
+  uint64_t* body = out + (size_t)k * N;
+  for (size_t i = 0; i < (size_t)k * N; i++) out[i] = r.next();
+  for (uint32_t i = 0; i < N; i++) body[i] = (uint64_t)r.gauss(noise_log2) + (m ? m[i] : 0);
+  for (uint32_t c = 0; c < k; c++) {
+    const uint64_t* A = out + (size_t)c * N;
+    const uint64_t* S = key + (size_t)c * N;
+    for (uint32_t j = 0; j < N; j++) {
+      if (!S[j]) continue;
+      for (uint32_t i = 0; i < N; i++) {
+        const uint32_t d = i + j;
+        if (d < N) body[d] += A[i];
+        else body[d - N] -= A[i];
+      }
+    }
+  }
+}
+
+// output GLWE key from ChaCha stream 4, PKSK row j from stream 0x300000 + j
+void pks_keygen(const tfhe_pks_params& pp, uint64_t seed, const uint64_t* in_key, uint64_t* out_key, uint64_t* pksk) {
+  const uint32_t k = pp.out_k, N = pp.out_N;
+  {
+    ChaCha r(seed, 4);
+    for (uint32_t i = 0; i < k * N; i++) out_key[i] = r.next() & 1;
+  }
+  if (!pksk) return;
+  const size_t row = (size_t)(k + 1) * N;
+  parallel_for((int64_t)pp.in_dim, [&](int64_t j) {
+    ChaCha r(seed, 0x300000 + (uint64_t)j);
+    std::vector<uint64_t> m(N, 0);
+    for (uint32_t l = 0; l < pp.level; l++) {
+      m[0] = in_key[j] << (64 - pp.base_log * (l + 1));
+      glwe_native(k, N, out_key, pp.noise_log2, r, m.data(), pksk + ((size_t)j * pp.level + l) * row);
+    }
+  });
+}
+
+void glwe_phase_native(uint32_t k, uint32_t N, const uint64_t* key, const uint64_t* glwe, uint64_t* out) {
+  memcpy(out, glwe + (size_t)k * N, (size_t)N * 8);
+  for (uint32_t c = 0; c < k; c++) {
+    const uint64_t* A = glwe + (size_t)c * N;
+    const uint64_t* S = key + (size_t)c * N;
+    for (uint32_t j = 0; j < N; j++) {
+      if (!S[j]) continue;
+      for (uint32_t i = 0; i < N; i++) {
+        const uint32_t d = i + j;
+        if (d < N) out[d] -= A[i];
+        else out[d - N] += A[i];
+      }
+    }
+  }
+}
+
+size_t pks_packed_words(const tfhe_pks_params& pp, uint32_t bodies) {
+  return (((size_t)pp.out_k * pp.out_N + bodies) * pp.storage_log + 63) / 64;
+}
+
+// modulus switch to storage_log bits, LSB-first bit packing (mask coefficients, then `bodies` body ones)
+void pks_compress(const tfhe_pks_params& pp, const uint64_t* glwe, uint32_t bodies, uint64_t* packed) {
+  const uint32_t w = pp.storage_log;
+  const size_t vals = (size_t)pp.out_k * pp.out_N + bodies;
+  const uint64_t mask = (w == 64) ? ~0ull : ((1ull << w) - 1);
+  memset(packed, 0, pks_packed_words(pp, bodies) * 8);
+  for (size_t v = 0; v < vals; v++) {
+    const uint64_t x = glwe[v];
+    const uint64_t ms = (((x >> (64 - w - 1)) + 1) >> 1) & mask;
+    const size_t bit = v * w, word = bit >> 6, off = bit & 63;
+    packed[word] |= ms << off;
+    if (off + w > 64) packed[word + 1] |= ms >> (64 - off);
+  }
+}
+
+void pks_extract(const tfhe_pks_params& pp, const uint64_t* packed, uint32_t bodies, uint64_t* glwe) {
+  const uint32_t w = pp.storage_log;
+  const size_t vals = (size_t)pp.out_k * pp.out_N + bodies;
+  const uint64_t mask = (w == 64) ? ~0ull : ((1ull << w) - 1);
+  memset(glwe, 0, (size_t)(pp.out_k + 1) * pp.out_N * 8);
+  for (size_t v = 0; v < vals; v++) {
+    const size_t bit = v * w, word = bit >> 6, off = bit & 63;
+    uint64_t ms = packed[word] >> off;
+    if (off + w > 64) ms |= packed[word + 1] << (64 - off);
+    glwe[v] = (ms & mask) << (64 - w);
+  }
+}
+
 }  // namespace client
 }  // namespace tfhe

@@ -20,5 +20,12 @@ void lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, uint64_t
 void lwe_phase(uint32_t dim, const uint64_t* key, const uint64_t* ct, size_t count, uint64_t* out);
 void lut_constant(uint32_t N, uint64_t torus_value, uint64_t* lut);
 void lut_from_table(uint32_t N, uint32_t msg_modulus, const uint64_t* table, uint64_t delta, uint64_t* lut);
+// packing keyswitch (LWE list -> GLWE) key and ciphertext compression
+size_t pksk_len(const tfhe_pks_params& pp);
+void pks_keygen(const tfhe_pks_params& pp, uint64_t seed, const uint64_t* in_key, uint64_t* out_key, uint64_t* pksk);
+void glwe_phase_native(uint32_t k, uint32_t N, const uint64_t* key, const uint64_t* glwe, uint64_t* out);
+size_t pks_packed_words(const tfhe_pks_params& pp, uint32_t bodies);
+void pks_compress(const tfhe_pks_params& pp, const uint64_t* glwe, uint32_t bodies, uint64_t* packed);
+void pks_extract(const tfhe_pks_params& pp, const uint64_t* packed, uint32_t bodies, uint64_t* glwe);
 }  // namespace client
 }  // namespace tfhe

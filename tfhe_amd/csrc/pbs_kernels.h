@@ -31,6 +31,10 @@ hipError_t launch_blind_rotate_2048(const u64* lwe_in, size_t B, int n, const u6
                                    hipStream_t s, size_t latency_max_batch = 0);
 hipError_t launch_sample_extract_2048(const u64* acc, size_t B, u64* out, hipStream_t s);
 hipError_t launch_ntt2048_fwd(u64* polys, size_t count, const u64* tw, hipStream_t s);
+// packing keyswitch (pks.hip)
+hipError_t launch_pks_corr(const u64* pksk, int K, int Nc, int base_log, u64* corr, hipStream_t s);
+hipError_t launch_pks_pack(const u64* lwes, size_t count, int in_dim, int base_log, int L, int k, int N, int lpg,
+                           const u64* pksk, const u64* corr, u32* A, u64* T, u64* out, hipStream_t s);
 // modulus-switch noise reduction (ms_reduce.hip), in place on B x (n+1); picks (device, nullable)
 hipError_t launch_ms_reduce(u64* lwe, size_t B, int n, const u64* zeros, int count, int log2_2N, double bound,
                             double r_sigma, double var128, int* picks, hipStream_t s);
