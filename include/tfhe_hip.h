@@ -126,7 +126,9 @@ int tfhe_hip_ms_reduce(tfhe_ctx* ctx, const uint64_t* lwe_small, size_t B, uint6
  * the compute behind POST /evaluate (e2e/test/fhe.test.ts:141-157).  Host buffers, synchronous. */
 int tfhe_hip_pbs(tfhe_ctx* ctx, const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
                  const uint32_t* lut_index, uint64_t* lwe_out);
-/* Device buffers, enqueued on `stream` (hipStream_t; NULL = the ctx stream).  Inputs resident in HBM. */
+/* Device buffers, enqueued on `stream` (hipStream_t; NULL = the ctx stream, TFHE_HIP_NULL_STREAM = the
+ * device's legacy null stream, e.g. torch's default stream).  Inputs resident in HBM. */
+#define TFHE_HIP_NULL_STREAM ((void*)(intptr_t)-1)
 int tfhe_hip_pbs_async(tfhe_ctx* ctx, const uint64_t* d_lwe_in, size_t B, const uint64_t* d_luts, size_t n_lut,
                        const uint32_t* d_lut_index, uint64_t* d_lwe_out, void* stream);
 
@@ -191,7 +193,7 @@ int tfhe_hip_pks_load_key(tfhe_pks_ctx* ctx, const uint64_t* pksk, size_t len);
 /* count LWEs (count x (in_dim+1)) -> ceil(count / lwe_per_glwe) GLWEs ((k+1) x N each); GLWE g holds
  * LWEs g*lwe_per_glwe ... in coefficients 0, 1, ...  Host buffers, synchronous. */
 int tfhe_hip_pks_pack(tfhe_pks_ctx* ctx, const uint64_t* lwes, size_t count, uint64_t* glwes);
-/* Device buffers, enqueued on `stream` (NULL = the ctx stream). */
+/* Device buffers, enqueued on `stream` (NULL = the ctx stream, TFHE_HIP_NULL_STREAM = the null stream). */
 int tfhe_hip_pks_pack_async(tfhe_pks_ctx* ctx, const uint64_t* d_lwes, size_t count, uint64_t* d_glwes, void* stream);
 size_t tfhe_hip_pks_packed_words(const tfhe_pks_params* pp, uint32_t bodies);
 int tfhe_hip_pks_compress(const tfhe_pks_params* pp, const uint64_t* glwe, uint32_t bodies, uint64_t* packed);

@@ -63,3 +63,15 @@ def test_compress_ciphertexts_into_list(setup, oracle_mod):
         ph = C.glwe_phase(1, 2048, ck.post_packing_key, c.extract())[:c.bodies]
         got.append(((ph + np.uint64(1 << 44)) >> np.uint64(45)) % np.uint64(2048))
     assert np.array_equal(np.concatenate(got), (np.arange(count, dtype=np.uint64) * 7) % 2048)
+
+
+def test_pack_async_orders_with_torch_default_stream(setup):
+    import torch
+    pp, opp, ck, ok, packer = setup
+    lwes = np.random.default_rng(3).integers(0, 2 ** 64 - 1, size=(40, pp.in_dim + 1), dtype=np.uint64)
+    ref = packer.pack(lwes)
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(lwes.view(np.int64)).to(dev)
+    d_out = torch.zeros((1, pp.glwe_len), dtype=torch.int64, device=dev)
+    packer.pack_async(d_in, 40, d_out)            # torch's current (default) stream
+    assert np.array_equal(d_out.cpu().numpy().view(np.uint64), ref)

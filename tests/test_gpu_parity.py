@@ -190,6 +190,10 @@ def test_device_resident_async_and_device_keys(engine, product_keys):
     eng2.pbs_async(d_in, d_lut, d_out)
     torch.cuda.synchronize()
     assert np.array_equal(d_out.cpu().numpy().view(np.uint64), ref)
+    # ordered with torch's default stream without an explicit device synchronize
+    d_out2 = torch.zeros_like(d_in)
+    eng2.pbs_async(d_in, d_lut, d_out2)
+    assert np.array_equal(d_out2.cpu().numpy().view(np.uint64), ref)
     eng2.close()
 
 

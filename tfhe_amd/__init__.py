@@ -155,6 +155,20 @@ def lib():
     return _LIB
 
 
+NULL_STREAM = ctypes.c_void_p(-1).value  # TFHE_HIP_NULL_STREAM: the device's legacy null stream
+
+
+def _stream_handle(stream, device: int) -> int:
+    """torch.cuda.Stream / raw handle / None (torch's current stream) -> the C-ABI stream argument.
+    torch's default stream has handle 0, which the C ABI reads as "ctx stream": map it to
+    TFHE_HIP_NULL_STREAM so the work really is ordered with torch's default stream."""
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream(device)
+    h = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream or 0)
+    return h if h else NULL_STREAM
+
+
 def _check(rc: int) -> None:
     if rc != 0:
         raise TfheError(rc, lib().tfhe_hip_last_error().decode(errors="replace"))
@@ -384,11 +398,7 @@ class Engine:
         """Device-resident batch (torch tensors on this device), enqueued on ``stream``
         (a torch.cuda.Stream or raw handle; default torch's current stream if torch is loaded)."""
         B = d_in.shape[0]
-        if stream is None:
-            import torch
-            stream = torch.cuda.current_stream(self.device).cuda_stream
-        elif hasattr(stream, "cuda_stream"):
-            stream = stream.cuda_stream
+        stream = _stream_handle(stream, self.device)
         n_lut = d_luts.numel() // self.params.N
         _check(lib().tfhe_hip_pbs_async(self._h, ctypes.c_void_p(d_in.data_ptr()), B,
                                         ctypes.c_void_p(d_luts.data_ptr()), n_lut,

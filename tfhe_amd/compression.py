@@ -16,7 +16,7 @@ from typing import List, Optional
 
 import numpy as np
 
-from . import _c_u64, _check, _u64, lib
+from . import _c_u64, _check, _stream_handle, _u64, lib
 
 PKS_PRESET_ML2048 = 0
 _U64P = ctypes.POINTER(ctypes.c_uint64)
@@ -114,7 +114,7 @@ class Packer:
     """Device context for the packing keyswitch (one GPU)."""
 
     def __init__(self, params: PksParams, device: int = 0):
-        self.params = params
+        self.params, self.device = params, device
         h = ctypes.c_void_p()
         _check(_lib().tfhe_hip_pks_create(ctypes.byref(params), device, ctypes.byref(h)))
         self._h = h
@@ -145,10 +145,11 @@ class Packer:
         return out
 
     def pack_async(self, d_lwes, count: int, d_glwes, stream=None) -> None:
-        """torch device tensors (int64/uint64), enqueued on `stream` (a torch.cuda.Stream or None)."""
-        s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+        """torch device tensors (int64/uint64), enqueued on `stream` (torch.cuda.Stream, raw handle, or None =
+        torch's current stream)."""
         _check(_lib().tfhe_hip_pks_pack_async(self._h, ctypes.c_void_p(d_lwes.data_ptr()), count,
-                                              ctypes.c_void_p(d_glwes.data_ptr()), s))
+                                              ctypes.c_void_p(d_glwes.data_ptr()),
+                                              ctypes.c_void_p(_stream_handle(stream, self.device))))
 
     def compress_ciphertexts_into_list(self, lwes: np.ndarray) -> List[CompressedGlwe]:
         """compression.rs:246-291: pack chunks of lwe_per_glwe, then modulus-switch + bit-pack each."""

@@ -472,7 +472,7 @@ int tfhe_hip_pbs_async(tfhe_ctx* c, const uint64_t* d_in, size_t B, const uint64
   if (B > 0x7FFFFFFF) return fail(TFHE_HIP_EINVAL, "pbs: batch too large");
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  return pbs_device(c, d_in, B, d_luts, n_lut, d_idx, d_out, stream ? (hipStream_t)stream : c->stream);
+  return pbs_device(c, d_in, B, d_luts, n_lut, d_idx, d_out, stream == TFHE_HIP_NULL_STREAM ? (hipStream_t)0 : stream ? (hipStream_t)stream : c->stream);
 }
 
 int tfhe_hip_pbs(tfhe_ctx* c, const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,

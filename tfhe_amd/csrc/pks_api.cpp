@@ -190,7 +190,7 @@ int tfhe_hip_pks_pack_async(tfhe_pks_ctx* c, const uint64_t* d_lwes, size_t coun
   if (!d_lwes || !d_glwes) return fail(TFHE_HIP_EINVAL, "pks_pack: null buffer");
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
-  return pack_device(c, d_lwes, count, d_glwes, stream ? (hipStream_t)stream : c->stream);
+  return pack_device(c, d_lwes, count, d_glwes, stream == TFHE_HIP_NULL_STREAM ? (hipStream_t)0 : stream ? (hipStream_t)stream : c->stream);
 }
 
 int tfhe_hip_pks_pack(tfhe_pks_ctx* c, const uint64_t* lwes, size_t count, uint64_t* glwes) {
