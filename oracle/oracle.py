@@ -355,3 +355,77 @@ def pks_extract(pp: PksParams, packed: np.ndarray, bodies: int) -> np.ndarray:
     lib().or_pks_extract(ctypes.byref(pp), _p(np.ascontiguousarray(packed, dtype=np.uint64)), ctypes.c_uint32(bodies),
                          _p(out))
     return out
+
+
+# ---- switch-and-squash / noise squashing (sns_oracle.c) ----------------------------------------
+class SnsParams(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32), ("k", ctypes.c_uint32), ("N", ctypes.c_uint32), ("base_log", ctypes.c_uint32),
+                ("level", ctypes.c_uint32), ("noise_log2", ctypes.c_int32)]
+
+
+def sns_params(preset: int = 0) -> SnsParams:
+    p = SnsParams()
+    assert lib().or_sns_params_preset(preset, ctypes.byref(p)) == 0
+    return p
+
+
+class SnsKeys:
+    def __init__(self, sp: SnsParams, seed: int, lwe_key: np.ndarray, with_bsk: bool = True):
+        L = lib()
+        L.or_sns_bsk_len.restype = ctypes.c_size_t
+        self.sp, self.seed = sp, seed
+        self.lwe_key = np.ascontiguousarray(lwe_key, dtype=np.uint64)
+        self.glwe_key = np.zeros(sp.k * sp.N, dtype=np.uint64)
+        self.bsk = np.zeros(L.or_sns_bsk_len(ctypes.byref(sp)), dtype=np.uint64) if with_bsk else None
+        L.or_sns_keygen(ctypes.byref(sp), ctypes.c_uint64(seed), _p(self.lwe_key), _p(self.glwe_key),
+                        _p(self.bsk) if with_bsk else None)
+        self._bsk_ntt = None
+
+    @property
+    def bsk_ntt(self) -> np.ndarray:
+        if self._bsk_ntt is None:
+            self._bsk_ntt = np.zeros_like(self.bsk)
+            lib().or_sns_bsk_to_ntt(ctypes.byref(self.sp), _p(self.bsk), _p(self._bsk_ntt))
+        return self._bsk_ntt
+
+
+def sns_squash(sp: SnsParams, keys: SnsKeys, small: np.ndarray, msg_modulus: int = 16, threads: int = 0) -> np.ndarray:
+    small = np.ascontiguousarray(small, dtype=np.uint64).reshape(-1, sp.n + 1)
+    out = np.zeros((small.shape[0], sp.k * sp.N + 1, 2), dtype=np.uint64)
+    lib().or_sns_squash(ctypes.byref(sp), _p(keys.bsk_ntt), _p(small), ctypes.c_size_t(small.shape[0]),
+                        ctypes.c_uint32(msg_modulus), _p(out), ctypes.c_int(threads))
+    return out
+
+
+def sns_blind_rotate(sp: SnsParams, keys: SnsKeys, small: np.ndarray, lut: np.ndarray) -> np.ndarray:
+    acc = np.zeros((sp.k + 1, 2, sp.N), dtype=np.uint64)
+    lib().or_sns_blind_rotate(ctypes.byref(sp), _p(keys.bsk_ntt), _p(np.ascontiguousarray(small, dtype=np.uint64)),
+                              _p(np.ascontiguousarray(lut, dtype=np.uint64)), _p(acc))
+    return acc
+
+
+def sns_lut_identity(sp: SnsParams, msg_modulus: int = 16) -> np.ndarray:
+    lut = np.zeros((2, sp.N), dtype=np.uint64)
+    lib().or_sns_lut_identity(ctypes.byref(sp), ctypes.c_uint32(msg_modulus), _p(lut))
+    return lut
+
+
+def sns_sample_extract(sp: SnsParams, acc: np.ndarray) -> np.ndarray:
+    out = np.zeros((sp.k * sp.N + 1, 2), dtype=np.uint64)
+    lib().or_sns_sample_extract(ctypes.byref(sp), _p(np.ascontiguousarray(acc, dtype=np.uint64)), _p(out))
+    return out
+
+
+def sns_phase(sp: SnsParams, glwe_key: np.ndarray, cts: np.ndarray) -> list:
+    cts = np.ascontiguousarray(cts, dtype=np.uint64).reshape(-1, sp.k * sp.N + 1, 2)
+    out = np.zeros((cts.shape[0], 2), dtype=np.uint64)
+    lib().or_sns_phase(ctypes.byref(sp), _p(np.ascontiguousarray(glwe_key, dtype=np.uint64)), _p(cts),
+                       ctypes.c_size_t(cts.shape[0]), _p(out))
+    return [int(o[0]) | (int(o[1]) << 64) for o in out]
+
+
+def sns_ntt(which: int, a: np.ndarray, inverse: bool = False) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.uint64).copy()
+    f = lib().or_sns_ntt_inv if inverse else lib().or_sns_ntt_fwd
+    f(ctypes.c_int(which), _p(a), ctypes.c_uint32(a.size))
+    return a

@@ -1,0 +1,50 @@
+"""Noise squashing on the MI355X (tfhe_amd/csrc/sns.hip) against the oracle: the 128-bit blind
+rotation accumulator and the squashed LWE bit-exact, and the full path from P-FHEVM big-key
+ciphertexts (engine keyswitch + MS noise reduction + squash) decrypting every message."""
+import numpy as np
+import pytest
+
+from conftest import KEY_SEED
+from tfhe_amd import sns as S
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sns_setup(fhevm_keys, oracle_mod):
+    ck, _ = fhevm_keys
+    sp = S.SnsParams.preset(0)
+    key = S.SquashedKey(sp, KEY_SEED, ck.lwe_key)
+    osp = oracle_mod.sns_params(0)
+    okey = oracle_mod.SnsKeys(osp, KEY_SEED, ck.lwe_key)
+    assert np.array_equal(key.bsk, okey.bsk)
+    sq = S.Squasher(sp, 0).load_key(key)
+    yield sp, osp, key, okey, sq
+    sq.close()
+
+
+def test_squash_vs_oracle(sns_setup, fhevm_engine, fhevm_keys, oracle_mod):
+    sp, osp, key, okey, sq = sns_setup
+    ck, _ = fhevm_keys
+    msgs = np.array([1, 7, 14], dtype=np.uint64)
+    small = fhevm_engine.keyswitch(ck.encrypt(msgs, 16, seed=0xC0FFEE71))
+    small, _ = fhevm_engine.ms_reduce(small)
+    acc = sq.blind_rotate(small[:1])
+    lut = oracle_mod.sns_lut_identity(osp, 16)
+    assert np.array_equal(acc[0], oracle_mod.sns_blind_rotate(osp, okey, small[0], lut))
+    out = sq.squash(small)
+    assert np.array_equal(out, oracle_mod.sns_squash(osp, okey, small, 16, threads=16))
+    assert np.array_equal(key.decrypt(out), msgs)
+
+
+def test_squash_noise_batch(sns_setup, fhevm_engine, fhevm_keys):
+    sp, osp, key, okey, sq = sns_setup
+    ck, _ = fhevm_keys
+    B = 300
+    msgs = (np.arange(B) % 16).astype(np.uint64)
+    out = S.squash_noise(fhevm_engine, sq, ck.encrypt(msgs, 16, seed=0xC0FFEE72))
+    assert out.shape == (B, 4097, 2)
+    assert np.array_equal(key.decrypt(out), msgs)
+    delta = 1 << 123
+    noise = [((v - int(m) * delta + (1 << 127)) % (1 << 128)) - (1 << 127) for v, m in zip(key.phase(out), msgs)]
+    assert max(abs(e) for e in noise) < 2 ** 72

@@ -1,0 +1,66 @@
+"""Switch-and-squash / noise squashing (tfhe_amd/sns.py) on CPU: product key
+generation and decryption against the oracle (oracle/sns_oracle.c), the oracle's Z_Q NTT against a
+schoolbook product, and the oracle pipeline end to end at the full parameter set (keyswitch ->
+modulus-switch noise reduction -> 128-bit bootstrap) decrypting every message with ~2^-63 noise."""
+import numpy as np
+import pytest
+
+from conftest import KEY_SEED
+from tfhe_amd import sns as S
+
+
+def test_preset():
+    sp = S.SnsParams.preset(S.SNS_PRESET_FHEVM)
+    assert (sp.n, sp.k, sp.N, sp.base_log, sp.level) == (918, 2, 2048, 24, 3)
+
+
+def test_keygen_and_phase_match_oracle(oracle_mod):
+    sp = S.SnsParams.preset(0)
+    osp = oracle_mod.sns_params(0)
+    sp.n = osp.n = 12                              # key structure at a reduced input dimension
+    key = np.random.default_rng(2).integers(0, 2, 12).astype(np.uint64)
+    a = S.SquashedKey(sp, KEY_SEED, key)
+    b = oracle_mod.SnsKeys(osp, KEY_SEED, key)
+    assert np.array_equal(a.glwe_key, b.glwe_key) and np.array_equal(a.bsk, b.bsk)
+    assert a.bsk.size == 12 * 9 * 3 * 2 * 2048
+    cts = np.random.default_rng(3).integers(0, 2 ** 64 - 1, size=(3, 4097, 2), dtype=np.uint64)
+    assert a.phase(cts) == oracle_mod.sns_phase(osp, b.glwe_key, cts)
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_oracle_ntt_is_negacyclic_product(oracle_mod, which):
+    N = 64
+    p = [0xFFFFFFFF00000001, 0xFFFFFFFC00000001][which]
+    rng = np.random.default_rng(which)
+    x = rng.integers(0, 2 ** 40, N).astype(object)
+    y = rng.integers(0, 2 ** 40, N).astype(object)
+    want = [0] * N
+    for i in range(N):
+        for j in range(N):
+            t = x[i] * y[j]
+            if i + j < N:
+                want[i + j] += t
+            else:
+                want[i + j - N] -= t
+    X = oracle_mod.sns_ntt(which, np.array(x, dtype=np.uint64))
+    Y = oracle_mod.sns_ntt(which, np.array(y, dtype=np.uint64))
+    Z = np.array([(int(a) * int(b)) % p for a, b in zip(X, Y)], dtype=np.uint64)
+    got = oracle_mod.sns_ntt(which, Z, inverse=True)
+    assert [int(v) for v in got] == [w % p for w in want]
+
+
+def test_oracle_squash_end_to_end(oracle_mod):
+    prm = oracle_mod.params(1)
+    ok = oracle_mod.Keys(prm, KEY_SEED, with_bsk=False)
+    osp = oracle_mod.sns_params(0)
+    sk = oracle_mod.SnsKeys(osp, KEY_SEED, ok.lwe_key)
+    msgs = np.array([0, 5, 10, 15], dtype=np.uint64)
+    big = ok.encrypt(msgs * np.uint64((1 << 63) // 16), seed=0xC0FFEE70)
+    small = np.stack([oracle_mod.keyswitch(prm, ok, c) for c in big])
+    small, _ = oracle_mod.ms_reduce(prm, ok, small)
+    out = oracle_mod.sns_squash(osp, sk, small, 16, threads=8)
+    ph = oracle_mod.sns_phase(osp, sk.glwe_key, out)
+    delta = 1 << 123
+    assert [((v + delta // 2) // delta) % 16 for v in ph] == [int(m) for m in msgs]
+    noise = [((v - int(m) * delta + (1 << 127)) % (1 << 128)) - (1 << 127) for v, m in zip(ph, msgs)]
+    assert max(abs(e) for e in noise) < 2 ** 70      # squashed: ~2^65 of the 2^128 torus

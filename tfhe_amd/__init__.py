@@ -85,7 +85,9 @@ ABI_SYMBOLS = (
     "tfhe_hip_ms_reduce", "tfhe_hip_pks_params_preset", "tfhe_hip_pksk_len", "tfhe_hip_pks_keygen",
     "tfhe_hip_pks_create", "tfhe_hip_pks_destroy", "tfhe_hip_pks_load_key", "tfhe_hip_pks_pack",
     "tfhe_hip_pks_pack_async", "tfhe_hip_pks_packed_words", "tfhe_hip_pks_compress", "tfhe_hip_pks_extract",
-    "tfhe_hip_glwe_phase",
+    "tfhe_hip_glwe_phase", "tfhe_hip_sns_params_preset", "tfhe_hip_sns_bsk_len", "tfhe_hip_sns_keygen",
+    "tfhe_hip_sns_create", "tfhe_hip_sns_destroy", "tfhe_hip_sns_load_key", "tfhe_hip_sns_squash",
+    "tfhe_hip_sns_squash_async", "tfhe_hip_sns_blind_rotate", "tfhe_hip_sns_phase",
 )
 
 # P-FHEVM modulus-switch noise reduction key (include/tfhe_hip.h TFHE_HIP_MS_FHEVM_*)
