@@ -57,7 +57,7 @@ def log(msg: str) -> None:
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def pmc_traffic(B: int):
+def pmc_traffic(B: int, kernel: str = "blind_rotate_kernel"):
     """HBM bytes per blind-rotate launch from the committed rocprofv3 PMC passes
     (profiles/*_pmc_blind_rotate.json, produced by tools/pmc_summary.py for this same command), or None."""
     import glob
@@ -66,12 +66,12 @@ def pmc_traffic(B: int):
         return None
     d = json.load(open(files[-1]))
     for k, v in d.items():
-        if "blind_rotate_kernel" in k:
+        if kernel in k:
             return round(v["hbm_bytes_per_launch"])
     return None
 
 
-def valu_profile(B: int, kernel_ms: float):
+def valu_profile(B: int, kernel_ms: float, kernel: str = "blind_rotate_kernel"):
     """VALU roofline of the blind-rotate kernel from the committed SQ counter pass
     (profiles/*_pmc_sq.csv: rocprofv3 --pmc SQ_INSTS_VALU ... of this bench at B = 4096): wave64 VALU
     instructions per launch (scaled per PBS to B) x 4 cycles on a 16-lane SIMD, over the SIMD-cycles of
@@ -82,7 +82,7 @@ def valu_profile(B: int, kernel_ms: float):
     if not files:
         return None
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(files[-1]))
-            if r["Counter_Name"] == "SQ_INSTS_VALU" and "blind_rotate_kernel" in r["Kernel_Name"]]
+            if r["Counter_Name"] == "SQ_INSTS_VALU" and kernel in r["Kernel_Name"]]
     if not vals:
         return None
     insts = sum(vals) / len(vals) / 4096 * B
@@ -99,7 +99,10 @@ def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int
     prm = O.params(preset)
     t = time.time()
     keys = O.Keys(prm, KEY_SEED)
-    keys.bsk_ntt
+    if prm.transform == 1:
+        keys.bsk_fourier
+    else:
+        keys.bsk_ntt
     log(f"oracle keys in {time.time() - t:.1f}s")
     lut = O.lut_constant(1024, O.MU)[None] if lut_host is None else lut_host[None]
     sel = cts[:sample]
@@ -112,8 +115,9 @@ def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int
         "unit": "PBS/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{sample} PBS of the same {'P-GATE' if preset == 0 else 'P-FHEVM'} batch (first {sample} ciphertexts), C oracle "
-                  f"(oracle/tfhe_oracle.c, -O3 -march=x86-64-v3, OpenMP {threads} threads, one PBS per thread), "
+        "sample": f"{sample} PBS of the same {('P-GATE', 'P-FHEVM', 'P-GATE FFT64')[preset]} batch (first {sample} "
+                  f"ciphertexts), C oracle ({'oracle/fft_oracle.c' if preset == 2 else 'oracle/tfhe_oracle.c'}, -O3 "
+                  f"-march=x86-64-v3, OpenMP {threads} threads, one PBS per thread), "
                   f"{dt:.1f}s",
     }, bool(np.array_equal(ref, gpu_out[:sample]))
 
@@ -127,8 +131,9 @@ def main() -> int:
     ap.add_argument("--cpu-sample", type=int, default=0, help="PBS in the CPU baseline sample (0 = auto)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on GPUs; gloo only for rehearsals")
-    ap.add_argument("--preset", choices=["gate", "fhevm"], default="gate",
-                    help="gate = the BASELINE metric (P-GATE); fhevm = production fhEVM parameters (secondary line)")
+    ap.add_argument("--preset", choices=["gate", "gate_fft", "fhevm"], default="gate",
+                    help="gate = the BASELINE metric (P-GATE, NTT transform); gate_fft = P-GATE on the FFT64 transform "
+                         "(tfhe-rs's f64 FFT); fhevm = production fhEVM parameters (secondary line)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses device 0 (with --dist-backend gloo)")
     args = ap.parse_args()
@@ -150,7 +155,10 @@ def main() -> int:
             dist.init_process_group(args.dist_backend)
 
     fhevm = args.preset == "fhevm"
-    params = tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM if fhevm else tfhe_amd.PRESET_GATE)
+    fft = args.preset == "gate_fft"
+    params = tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM if fhevm else
+                                    tfhe_amd.PRESET_GATE_FFT if fft else tfhe_amd.PRESET_GATE)
+    br_kernel = "blind_rotate2048_kernel" if fhevm else "blind_rotate_fft_kernel" if fft else "blind_rotate_kernel"
     br_bytes = BR_BYTES_PER_PBS_FHEVM if fhevm else BR_BYTES_PER_PBS
     B = args.batch
 
@@ -245,13 +253,15 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u64",
+            "dtype": "f64" if fft else "u64",
             "data": ("synthetic: ChaCha20-seeded LWE encryptions of uniform bits (key seed 0x7F4E0001), gate LUT"
                      if not fhevm else "synthetic: ChaCha20-seeded shortint encryptions m < 16 under the big key "
                      "(key seed 0x7F4E0001), identity LUT"),
             "config": {
                 "workload": ("P-GATE PBS (blind rotate + sample extract + keyswitch), n=630 k=1 N=1024, "
-                             f"PBS 2^7x3, KS 2^2x8, batch {B} per GPU") if not fhevm else
+                             f"PBS 2^7x3, KS 2^2x8, batch {B} per GPU"
+                             + (", FFT64 transform (f64 FFT over the 2^64 torus)" if fft else ", NTT transform (Z_p)"))
+                            if not fhevm else
                             ("P-FHEVM PBS (keyswitch + blind rotate + sample extract), n=918 k=1 N=2048, "
                              f"PBS 2^23x1, KS 2^4x4, batch {B} per GPU"),
                 "batch_per_gpu": B,
@@ -260,17 +270,17 @@ def main() -> int:
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": ("blind_rotate2048_kernel" if fhevm else "blind_rotate_kernel") + " (+fused sample extract)",
+                "kernel": br_kernel + " (+fused sample extract)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None if fhevm else pmc_traffic(B),
+                "traffic": None if fhevm else pmc_traffic(B, br_kernel),
                 "bytes_per_launch": B * br_bytes,
                 "kernel_ms": round(br_avg, 3),
                 "launches": br_n,
             },
-            "valu_roofline": None if fhevm else valu_profile(B, br_avg),
+            "valu_roofline": None if fhevm else valu_profile(B, br_avg, br_kernel),
             "keyswitch_ms": round(ks_ms / max(ks_n, 1), 3),
             "ms_noise_reduction_ms": round(msr_ms / msr_n, 3) if msr_n else None,
             "key_broadcast_ms": round(bcast_ms, 3),
@@ -280,7 +290,7 @@ def main() -> int:
             threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
             # ~10-20 s of CPU work: the oracle does ~3.5 PBS/s per thread at P-GATE (~1.3 at P-FHEVM)
             sample = args.cpu_sample or (max(16 * threads, 32) if fhevm else max(40 * threads, 64))
-            cb, exact = cpu_baseline(cts, out, min(sample, B), threads, 1 if fhevm else 0,
+            cb, exact = cpu_baseline(cts, out, min(sample, B), threads, 1 if fhevm else 2 if fft else 0,
                                      lut_host if fhevm else None)
             result["cpu_baseline"] = cb
             result["sample_bitexact"] = exact

@@ -10,11 +10,13 @@
  *
  * Conventions
  *   - LWE ciphertexts: u64[dim + 1] = (a_0 .. a_{dim-1}, b), native torus Z_{2^64}.
- *   - GLWE / BSK values: Z_p, p = 2^64 - 2^32 + 1, canonical in [0, p).
+ *   - GLWE / BSK values: Z_p, p = 2^64 - 2^32 + 1, canonical in [0, p) (transform 0, the NTT engine);
+ *     native torus Z_{2^64} (transform 1, the FFT64 engine: tfhe-rs's own f64-FFT arithmetic).
  *   - BSK (standard domain): u64[n][(k+1)*l][k+1][N]; row index = c*l + lvl (c = component that
  *     carries s_i * 2^(64 - base_log*(lvl+1))), column = GLWE component (0..k-1 mask, k body).
  *   - KSK: u64[k*N][ks_level][n + 1], KSK[j][r] = LWE_s(s'_j * 2^(64 - ks_base_log*(r+1))).
- *   - LUT ("accumulator"): u64[N] in Z_p (see tfhe_hip_lut_*).
+ *   - LUT ("accumulator"): u64[N] in Z_p (see tfhe_hip_lut_*) for both transforms; the FFT64 engine
+ *     maps each value back to the torus (x + round(x / 2^32), exact for Delta * m, Delta >= 2^32).
  *   - Every function returns 0 on success or a negative TFHE_HIP_E* code; it never aborts.
  *     tfhe_hip_last_error() returns the message of the last failure on the calling thread.
  *   - Ownership: the caller owns every host buffer; calls read/write them synchronously (the
@@ -41,6 +43,10 @@ extern "C" {
 
 #define TFHE_HIP_PRESET_GATE 0   /* n=630 k=1 N=1024, PBS 7x3, KS 2x8 (TFHE 128-bit default) */
 #define TFHE_HIP_PRESET_FHEVM 1  /* n=918 k=1 N=2048, PBS 23x1, KS 4x4 (PARAM_MESSAGE_2_CARRY_2_KS_PBS) */
+#define TFHE_HIP_PRESET_GATE_FFT 2 /* P-GATE on the FFT64 transform (native-torus BSK, f64 FFT) */
+
+#define TFHE_HIP_TRANSFORM_NTT 0   /* GLWE/BSK over Z_p, Goldilocks NTT (exact integer arithmetic) */
+#define TFHE_HIP_TRANSFORM_FFT64 1 /* GLWE/BSK over Z_2^64, f64 FFT (tfhe-rs FFT64; oracle/fft_oracle.c) */
 
 typedef struct tfhe_params {
   uint32_t n, k, N;
@@ -49,6 +55,7 @@ typedef struct tfhe_params {
   int32_t lwe_noise_log2;  /* stddev as log2 of a torus fraction */
   int32_t glwe_noise_log2;
   uint32_t order;          /* 0 = PBS then KS (ciphertexts under the small key), 1 = KS then PBS */
+  uint32_t transform;      /* TFHE_HIP_TRANSFORM_*: external-product arithmetic (and BSK domain) */
 } tfhe_params;
 
 typedef struct tfhe_ctx tfhe_ctx;
@@ -133,7 +140,7 @@ int tfhe_hip_pbs_async(tfhe_ctx* ctx, const uint64_t* d_lwe_in, size_t B, const 
                        const uint32_t* d_lut_index, uint64_t* d_lwe_out, void* stream);
 
 /* Stage-level entry points (host buffers) used by the parity tests. */
-/* acc_out: B x (k+1) x N values in Z_p (coefficient domain) after the CMUX loop. */
+/* acc_out: B x (k+1) x N values in the GLWE ring (Z_p for NTT, torus for FFT64) after the CMUX loop. */
 int tfhe_hip_blind_rotate(tfhe_ctx* ctx, const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
                           const uint32_t* lut_index, uint64_t* acc_out);
 /* acc (Z_p, B x (k+1)N) -> LWE under the GLWE key, converted to 2^64: B x (kN + 1). */
@@ -144,6 +151,13 @@ int tfhe_hip_keyswitch(tfhe_ctx* ctx, const uint64_t* lwe_big, size_t B, uint64_
  * A[j] = a(psi^(2j+1)), psi the primitive 2N-th root with psi^(2N/64) = 8.  ntt_inv includes 1/N. */
 int tfhe_hip_ntt_fwd(tfhe_ctx* ctx, uint64_t* polys, size_t count);
 int tfhe_hip_ntt_inv(tfhe_ctx* ctx, uint64_t* polys, size_t count);
+
+/* FFT64 transform (N = 1024), natural order, for parity tests of the device FFT against
+ * oracle/fft_oracle.c: fwd reads count x N torus values as int64, writes count x N/2 complex (re, im
+ * doubles); inv reads count x N/2 complex and writes count x N doubles (no 1/M, no rounding).
+ * EUNSUPPORTED unless the ctx was created with transform = TFHE_HIP_TRANSFORM_FFT64. */
+int tfhe_hip_fft_fwd(tfhe_ctx* ctx, const uint64_t* polys, size_t count, double* out);
+int tfhe_hip_fft_inv(tfhe_ctx* ctx, const double* in, size_t count, double* out);
 
 /* Gate bootstrapping (FheBool NAND): out = PBS((0, 1/8) - c1 - c2, LUT == 1/8), B gates. */
 int tfhe_hip_nand(tfhe_ctx* ctx, const uint64_t* c1, const uint64_t* c2, size_t B, uint64_t* out);

@@ -97,6 +97,17 @@ static int get_params(napi_env env, napi_value v, tfhe_params* p) {
   p->n = vals[0]; p->k = vals[1]; p->N = vals[2]; p->pbs_base_log = vals[3]; p->pbs_level = vals[4];
   p->ks_base_log = vals[5]; p->ks_level = vals[6]; p->lwe_noise_log2 = vals[7]; p->glwe_noise_log2 = vals[8];
   p->order = vals[9];
+  p->transform = 0; /* optional: TFHE_HIP_TRANSFORM_* (absent = NTT) */
+  {
+    napi_value f;
+    bool has = false;
+    if (napi_has_named_property(env, v, "transform", &has) == napi_ok && has &&
+        napi_get_named_property(env, v, "transform", &f) == napi_ok) {
+      int32_t tr = 0;
+      if (napi_get_value_int32(env, f, &tr) != napi_ok) return 0;
+      p->transform = (uint32_t)tr;
+    }
+  }
   return 1;
 }
 
@@ -107,6 +118,7 @@ static napi_value params_to_js(napi_env env, const tfhe_params* p) {
   SETF("n", p->n) SETF("k", p->k) SETF("N", p->N) SETF("pbs_base_log", p->pbs_base_log)
   SETF("pbs_level", p->pbs_level) SETF("ks_base_log", p->ks_base_log) SETF("ks_level", p->ks_level)
   SETF("lwe_noise_log2", p->lwe_noise_log2) SETF("glwe_noise_log2", p->glwe_noise_log2) SETF("order", p->order)
+  SETF("transform", p->transform)
 #undef SETF
   return o;
 }
@@ -116,7 +128,7 @@ static napi_value js_params_preset(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  tfhe_params p;
+  tfhe_params p = {0};
   int32_t preset = 0;
   if (argc > 0) napi_get_value_int32(env, argv[0], &preset);
   int rc = tfhe_hip_params_preset(preset, &p);
@@ -129,7 +141,7 @@ static napi_value js_keygen(napi_env env, napi_callback_info info) {
   size_t argc = 3;
   napi_value argv[3];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  tfhe_params p;
+  tfhe_params p = {0};
   uint64_t seed = 0;
   if (argc < 2 || !get_params(env, argv[0], &p) || !get_u64(env, argv[1], &seed)) {
     napi_throw_type_error(env, "EINVAL", "keygen(params, seed[, withServerKey])");
@@ -272,7 +284,7 @@ static napi_value js_create(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  tfhe_params p;
+  tfhe_params p = {0};
   int32_t dev = 0;
   if (argc < 1 || !get_params(env, argv[0], &p)) {
     napi_throw_type_error(env, "EINVAL", "createEngine(params[, device])");

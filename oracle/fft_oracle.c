@@ -1,0 +1,324 @@
+/*
+ * fft_oracle.c — CPU restatement of the FFT64 external product (tfhe-rs's own arithmetic).
+ *
+ * TEST INFRASTRUCTURE ONLY (see tfhe_oracle.h): used by tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg as the checker; never linked into the product.
+ *
+ * tfhe-rs (npm tfhe / node-tfhe 0.8.7 — packages/pnpm-lock.yaml:1988-1995 — absent from the mount)
+ * runs keyswitch_programmable_bootstrap (ml/biometrics/notebooks/main.rs:71) over the native 2^64
+ * torus with the external product computed by an f64 negacyclic FFT (concrete-fft: fold the N real
+ * coefficients into N/2 complex, twist by zeta^j, zeta = e^{i pi/N}, cyclic DFT; BSK stored in the
+ * Fourier domain).  The exact product it approximates is the reference's wrapping negacyclic
+ * product (ml/extensions/rust/src/computations.rs:50-54,101-105); or_poly_mul_torus_schoolbook below
+ * computes that exactly and tests bound the FFT's deviation from it.
+ *
+ * This file fixes ONE operation sequence (every +, -, *, fma, in order) so the gfx950 kernels in
+ * tfhe_amd/csrc/pbs_fft.hip reproduce every double bit-for-bit:
+ *   cmul(z, w)       re = fma(z.re, w.re, -(z.im * w.im)),  im = fma(z.re, w.im, z.im * w.re)
+ *                    (inverse transforms use w = (w.re, -w.im))
+ *   dft8             radix-2 decimation in frequency, 3 stages, natural order in and out; the
+ *                    internal rotations by e^{+-i pi/4 j} are the explicit forms in w8() below
+ *   3 passes         M = 512 = 8 x 8 x 8 over a 64 x 8 grid (the device's lane x register grid):
+ *                    A: lane L = n0 + 8 n1 transforms n2, then x[k0] *= w^{L k0}           (k0 > 0)
+ *                    B: lane n0 + 8 k0 transforms n1, then x[k1] *= w^{8 n0 k1}            (k1 > 0)
+ *                    C: lane k0 + 8 k1 transforms n0 -> Z[k0 + 8 k1 + 64 k2] in slot k2
+ *   MAC              re = fma(D.re, K.re, re); re = fma(-D.im, K.im, re);
+ *                    im = fma(D.re, K.im, im); im = fma(D.im, K.re, im)   from (0, 0), r ascending
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "tfhe_oracle.h"
+
+#define FFT_M 512
+
+/* ---- twiddles: fixed series in plain double (no libm), |x| <= pi/4 ------------------------ */
+static double fs_sin(double x) {
+  double x2 = x * x, term = x, sum = 0.0;
+  for (int i = 1; i <= 21; i += 2) { sum += term; term = -term * x2 / (double)((i + 1) * (i + 2)); }
+  return sum;
+}
+static double fs_cos(double x) {
+  double x2 = x * x, term = 1.0, sum = 0.0;
+  for (int i = 0; i <= 20; i += 2) { sum += term; term = -term * x2 / (double)((i + 1) * (i + 2)); }
+  return sum;
+}
+static void tw_octant(uint32_t t, uint32_t M, double* c, double* s) { /* t <= M/8 */
+  const double x = (double)t * (6.28318530717958647692 / (double)M);
+  *c = fs_cos(x);
+  *s = fs_sin(x);
+}
+static void tw_quarter(uint32_t t, uint32_t M, double* c, double* s) { /* t <= M/4 */
+  if (8 * t > M) {
+    double cu, su;
+    tw_octant(M / 4 - t, M, &cu, &su);
+    *c = su;
+    *s = cu;
+  } else {
+    tw_octant(t, M, c, s);
+  }
+}
+void or_fft_twiddle(uint32_t t, uint32_t M, double* c, double* s) {
+  t %= M;
+  int neg = 0;
+  if (2 * t > M) { t = M - t; neg = 1; }
+  double cc, ss;
+  if (4 * t > M) { /* theta = pi/2 + phi */
+    double cu, su;
+    tw_quarter(t - M / 4, M, &cu, &su);
+    cc = -su;
+    ss = cu;
+  } else {
+    tw_quarter(t, M, &cc, &ss);
+  }
+  *c = cc;
+  *s = neg ? -ss : ss;
+}
+
+typedef struct fft_tab {
+  or_c64 twist[FFT_M];  /* zeta^j, zeta = e^{i pi / N} */
+  or_c64 twA[8][64];    /* w^{L k0}, w = e^{2 pi i / M} */
+  or_c64 twB[8][64];    /* w^{8 (L & 7) k1} */
+} fft_tab;
+
+static fft_tab g_tab;
+static int g_tab_ready = 0;
+
+static const fft_tab* tab(void) {
+#pragma omp critical(or_fft_tab)
+  {
+    if (!g_tab_ready) {
+      for (uint32_t j = 0; j < FFT_M; j++) or_fft_twiddle(j, 2 * FFT_M * 2, &g_tab.twist[j].re, &g_tab.twist[j].im);
+      for (uint32_t e = 0; e < 8; e++)
+        for (uint32_t L = 0; L < 64; L++) {
+          or_fft_twiddle((L * e) % FFT_M, FFT_M, &g_tab.twA[e][L].re, &g_tab.twA[e][L].im);
+          or_fft_twiddle((8 * (L & 7) * e) % FFT_M, FFT_M, &g_tab.twB[e][L].re, &g_tab.twB[e][L].im);
+        }
+      __atomic_store_n(&g_tab_ready, 1, __ATOMIC_RELEASE);
+    }
+  }
+  return &g_tab;
+}
+
+/* ---- complex pieces ------------------------------------------------------------------------ */
+static inline or_c64 cadd(or_c64 a, or_c64 b) { or_c64 r = {a.re + b.re, a.im + b.im}; return r; }
+static inline or_c64 csub(or_c64 a, or_c64 b) { or_c64 r = {a.re - b.re, a.im - b.im}; return r; }
+static inline or_c64 cmul(or_c64 z, double wr, double wi) {
+  or_c64 r = {fma(z.re, wr, -(z.im * wi)), fma(z.re, wi, z.im * wr)};
+  return r;
+}
+
+#define SQRT1_2 0.70710678118654752440
+/* t * e^{+-i pi j / 4}, j in 1..3, explicit forms (exact negations) */
+static inline or_c64 w8(or_c64 t, int j, int inv) {
+  const double p = t.re, q = t.im;
+  or_c64 r;
+  if (!inv) {
+    if (j == 1) { r.re = (p - q) * SQRT1_2; r.im = (p + q) * SQRT1_2; }
+    else if (j == 2) { r.re = -q; r.im = p; }
+    else { r.re = -((p + q) * SQRT1_2); r.im = (p - q) * SQRT1_2; }
+  } else {
+    if (j == 1) { r.re = (p + q) * SQRT1_2; r.im = (q - p) * SQRT1_2; }
+    else if (j == 2) { r.re = q; r.im = -p; }
+    else { r.re = (q - p) * SQRT1_2; r.im = -((p + q) * SQRT1_2); }
+  }
+  return r;
+}
+
+static void dft8(or_c64 x[8], int inv) {
+  or_c64 y[8], z[8], u[8];
+  for (int j = 0; j < 4; j++) {
+    y[j] = cadd(x[j], x[j + 4]);
+    const or_c64 t = csub(x[j], x[j + 4]);
+    y[j + 4] = j ? w8(t, j, inv) : t;
+  }
+  for (int h = 0; h < 8; h += 4)
+    for (int j = 0; j < 2; j++) {
+      z[h + j] = cadd(y[h + j], y[h + j + 2]);
+      const or_c64 t = csub(y[h + j], y[h + j + 2]);
+      z[h + j + 2] = j ? w8(t, 2, inv) : t;
+    }
+  for (int g = 0; g < 8; g += 2) {
+    u[g] = cadd(z[g], z[g + 1]);
+    u[g + 1] = csub(z[g], z[g + 1]);
+  }
+  static const int brv3[8] = {0, 4, 2, 6, 1, 5, 3, 7};
+  for (int k = 0; k < 8; k++) x[k] = u[brv3[k]];
+}
+
+/* the 3-pass DFT, natural order in and out (in may alias out) */
+static void dft512(const or_c64* in, or_c64* out, int inv) {
+  const fft_tab* T = tab();
+  const double sg = inv ? -1.0 : 1.0;
+  or_c64 A[64][8], Bv[64][8], x[8];
+  for (int L = 0; L < 64; L++) {
+    for (int e = 0; e < 8; e++) x[e] = in[L + 64 * e];
+    dft8(x, inv);
+    for (int e = 1; e < 8; e++) x[e] = cmul(x[e], T->twA[e][L].re, sg * T->twA[e][L].im);
+    memcpy(A[L], x, sizeof(x));
+  }
+  for (int L = 0; L < 64; L++) {
+    for (int e = 0; e < 8; e++) x[e] = A[(L & 7) + 8 * e][L >> 3];
+    dft8(x, inv);
+    for (int e = 1; e < 8; e++) x[e] = cmul(x[e], T->twB[e][L].re, sg * T->twB[e][L].im);
+    memcpy(Bv[L], x, sizeof(x));
+  }
+  for (int L = 0; L < 64; L++) {
+    for (int e = 0; e < 8; e++) x[e] = Bv[e + 8 * (L & 7)][L >> 3];
+    dft8(x, inv);
+    for (int e = 0; e < 8; e++) out[L + 64 * e] = x[e];
+  }
+}
+
+void or_fft_fwd(const double* a, uint32_t N, or_c64* out) {
+  if (N != 2 * FFT_M) abort();
+  const fft_tab* T = tab();
+  or_c64 z[FFT_M];
+  for (int j = 0; j < FFT_M; j++) {
+    const or_c64 v = {a[j], a[j + FFT_M]};
+    z[j] = cmul(v, T->twist[j].re, T->twist[j].im);
+  }
+  dft512(z, out, 0);
+}
+
+void or_fft_inv(const or_c64* in, uint32_t N, double* out) {
+  if (N != 2 * FFT_M) abort();
+  const fft_tab* T = tab();
+  or_c64 z[FFT_M];
+  dft512(in, z, 1);
+  for (int j = 0; j < FFT_M; j++) {
+    const or_c64 v = cmul(z[j], T->twist[j].re, -T->twist[j].im);
+    out[j] = v.re;
+    out[j + FFT_M] = v.im;
+  }
+}
+
+/* round(x) (ties to even) mod 2^64; every step after rint is exact */
+uint64_t or_f64_to_torus(double x) {
+  const double t = rint(x);
+  const double h = floor(t * 0x1p-32);
+  const double l = t - h * 0x1p32;
+  const double hh = floor(h * 0x1p-32);
+  const double hm = h - hh * 0x1p32;
+  return ((uint64_t)hm << 32) | (uint64_t)l;
+}
+
+void or_bsk_to_fourier(const or_params* p, const uint64_t* bsk, or_c64* bsk_f) {
+  const uint32_t N = p->N, M = N / 2;
+  const size_t polys = or_bsk_len(p) / N;
+#pragma omp parallel for schedule(static)
+  for (size_t q = 0; q < polys; q++) {
+    double a[2 * FFT_M];
+    for (uint32_t j = 0; j < N; j++) a[j] = (double)(int64_t)bsk[q * N + j];
+    or_c64* o = bsk_f + q * M;
+    or_fft_fwd(a, N, o);
+    for (uint32_t j = 0; j < M; j++) {
+      o[j].re = o[j].re * 0x1p-9;
+      o[j].im = o[j].im * 0x1p-9;
+    }
+  }
+}
+
+/* (X^t * in)[i] on native torus values, t in [0, 2N) */
+static void monomial_torus(uint64_t* out, const uint64_t* in, uint32_t N, uint32_t t) {
+  for (uint32_t i = 0; i < N; i++) {
+    int64_t d = (int64_t)i - (int64_t)t;
+    int neg = 0;
+    while (d < 0) { d += N; neg ^= 1; }
+    out[i] = neg ? 0 - in[d] : in[d];
+  }
+}
+
+void or_blind_rotate_fft(const or_params* p, const or_c64* bsk_f, const uint64_t* lwe_in, const uint64_t* lut,
+                         uint64_t* acc) {
+  const uint32_t N = p->N, M = N / 2, k = p->k, L = p->pbs_level, n = p->n;
+  if (k != 1 || N != 2 * FFT_M || L > 8) abort();
+  const size_t per_i = (size_t)(k + 1) * L * (k + 1) * M;
+  uint64_t lt[2 * FFT_M], rot[2 * FFT_M];
+  for (uint32_t i = 0; i < N; i++) lt[i] = or_p_to_tor(lut[i]); /* convert, then rotate */
+  memset(acc, 0, (size_t)N * 8);
+  const uint32_t bt = or_mod_switch(lwe_in[n], 2 * N);
+  monomial_torus(acc + N, lt, N, (2 * N - bt) % (2 * N));
+  double dig[8][2 * FFT_M];
+  or_c64 D[FFT_M], O[2][FFT_M];
+  double res[2 * FFT_M];
+  int64_t d[64];
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t a = or_mod_switch(lwe_in[i], 2 * N);
+    if (a == 0) continue; /* (X^0 - 1) acc == 0: every double stays +-0, rounds to 0 */
+    memset(O, 0, sizeof(O));
+    for (uint32_t c = 0; c <= k; c++) {
+      monomial_torus(rot, acc + (size_t)c * N, N, a);
+      for (uint32_t j = 0; j < N; j++) {
+        or_decompose(rot[j] - acc[(size_t)c * N + j], p->pbs_base_log, L, d);
+        for (uint32_t l = 0; l < L; l++) dig[l][j] = (double)d[l];
+      }
+      for (uint32_t l = 0; l < L; l++) {
+        or_fft_fwd(dig[l], N, D);
+        const or_c64* row = bsk_f + per_i * i + (size_t)(c * L + l) * (k + 1) * M;
+        for (uint32_t j = 0; j <= k; j++) {
+          const or_c64* K = row + (size_t)j * M;
+          for (uint32_t f = 0; f < M; f++) {
+            O[j][f].re = fma(D[f].re, K[f].re, O[j][f].re);
+            O[j][f].re = fma(-D[f].im, K[f].im, O[j][f].re);
+            O[j][f].im = fma(D[f].re, K[f].im, O[j][f].im);
+            O[j][f].im = fma(D[f].im, K[f].re, O[j][f].im);
+          }
+        }
+      }
+    }
+    for (uint32_t j = 0; j <= k; j++) {
+      or_fft_inv(O[j], N, res);
+      for (uint32_t f = 0; f < N; f++) acc[(size_t)j * N + f] += or_f64_to_torus(res[f]);
+    }
+  }
+}
+
+void or_sample_extract_torus(const or_params* p, const uint64_t* acc, uint64_t* out) {
+  const uint32_t N = p->N, k = p->k;
+  for (uint32_t c = 0; c < k; c++) {
+    const uint64_t* A = acc + (size_t)c * N;
+    out[(size_t)c * N] = A[0];
+    for (uint32_t j = 1; j < N; j++) out[(size_t)c * N + j] = 0 - A[N - j];
+  }
+  out[(size_t)k * N] = acc[(size_t)k * N];
+}
+
+void or_pbs_batch_fft(const or_params* p, const or_c64* bsk_f, const uint64_t* ksk, const uint64_t* lwe_in, size_t B,
+                      const uint64_t* luts, size_t n_lut, const uint32_t* lut_index, uint64_t* lwe_out, int threads) {
+  if (p->order != 0) abort();
+  const size_t din = (size_t)p->n + 1, big = (size_t)p->k * p->N + 1, row = (size_t)(p->k + 1) * p->N;
+#ifdef _OPENMP
+  if (threads <= 0) threads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
+#endif
+  for (size_t q = 0; q < B; q++) {
+    size_t li = lut_index ? lut_index[q] : 0;
+    if (li >= n_lut) li = 0;
+    uint64_t* acc = (uint64_t*)malloc(row * 8);
+    uint64_t* ext = (uint64_t*)malloc(big * 8);
+    or_blind_rotate_fft(p, bsk_f, lwe_in + q * din, luts + li * p->N, acc);
+    or_sample_extract_torus(p, acc, ext);
+    or_keyswitch(p, ksk, ext, lwe_out + q * din);
+    free(acc);
+    free(ext);
+  }
+  (void)threads;
+}
+
+void or_poly_mul_torus_schoolbook(uint64_t* out, const int64_t* a, const uint64_t* b, uint32_t N) {
+  memset(out, 0, (size_t)N * 8);
+  for (uint32_t i = 0; i < N; i++) {
+    if (!a[i]) continue;
+    const uint64_t ai = (uint64_t)a[i];
+    for (uint32_t j = 0; j < N; j++) {
+      const uint32_t d = i + j;
+      if (d < N) out[d] += ai * b[j];
+      else out[d - N] -= ai * b[j];
+    }
+  }
+}

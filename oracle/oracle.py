@@ -26,7 +26,7 @@ class Params(ctypes.Structure):
         ("pbs_base_log", ctypes.c_uint32), ("pbs_level", ctypes.c_uint32),
         ("ks_base_log", ctypes.c_uint32), ("ks_level", ctypes.c_uint32),
         ("lwe_noise_log2", ctypes.c_int32), ("glwe_noise_log2", ctypes.c_int32),
-        ("order", ctypes.c_uint32),
+        ("order", ctypes.c_uint32), ("transform", ctypes.c_uint32),
     ]
 
 
@@ -74,6 +74,8 @@ def lib():
         L.or_ms_reduce.restype = ctypes.c_int
         L.or_bsk_len.restype = ctypes.c_size_t
         L.or_ksk_len.restype = ctypes.c_size_t
+        L.or_f64_to_torus.restype = ctypes.c_uint64
+        L.or_f64_to_torus.argtypes = [ctypes.c_double]
         _LIB = L
     return _LIB
 
@@ -192,6 +194,14 @@ class Keys:
             lib().or_bsk_to_ntt(ctypes.byref(self.prm), _p(self.bsk), _p(self._bsk_ntt))
         return self._bsk_ntt
 
+    @property
+    def bsk_fourier(self) -> np.ndarray:
+        """FFT64 transform: Fourier-domain BSK, complex128 [polys][N/2] (or_bsk_to_fourier)."""
+        if getattr(self, "_bsk_f", None) is None:
+            self._bsk_f = np.zeros((self.bsk.size // self.prm.N, self.prm.N // 2), dtype=np.complex128)
+            lib().or_bsk_to_fourier(ctypes.byref(self.prm), _p(self.bsk), _p(self._bsk_f, ctypes.c_void_p))
+        return self._bsk_f
+
     # --- encryption under the input-side key (small key for PBS_KS order, big for KS_PBS) ---
     def in_key(self):
         return (self.lwe_key, self.prm.n) if self.prm.order == 0 else (self.glwe_key, self.prm.k * self.prm.N)
@@ -256,6 +266,8 @@ def ms_reduce(prm: Params, keys: Keys, small: np.ndarray):
 
 def pbs_batch(prm: Params, keys: Keys, lwe_in: np.ndarray, luts: np.ndarray, lut_index=None,
               threads: int = 0, ms: bool = True) -> np.ndarray:
+    if prm.transform == 1:
+        return pbs_batch_fft(prm, keys, lwe_in, luts, lut_index, threads)
     lwe_in = np.ascontiguousarray(lwe_in, dtype=np.uint64)
     luts = np.ascontiguousarray(luts, dtype=np.uint64).reshape(-1, prm.N)
     B = lwe_in.shape[0]
@@ -269,6 +281,72 @@ def pbs_batch(prm: Params, keys: Keys, lwe_in: np.ndarray, luts: np.ndarray, lut
                        _p(lwe_in), ctypes.c_size_t(B),
                        _p(luts), ctypes.c_size_t(luts.shape[0]), _p(li, U32P) if li is not None else None,
                        _p(out), ctypes.c_int(threads))
+    return out
+
+
+# ---- FFT64 transform (fft_oracle.c) -----------------------------------------------------------------
+def fft_fwd(a) -> np.ndarray:
+    """N real values (exact doubles, e.g. digits or int64 torus values) -> N/2 complex128."""
+    a = np.ascontiguousarray(a, dtype=np.float64).reshape(-1, np.shape(a)[-1])
+    N = a.shape[1]
+    out = np.zeros((a.shape[0], N // 2), dtype=np.complex128)
+    for i in range(a.shape[0]):
+        lib().or_fft_fwd(_p(a[i], ctypes.c_void_p), ctypes.c_uint32(N), _p(out[i], ctypes.c_void_p))
+    return out
+
+
+def fft_inv(z) -> np.ndarray:
+    """N/2 complex -> N doubles, without the 1/M factor and without rounding."""
+    z = np.ascontiguousarray(z, dtype=np.complex128).reshape(-1, np.shape(z)[-1])
+    N = 2 * z.shape[1]
+    out = np.zeros((z.shape[0], N), dtype=np.float64)
+    for i in range(z.shape[0]):
+        lib().or_fft_inv(_p(z[i], ctypes.c_void_p), ctypes.c_uint32(N), _p(out[i], ctypes.c_void_p))
+    return out
+
+
+def f64_to_torus(x: float) -> int:
+    return int(lib().or_f64_to_torus(float(x)))
+
+
+def fft_twiddle(t: int, M: int) -> tuple:
+    c, s = ctypes.c_double(), ctypes.c_double()
+    lib().or_fft_twiddle(ctypes.c_uint32(t), ctypes.c_uint32(M), ctypes.byref(c), ctypes.byref(s))
+    return c.value, s.value
+
+
+def poly_mul_torus_schoolbook(a_small, b) -> np.ndarray:
+    a = np.ascontiguousarray(a_small, dtype=np.int64)
+    b = np.ascontiguousarray(b, dtype=np.uint64)
+    out = np.zeros(b.shape[0], dtype=np.uint64)
+    lib().or_poly_mul_torus_schoolbook(_p(out), _p(a, I64P), _p(b), ctypes.c_uint32(b.shape[0]))
+    return out
+
+
+def blind_rotate_fft(prm: Params, keys: Keys, lwe_in: np.ndarray, lut: np.ndarray) -> np.ndarray:
+    acc = np.zeros((prm.k + 1) * prm.N, dtype=np.uint64)
+    lib().or_blind_rotate_fft(ctypes.byref(prm), _p(keys.bsk_fourier, ctypes.c_void_p),
+                              _p(np.ascontiguousarray(lwe_in, dtype=np.uint64)),
+                              _p(np.ascontiguousarray(lut, dtype=np.uint64)), _p(acc))
+    return acc
+
+
+def sample_extract_torus(prm: Params, acc: np.ndarray) -> np.ndarray:
+    out = np.zeros(prm.k * prm.N + 1, dtype=np.uint64)
+    lib().or_sample_extract_torus(ctypes.byref(prm), _p(np.ascontiguousarray(acc, dtype=np.uint64)), _p(out))
+    return out
+
+
+def pbs_batch_fft(prm: Params, keys: Keys, lwe_in: np.ndarray, luts: np.ndarray, lut_index=None,
+                  threads: int = 0) -> np.ndarray:
+    lwe_in = np.ascontiguousarray(lwe_in, dtype=np.uint64)
+    luts = np.ascontiguousarray(luts, dtype=np.uint64).reshape(-1, prm.N)
+    B = lwe_in.shape[0]
+    out = np.zeros((B, prm.n + 1), dtype=np.uint64)
+    li = np.ascontiguousarray(lut_index, dtype=np.uint32) if lut_index is not None else None
+    lib().or_pbs_batch_fft(ctypes.byref(prm), _p(keys.bsk_fourier, ctypes.c_void_p), _p(keys.ksk), _p(lwe_in),
+                           ctypes.c_size_t(B), _p(luts), ctypes.c_size_t(luts.shape[0]),
+                           _p(li, U32P) if li is not None else None, _p(out), ctypes.c_int(threads))
     return out
 
 

@@ -32,6 +32,11 @@ int or_params_preset(int preset, or_params* o) {
     o->order = 0;
     return 0;
   }
+  if (preset == 2) { /* P-GATE, FFT64 transform (native torus BSK) */
+    or_params_preset(0, o);
+    o->transform = 1;
+    return 0;
+  }
   if (preset == 1) {
     o->n = 918; o->k = 1; o->N = 2048;
     o->pbs_base_log = 23; o->pbs_level = 1;
@@ -363,6 +368,9 @@ static void glwe_encrypt_zero_p(const or_params* p, const uint64_t* glwe_key, or
   }
 }
 
+static void glwe_encrypt_native(uint32_t k, uint32_t N, const uint64_t* key, int32_t noise_log2, or_rng* r,
+                                const uint64_t* m, uint64_t* out);
+
 static void lwe_encrypt_one(uint32_t dim, const uint64_t* key, int32_t noise_log2, or_rng* r, uint64_t m,
                             uint64_t* out) {
   uint64_t b = 0;
@@ -397,10 +405,13 @@ void or_server_keygen(const or_params* p, uint64_t seed, const uint64_t* lwe_key
       for (uint32_t c = 0; c <= k; c++)
         for (uint32_t l = 0; l < L; l++) {
           uint64_t* out = bsk + per_i * i + row * (c * L + l);
-          glwe_encrypt_zero_p(p, glwe_key, &rr, out);
-          if (lwe_key[i]) {
-            uint64_t g = 1ull << (64 - p->pbs_base_log * (l + 1));
-            out[(size_t)c * N] = or_add(out[(size_t)c * N], g);
+          uint64_t g = 1ull << (64 - p->pbs_base_log * (l + 1));
+          if (p->transform == 1) { /* native torus GGSW (FFT64) */
+            glwe_encrypt_native(k, N, glwe_key, p->glwe_noise_log2, &rr, NULL, out);
+            if (lwe_key[i]) out[(size_t)c * N] += g;
+          } else {
+            glwe_encrypt_zero_p(p, glwe_key, &rr, out);
+            if (lwe_key[i]) out[(size_t)c * N] = or_add(out[(size_t)c * N], g);
           }
         }
     }

@@ -48,9 +48,11 @@ typedef struct or_params {
   int32_t lwe_noise_log2;   /* stddev = 2^x of the torus */
   int32_t glwe_noise_log2;
   uint32_t order;           /* 0 = PBS then KS (small key ciphertexts), 1 = KS then PBS */
+  uint32_t transform;       /* 0 = NTT over Z_p (Goldilocks); 1 = f64 FFT over the native 2^64 torus */
 } or_params;
 
-/* preset 0 = P-GATE (n=630,k=1,N=1024, 7x3, 2x8), preset 1 = P-FHEVM (918,1,2048, 23x1, 4x4). */
+/* preset 0 = P-GATE (n=630,k=1,N=1024, 7x3, 2x8), preset 1 = P-FHEVM (918,1,2048, 23x1, 4x4),
+ * preset 2 = P-GATE on the FFT64 transform (fft_oracle.c). */
 int or_params_preset(int preset, or_params* out);
 
 /* ---- PRNG (ChaCha20, RFC 8439 block function) -------------------------------------- */
@@ -210,6 +212,45 @@ void or_sns_squash(const or_sns_params* sp, const uint64_t* bsk_ntt, const uint6
                    uint32_t msg_modulus, uint64_t* out, int threads);
 void or_sns_phase(const or_sns_params* sp, const uint64_t* glwe_key, const uint64_t* cts, size_t count,
                   uint64_t* out);
+
+/* ---- FFT64 transform (fft_oracle.c): tfhe-rs's own external-product arithmetic ------------------
+ * tfhe-rs (absent from the mount; npm tfhe/node-tfhe 0.8.7) computes the GGSW x GLWE
+ * external product with an f64 FFT over the native 2^64 torus (concrete-fft): the BSK lives in the
+ * Fourier domain as N/2 complex doubles per polynomial, digit polynomials are transformed, multiplied
+ * pointwise, transformed back and rounded to the torus.  Restated here with ONE fixed f64 operation
+ * sequence, which the device kernels (pbs_fft.hip) reproduce bit-for-bit:
+ *   fold + twist   z_j = (a_j + i a_{j+N/2}) * zeta^j, zeta = e^{i pi/N}       (j < M = N/2)
+ *   DFT            Z_k = sum_j z_j e^{+2 pi i jk/M}: three radix-8 passes (M = 512 = 8 x 8 x 8),
+ *                  natural order in and out (layout and per-element operation order: fft_oracle.c)
+ *   BSK            Fourier(BSK) = DFT(twist((double)(int64)bsk)) * 2^-9     (1/M folded in)
+ *   MAC            O_j = sum_r D_r (.) BSK[r][j], r = c*l + lvl in order, 4 fma per complex term
+ *   inverse        z'_j = sum_k O_k e^{-2 pi i jk/M} (same passes, conjugate twiddles), untwist by
+ *                  conj(zeta^j), coefficient j = Re, j + N/2 = Im, rint (ties to even), mod 2^64
+ * Twiddles cos/sin(2 pi t/M) come from fixed series in plain double arithmetic (octant-reduced), so
+ * tables are bit-identical on every host.  The accumulator, LUT, BSK (standard domain) and sample
+ * extraction are native torus values; the LUT is handed over in the Z_p encoding of the NTT engine
+ * (tfhe_hip_lut_*) and mapped back with or_p_to_tor.  Rounding noise of the transform: < 2^-30 of the
+ * torus per PBS (tests/test_fft.py measures it against the exact schoolbook product).
+ * Parity: GPU == this restatement bit-for-bit; vs tfhe-rs "parity unpinned" like the NTT path. */
+typedef struct or_c64 { double re, im; } or_c64;
+/* cos(2 pi t / M), sin(2 pi t / M) for 0 <= t < M (M a multiple of 8), fixed-series evaluation */
+void or_fft_twiddle(uint32_t t, uint32_t M, double* c, double* s);
+/* forward: N real values (exact doubles) -> N/2 complex (natural order) */
+void or_fft_fwd(const double* a, uint32_t N, or_c64* out);
+/* inverse WITHOUT the 1/M factor: N/2 complex -> N doubles (not rounded) */
+void or_fft_inv(const or_c64* in, uint32_t N, double* out);
+/* round(x) mod 2^64 (ties to even) */
+uint64_t or_f64_to_torus(double x);
+/* Fourier BSK: or_bsk_len/N polynomials x N/2 complex, scaled by 2^-log2(N/2) */
+void or_bsk_to_fourier(const or_params* p, const uint64_t* bsk, or_c64* bsk_f);
+/* acc_out: (k+1)*N native torus values.  lut: N values in the Z_p LUT encoding. */
+void or_blind_rotate_fft(const or_params* p, const or_c64* bsk_f, const uint64_t* lwe_in, const uint64_t* lut,
+                         uint64_t* acc_out);
+void or_sample_extract_torus(const or_params* p, const uint64_t* acc, uint64_t* lwe_big_out);
+void or_pbs_batch_fft(const or_params* p, const or_c64* bsk_f, const uint64_t* ksk, const uint64_t* lwe_in, size_t B,
+                      const uint64_t* luts, size_t n_lut, const uint32_t* lut_index, uint64_t* lwe_out, int threads);
+/* exact negacyclic product over Z_2^64 (wrapping): the independent arbiter of the FFT's rounding */
+void or_poly_mul_torus_schoolbook(uint64_t* out, const int64_t* a, const uint64_t* b, uint32_t N);
 
 /* ---- LUT helpers --------------------------------------------------------------------- */
 void or_lut_constant(uint32_t N, uint64_t torus_value, uint64_t* lut); /* gate LUT: every coef = v */

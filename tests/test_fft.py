@@ -1,0 +1,123 @@
+"""FFT64 transform on CPU: the oracle restatement (oracle/fft_oracle.c) against its definition, the
+exact torus product it approximates, and the product's host-side keygen.
+
+The f64 FFT is tfhe-rs's own external-product arithmetic ("tfhe-rs uses an f64 FFT"); the
+reference's exact wrapping product (ml/extensions/rust/src/computations.rs:50-54) is the arbiter of
+its rounding error here.  Device parity (bit-exact against this oracle) is tests/test_gpu_fft.py.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import KEY_SEED
+
+N, M = 1024, 512
+
+
+def _dft_definition(a):
+    """z_j = (a_j + i a_{j+M}) zeta^j, Z_k = sum_j z_j e^{+2 pi i jk/M} in long double-free numpy."""
+    zeta = np.exp(1j * np.pi * np.arange(M) / N)
+    z = (a[:M] + 1j * a[M:]) * zeta
+    return np.fft.ifft(z) * M  # numpy's ifft uses e^{+2 pi i jk/M} / M
+
+
+def test_twiddles_match_libm(oracle_mod):
+    for Mt in (512, 2048):
+        for t in range(0, Mt, 7):
+            c, s = oracle_mod.fft_twiddle(t, Mt)
+            # libm's own argument 2*pi*t/M carries ~1 ulp of rounding: compare at 1.5e-15
+            assert abs(c - math.cos(2 * math.pi * t / Mt)) < 1.5e-15
+            assert abs(s - math.sin(2 * math.pi * t / Mt)) < 1.5e-15
+    # exact symmetry points
+    assert oracle_mod.fft_twiddle(0, 512) == (1.0, 0.0)
+    assert oracle_mod.fft_twiddle(128, 512) == (0.0, 1.0)
+    assert oracle_mod.fft_twiddle(256, 512) == (-1.0, 0.0)
+
+
+def test_forward_matches_definition(oracle_mod):
+    rng = np.random.default_rng(3)
+    for a in (rng.integers(-64, 64, N).astype(np.float64),
+              rng.integers(-2**62, 2**62, N).astype(np.float64)):
+        Z = oracle_mod.fft_fwd(a)[0]
+        ref = _dft_definition(a)
+        assert np.max(np.abs(Z - ref)) <= 1e-12 * np.max(np.abs(ref)) + 1e-9
+
+
+def test_inverse_roundtrip(oracle_mod):
+    rng = np.random.default_rng(4)
+    a = rng.integers(-2**40, 2**40, N).astype(np.float64)
+    back = oracle_mod.fft_inv(oracle_mod.fft_fwd(a))[0] / M
+    assert np.max(np.abs(back - a)) < 1e-3
+
+
+def test_product_vs_exact_torus_schoolbook(oracle_mod):
+    """digit polynomial (|d| <= 64) x uniform torus polynomial: FFT product rounded to the torus stays
+    within 2^28 of the exact wrapping product (2^-36 of the torus)."""
+    rng = np.random.default_rng(5)
+    worst = 0
+    for _ in range(4):
+        d = rng.integers(-64, 65, N)
+        b = rng.integers(0, 2**64, N, dtype=np.uint64)
+        Fb = oracle_mod.fft_fwd(b.view(np.int64).astype(np.float64))[0] * 2.0**-9
+        prod = oracle_mod.fft_inv(oracle_mod.fft_fwd(d.astype(np.float64))[0] * Fb)[0]
+        got = np.array([oracle_mod.f64_to_torus(x) for x in prod], dtype=np.uint64)
+        ref = oracle_mod.poly_mul_torus_schoolbook(d, b)
+        err = np.abs((got - ref).view(np.int64).astype(np.float64))
+        worst = max(worst, float(err.max()))
+    assert worst < 2.0**28, f"FFT product error 2^{math.log2(worst):.1f}"
+
+
+def test_f64_to_torus_rounding(oracle_mod):
+    f = oracle_mod.f64_to_torus
+    assert f(2.5) == 2 and f(3.5) == 4 and f(-2.5) == (1 << 64) - 2  # ties to even
+    assert f(-1.0) == (1 << 64) - 1 and f(0.49) == 0 and f(-0.0) == 0
+    assert f(2.0**64 + 2.0**20) == 2**20
+    assert f(-(2.0**70) + 2.0**30) == 2**30
+    assert f(2.0**63) == 2**63 and f(-(2.0**63)) == 2**63
+
+
+def test_product_keygen_matches_oracle(oracle_mod):
+    """tfhe_hip_keygen on the FFT64 preset: native-torus BSK bit-identical to or_keygen (host code)."""
+    import tfhe_amd
+    p = tfhe_amd.Params.preset(tfhe_amd.PRESET_GATE_FFT)
+    assert p.transform == tfhe_amd.TRANSFORM_FFT64 and p.N == 1024 and p.n == 630
+    ck, sk = tfhe_amd.gen_keys(p, KEY_SEED)
+    ok = oracle_mod.Keys(oracle_mod.params(2), KEY_SEED)
+    assert np.array_equal(sk.bsk, ok.bsk)
+    assert np.array_equal(sk.ksk, ok.ksk)
+    # same secret keys as the NTT preset; the BSKs differ (torus vs Z_p GGSW)
+    ok0 = oracle_mod.Keys(oracle_mod.params(0), KEY_SEED, with_bsk=False, with_ksk=False)
+    assert np.array_equal(ok.lwe_key, ok0.lwe_key) and np.array_equal(ok.glwe_key, ok0.glwe_key)
+
+
+@pytest.fixture(scope="module")
+def fft_keys(oracle_mod):
+    return oracle_mod.Keys(oracle_mod.params(2), KEY_SEED)
+
+
+def test_oracle_pbs_decrypts(oracle_mod, fft_keys):
+    prm = oracle_mod.params(2)
+    rng = np.random.default_rng(6)
+    bits = rng.integers(0, 2, 32)
+    cts = fft_keys.encrypt([oracle_mod.encode_bit(int(b)) for b in bits], seed=0xC0FFEE21)
+    out = oracle_mod.pbs_batch(prm, fft_keys, cts, oracle_mod.lut_constant(N, oracle_mod.MU)[None])
+    ph = fft_keys.phase(out)
+    assert [oracle_mod.decode_bit(int(x)) for x in ph] == [int(b) for b in bits]
+    err = [((int(x) - oracle_mod.encode_bit(int(b))) + 2**63) % 2**64 - 2**63 for x, b in zip(ph, bits)]
+    assert max(abs(e) for e in err) < 2**60  # 1/16 of the torus: inside the 1/8 gate margin
+
+
+def test_oracle_blind_rotate_lut_table(oracle_mod, fft_keys):
+    """decrypt(BR(m)) == f(m) for every message of an 8-valued table (biometrics main.rs:65-77)."""
+    prm = oracle_mod.params(2)
+    delta = (1 << 63) // 8
+    table = [(3 * m + 1) % 8 for m in range(8)]
+    lut = oracle_mod.lut_from_table(N, 8, table, delta)
+    msgs = [m * delta for m in range(8)]
+    cts = fft_keys.encrypt(msgs, seed=0xC0FFEE22)
+    for m in range(8):
+        acc = oracle_mod.blind_rotate_fft(prm, fft_keys, cts[m], lut)
+        big = oracle_mod.sample_extract_torus(prm, acc)
+        ph = fft_keys.phase(big, fft_keys.glwe_key, N)[0]
+        assert ((int(ph) + delta // 2) // delta) % 16 == table[m]

@@ -1,0 +1,111 @@
+"""GPU parity of the FFT64 transform (pbs_fft.hip) against oracle/fft_oracle.c, bit-exact, through the
+C ABI: the transform itself, the blind rotation accumulators, full PBS (multi-LUT, ragged batches that
+leave padding waves in the last workgroup), gate bootstrapping, and a 4096 batch by decryption plus a
+sampled bit-exact subset.
+"""
+import numpy as np
+import pytest
+
+from conftest import KEY_SEED
+
+import tfhe_amd
+
+pytestmark = pytest.mark.gpu
+N = 1024
+
+
+@pytest.fixture(scope="module")
+def fft_keys():
+    return tfhe_amd.gen_keys(tfhe_amd.Params.preset(tfhe_amd.PRESET_GATE_FFT), KEY_SEED)
+
+
+@pytest.fixture(scope="module")
+def fft_engine(fft_keys):
+    ck, sk = fft_keys
+    eng = tfhe_amd.Engine(ck.params, 0)
+    eng.load_keys(sk)
+    yield eng
+    eng.close()
+
+
+@pytest.fixture(scope="module")
+def fft_params(oracle_mod):
+    return oracle_mod.params(2)
+
+
+@pytest.fixture(scope="module")
+def fft_okeys(oracle_mod, fft_params):
+    return oracle_mod.Keys(fft_params, KEY_SEED)
+
+
+def test_fft_forward_inverse_bitexact(fft_engine, oracle_mod):
+    rng = np.random.default_rng(31)
+    x = rng.integers(0, 2**64, size=(19, N), dtype=np.uint64)
+    x[0] = 0
+    x[1] = np.uint64(2**63)                       # most negative int64
+    x[2] = rng.integers(0, 129, N).astype(np.uint64) - np.uint64(64)  # digit-sized values
+    Z = fft_engine.fft_fwd(x)
+    Zo = oracle_mod.fft_fwd(x.view(np.int64).astype(np.float64))
+    assert np.array_equal(Z.view(np.uint64), Zo.view(np.uint64)), "forward FFT differs from the oracle"
+    y = fft_engine.fft_inv(Zo)
+    yo = oracle_mod.fft_inv(Zo)
+    assert np.array_equal(y.view(np.uint64), yo.view(np.uint64)), "inverse FFT differs from the oracle"
+    # and it is a transform: inverse(forward(x)) / M == x up to f64 rounding (2^-40 of 2^63 values)
+    assert np.max(np.abs(y[3] / 512 - x[3].view(np.int64).astype(np.float64))) <= 2.0**23
+
+
+def test_blind_rotate_accumulators_bitexact(fft_engine, fft_keys, oracle_mod, fft_params, fft_okeys):
+    ck, _ = fft_keys
+    rng = np.random.default_rng(32)
+    cts = ck.encrypt_torus(rng.integers(0, 2**63, 5, dtype=np.uint64), seed=0xC0FFEE31)
+    luts = np.stack([oracle_mod.lut_from_table(N, 8, [(m * 5 + 3) % 8 for m in range(8)], (1 << 63) // 8),
+                     oracle_mod.lut_constant(N, 1 << 61)])
+    idx = np.array([0, 1, 0, 1, 1], dtype=np.uint32)
+    acc = fft_engine.blind_rotate(cts, luts, idx)
+    for i in range(5):
+        ref = oracle_mod.blind_rotate_fft(fft_params, fft_okeys, cts[i], luts[idx[i]])
+        assert np.array_equal(acc[i], ref), f"accumulator {i} differs from the oracle"
+    big = fft_engine.sample_extract(acc)
+    for i in range(5):
+        assert np.array_equal(big[i], oracle_mod.sample_extract_torus(fft_params, acc[i]))
+
+
+@pytest.mark.parametrize("B", [1, 13, 37])
+def test_pbs_bitexact_ragged(fft_engine, fft_keys, oracle_mod, fft_params, fft_okeys, B):
+    ck, _ = fft_keys
+    rng = np.random.default_rng(33 + B)
+    msgs = rng.integers(0, 8, B).astype(np.uint64) * np.uint64((1 << 63) // 8)
+    cts = ck.encrypt_torus(msgs, seed=0xC0FFEE40 + B)
+    luts = np.stack([oracle_mod.lut_from_table(N, 8, [(m + s) % 8 for m in range(8)], (1 << 63) // 8)
+                     for s in range(3)])
+    idx = rng.integers(0, 3, B).astype(np.uint32)
+    out = fft_engine.pbs(cts, luts, idx)
+    ref = oracle_mod.pbs_batch_fft(fft_params, fft_okeys, cts, luts, idx)
+    assert np.array_equal(out, ref)
+    m = np.array([int(v) for v in msgs]) // ((1 << 63) // 8)
+    dec = [((int(p) + (1 << 59)) >> 60) % 16 for p in ck.phase(out)]
+    assert dec == [int((mm + idx[q]) % 8) for q, mm in enumerate(m)]
+
+
+def test_gates_on_fft_engine(fft_engine, fft_keys):
+    ck, _ = fft_keys
+    rng = np.random.default_rng(34)
+    a, b = rng.integers(0, 2, 64).astype(bool), rng.integers(0, 2, 64).astype(bool)
+    ca, cb = ck.encrypt_bool(a, seed=0xC0FFEE51), ck.encrypt_bool(b, seed=0xC0FFEE52)
+    assert np.array_equal(ck.decrypt_bool(fft_engine.nand(ca, cb)), ~(a & b))
+    x = tfhe_amd.FheBool(fft_engine, ca)
+    y = tfhe_amd.FheBool(fft_engine, cb)
+    assert np.array_equal((x ^ y).decrypt(ck), a ^ b)
+    assert np.array_equal((x & y).decrypt(ck), a & b)
+
+
+def test_batch_4096_decrypts_and_sampled_bitexact(fft_engine, fft_keys, oracle_mod, fft_params, fft_okeys):
+    ck, _ = fft_keys
+    rng = np.random.default_rng(35)
+    bits = rng.integers(0, 2, 4096).astype(bool)
+    cts = ck.encrypt_bool(bits, seed=0xC0FFEE03)
+    out = fft_engine.pbs(cts, fft_engine.gate_lut())
+    assert np.array_equal(ck.decrypt_bool(out), bits)
+    sample = np.r_[0:16, 4080:4096]
+    ref = oracle_mod.pbs_batch_fft(fft_params, fft_okeys, cts[sample], oracle_mod.lut_constant(N, 1 << 61)[None])
+    assert np.array_equal(out[sample], ref)

@@ -25,7 +25,8 @@ import numpy as np
 
 __all__ = [
     "Params", "TfheError", "lib", "ClientKey", "ServerKey", "gen_keys", "Engine", "FheBool", "FheUint8",
-    "PRESET_GATE", "PRESET_FHEVM", "MU", "encode_bool", "decode_bool",
+    "PRESET_GATE", "PRESET_FHEVM", "PRESET_GATE_FFT", "TRANSFORM_NTT", "TRANSFORM_FFT64", "MU", "encode_bool",
+    "decode_bool",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -33,6 +34,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TFHE_HIP_LIB") or os.path.join(_HERE, "libtfhe_hip.so")
 PRESET_GATE = 0
 PRESET_FHEVM = 1
+PRESET_GATE_FFT = 2  # P-GATE on the FFT64 transform (tfhe-rs's f64-FFT external product)
+TRANSFORM_NTT = 0
+TRANSFORM_FFT64 = 1
 MU = 1 << 61  # gate encoding: true = +1/8, false = -1/8 of the 2^64 torus
 _U64P = ctypes.POINTER(ctypes.c_uint64)
 _U32P = ctypes.POINTER(ctypes.c_uint32)
@@ -54,7 +58,7 @@ class Params(ctypes.Structure):
         ("pbs_base_log", ctypes.c_uint32), ("pbs_level", ctypes.c_uint32),
         ("ks_base_log", ctypes.c_uint32), ("ks_level", ctypes.c_uint32),
         ("lwe_noise_log2", ctypes.c_int32), ("glwe_noise_log2", ctypes.c_int32),
-        ("order", ctypes.c_uint32),
+        ("order", ctypes.c_uint32), ("transform", ctypes.c_uint32),
     ]
 
     @classmethod
@@ -87,7 +91,8 @@ ABI_SYMBOLS = (
     "tfhe_hip_pks_pack_async", "tfhe_hip_pks_packed_words", "tfhe_hip_pks_compress", "tfhe_hip_pks_extract",
     "tfhe_hip_glwe_phase", "tfhe_hip_sns_params_preset", "tfhe_hip_sns_bsk_len", "tfhe_hip_sns_keygen",
     "tfhe_hip_sns_create", "tfhe_hip_sns_destroy", "tfhe_hip_sns_load_key", "tfhe_hip_sns_squash",
-    "tfhe_hip_sns_squash_async", "tfhe_hip_sns_blind_rotate", "tfhe_hip_sns_phase",
+    "tfhe_hip_sns_squash_async", "tfhe_hip_sns_blind_rotate", "tfhe_hip_sns_phase", "tfhe_hip_fft_fwd",
+    "tfhe_hip_fft_inv",
 )
 
 # P-FHEVM modulus-switch noise reduction key (include/tfhe_hip.h TFHE_HIP_MS_FHEVM_*)
@@ -138,6 +143,8 @@ def lib():
         L.tfhe_hip_load_keys_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                                 ctypes.c_size_t]
         L.tfhe_hip_pbs.argtypes = [ctypes.c_void_p, _U64P, ctypes.c_size_t, _U64P, ctypes.c_size_t, _U32P, _U64P]
+        L.tfhe_hip_fft_fwd.argtypes = [ctypes.c_void_p, _U64P, ctypes.c_size_t, ctypes.c_void_p]
+        L.tfhe_hip_fft_inv.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         L.tfhe_hip_pbs_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                          ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.tfhe_hip_blind_rotate.argtypes = [ctypes.c_void_p, _U64P, ctypes.c_size_t, _U64P, ctypes.c_size_t, _U32P,
@@ -440,6 +447,21 @@ class Engine:
         x = _c_u64(polys).copy()
         _check(lib().tfhe_hip_ntt_inv(self._h, _u64(x), x.size // self.params.N))
         return x
+
+    def fft_fwd(self, polys: np.ndarray) -> np.ndarray:
+        """FFT64 ctx: N torus values (read as int64) per polynomial -> N/2 complex128, natural order."""
+        x = _c_u64(polys).reshape(-1, self.params.N)
+        out = np.zeros((x.shape[0], self.params.N // 2), dtype=np.complex128)
+        _check(lib().tfhe_hip_fft_fwd(self._h, _u64(x), x.shape[0], ctypes.c_void_p(out.ctypes.data)))
+        return out
+
+    def fft_inv(self, spec: np.ndarray) -> np.ndarray:
+        """FFT64 ctx: N/2 complex -> N doubles (no 1/M, no rounding)."""
+        z = np.ascontiguousarray(spec, dtype=np.complex128).reshape(-1, self.params.N // 2)
+        out = np.zeros((z.shape[0], self.params.N), dtype=np.float64)
+        _check(lib().tfhe_hip_fft_inv(self._h, ctypes.c_void_p(z.ctypes.data), z.shape[0],
+                                      ctypes.c_void_p(out.ctypes.data)))
+        return out
 
     def nand(self, c1: np.ndarray, c2: np.ndarray) -> np.ndarray:
         dim = self.params.n + 1

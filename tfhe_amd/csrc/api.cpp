@@ -42,7 +42,7 @@ int fail(int code, const char* fmt, ...) {
 bool params_valid(const tfhe_params* p) {
   return p && p->n > 0 && p->k > 0 && p->N >= 32 && (p->N & (p->N - 1)) == 0 && p->pbs_level > 0 &&
          p->pbs_base_log > 0 && p->pbs_base_log * p->pbs_level < 64 && p->ks_level > 0 && p->ks_base_log > 0 &&
-         p->ks_base_log * p->ks_level < 64;
+         p->ks_base_log * p->ks_level < 64 && p->transform <= TFHE_HIP_TRANSFORM_FFT64;
 }
 
 // The device kernels of this build: P-GATE shape (k=1, N=1024, PBS 7x3, KS 2x8, PBS then KS).
@@ -52,8 +52,10 @@ bool params_on_device(const tfhe_params* p) {
                     p->ks_level == 8 && p->order == 0;
   const bool fhevm = p->k == 1 && p->N == 2048 && p->pbs_base_log == 23 && p->pbs_level == 1 &&
                      p->ks_base_log == 4 && p->ks_level == 4 && p->order == 1;
-  return gate || fhevm;
+  return gate || (fhevm && p->transform == TFHE_HIP_TRANSFORM_NTT);
 }
+
+bool is_fft(const tfhe_params& p) { return p.transform == TFHE_HIP_TRANSFORM_FFT64; }
 
 // canonical psi: primitive 2N-th root of unity with psi^(2N/64) = 8 (generator 7)
 u64 canonical_psi(uint32_t N) {
@@ -158,6 +160,9 @@ uint32_t io_dim(const tfhe_params& p) { return p.order == 0 ? p.n : p.k * p.N; }
 
 hipError_t launch_br(tfhe_ctx* c, const u64* in, size_t B, const u64* luts, const u32* idx, size_t n_lut, u64* out_big,
                      u64* out_acc, hipStream_t s) {
+  if (is_fft(c->p))
+    return tfhe::launch_blind_rotate_fft(in, B, (int)c->p.n, luts, idx, (int)n_lut, (const double*)c->d_bsk,
+                                         (const double*)c->d_tw, out_big, out_acc, s);
   if (c->p.N == 2048)
     return tfhe::launch_blind_rotate_2048(in, B, (int)c->p.n, luts, idx, (int)n_lut, c->d_bsk, c->d_tw, out_big, out_acc,
                                           s, c->lat_max);
@@ -252,11 +257,15 @@ int tfhe_hip_params_preset(int preset, tfhe_params* o) {
   if (!o) return fail(TFHE_HIP_EINVAL, "null params");
   memset(o, 0, sizeof(*o));
   if (preset == TFHE_HIP_PRESET_GATE) {
-    *o = tfhe_params{630, 1, 1024, 7, 3, 2, 8, -15, -25, 0};
+    *o = tfhe_params{630, 1, 1024, 7, 3, 2, 8, -15, -25, 0, TFHE_HIP_TRANSFORM_NTT};
     return 0;
   }
   if (preset == TFHE_HIP_PRESET_FHEVM) {
-    *o = tfhe_params{918, 1, 2048, 23, 1, 4, 4, -19, -47, 1};
+    *o = tfhe_params{918, 1, 2048, 23, 1, 4, 4, -19, -47, 1, TFHE_HIP_TRANSFORM_NTT};
+    return 0;
+  }
+  if (preset == TFHE_HIP_PRESET_GATE_FFT) {
+    *o = tfhe_params{630, 1, 1024, 7, 3, 2, 8, -15, -25, 0, TFHE_HIP_TRANSFORM_FFT64};
     return 0;
   }
   return fail(TFHE_HIP_EINVAL, "unknown preset %d", preset);
@@ -325,10 +334,10 @@ int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out) {
   if (!params_valid(p)) return fail(TFHE_HIP_EINVAL, "create: invalid parameters");
   if (!params_on_device(p))
     return fail(TFHE_HIP_EUNSUPPORTED,
-                "create: device kernels of this build cover P-GATE (k=1, N=1024, PBS 7x3, KS 2x8, PBS->KS) and "
-                "P-FHEVM (k=1, N=2048, PBS 23x1, KS 4x4, KS->PBS); got "
-                "k=%u N=%u pbs %ux%u ks %ux%u order %u",
-                p->k, p->N, p->pbs_base_log, p->pbs_level, p->ks_base_log, p->ks_level, p->order);
+                "create: device kernels of this build cover P-GATE (k=1, N=1024, PBS 7x3, KS 2x8, PBS->KS; NTT or "
+                "FFT64) and P-FHEVM (k=1, N=2048, PBS 23x1, KS 4x4, KS->PBS; NTT); got "
+                "k=%u N=%u pbs %ux%u ks %ux%u order %u transform %u",
+                p->k, p->N, p->pbs_base_log, p->pbs_level, p->ks_base_log, p->ks_level, p->order, p->transform);
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return fail(TFHE_HIP_EINVAL, "create: device %d of %d", device, ndev);
@@ -343,8 +352,19 @@ int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out) {
   };
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail(TFHE_HIP_EDEVICE, "create: hipStreamCreate failed"));
-  // twiddle tables of the device NTT layout (pbs_kernels.hip: make_ntt_tables)
   using namespace tfhe;
+  if (is_fft(*p)) {  // FFT64: twist / pass tables (pbs_fft.hip: make_fft_tables); no latency kernel
+    c->lat_max = 0;
+    std::vector<double> tw(fft_tables_len());
+    make_fft_tables(tw.data());
+    if (hipMalloc(&c->d_tw, tw.size() * 8) != hipSuccess)
+      return cleanup(fail(TFHE_HIP_ENOMEM, "create: twiddle allocation failed"));
+    if (hipMemcpy(c->d_tw, tw.data(), tw.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+      return cleanup(fail(TFHE_HIP_EDEVICE, "create: twiddle upload failed"));
+    *out = c;
+    return 0;
+  }
+  // twiddle tables of the device NTT layout (pbs_kernels.hip: make_ntt_tables)
   const uint32_t N = p->N;
   std::vector<u64> tw(N == 2048 ? ntt2048_tables_len() : 4 * N);
   if (N == 2048) make_ntt2048_tables(canonical_psi(N), tw.data());
@@ -402,7 +422,9 @@ static int load_keys_impl(tfhe_ctx* c, const uint64_t* bsk, size_t bsk_len, cons
     tmp = (void*)bsk;
   }
   const size_t polys = bsk_len / c->p.N;
-  if (c->p.N == 2048)
+  if (is_fft(c->p))
+    HIP_TRY(tfhe::launch_bsk_to_fourier((const u64*)tmp, (double*)c->d_bsk, polys, (const double*)c->d_tw, c->stream));
+  else if (c->p.N == 2048)
     HIP_TRY(tfhe::launch_bsk_to_ntt_2048((const u64*)tmp, c->d_bsk, polys, c->d_tw, c->ninv, c->stream));
   else
     HIP_TRY(tfhe::launch_bsk_to_ntt((const u64*)tmp, c->d_bsk, (int)(polys / 12), c->d_tw, c->ninv, c->stream));
@@ -526,7 +548,8 @@ int tfhe_hip_sample_extract(tfhe_ctx* c, const uint64_t* acc, size_t B, uint64_t
   std::vector<void*> d;
   int rc = stage(c, {{acc, B * acc_len * 8}}, d, B * big * 8);
   if (rc) return rc;
-  if (c->p.N == 2048) HIP_TRY(tfhe::launch_sample_extract_2048((const u64*)d[0], B, (u64*)d[1], c->stream));
+  if (is_fft(c->p)) HIP_TRY(tfhe::launch_sample_extract_torus((const u64*)d[0], B, (u64*)d[1], c->stream));
+  else if (c->p.N == 2048) HIP_TRY(tfhe::launch_sample_extract_2048((const u64*)d[0], B, (u64*)d[1], c->stream));
   else HIP_TRY(tfhe::launch_sample_extract((const u64*)d[0], B, (u64*)d[1], c->stream));
   HIP_TRY(hipMemcpyAsync(out, d[1], B * big * 8, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -551,6 +574,7 @@ int tfhe_hip_keyswitch(tfhe_ctx* c, const uint64_t* in, size_t B, uint64_t* out)
 
 static int ntt_impl(tfhe_ctx* c, uint64_t* polys, size_t count, bool inverse) {
   if (!c || (count && !polys)) return fail(TFHE_HIP_EINVAL, "ntt: bad arguments");
+  if (is_fft(c->p)) return fail(TFHE_HIP_EUNSUPPORTED, "ntt: this ctx runs the FFT64 transform (tfhe_hip_fft_*)");
   if (count == 0) return 0;
   for (size_t i = 0; i < count * c->p.N; i++)
     if (polys[i] >= tfhe::GL_P) return fail(TFHE_HIP_EINVAL, "ntt: value at %zu not reduced mod p", i);
@@ -573,6 +597,38 @@ static int ntt_impl(tfhe_ctx* c, uint64_t* polys, size_t count, bool inverse) {
 }
 
 int tfhe_hip_ntt_fwd(tfhe_ctx* c, uint64_t* polys, size_t count) { return ntt_impl(c, polys, count, false); }
+
+int tfhe_hip_fft_fwd(tfhe_ctx* c, const uint64_t* polys, size_t count, double* out) {
+  if (!c || (count && (!polys || !out))) return fail(TFHE_HIP_EINVAL, "fft_fwd: bad arguments");
+  if (!is_fft(c->p)) return fail(TFHE_HIP_EUNSUPPORTED, "fft_fwd: ctx transform is not FFT64");
+  if (count == 0) return 0;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  const size_t bytes = count * c->p.N * 8;
+  std::vector<void*> d;
+  int rc = stage(c, {{polys, bytes}}, d, bytes);
+  if (rc) return rc;
+  HIP_TRY(tfhe::launch_fft_fwd((const u64*)d[0], count, (double*)d[1], (const double*)c->d_tw, c->stream));
+  HIP_TRY(hipMemcpyAsync(out, d[1], bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int tfhe_hip_fft_inv(tfhe_ctx* c, const double* in, size_t count, double* out) {
+  if (!c || (count && (!in || !out))) return fail(TFHE_HIP_EINVAL, "fft_inv: bad arguments");
+  if (!is_fft(c->p)) return fail(TFHE_HIP_EUNSUPPORTED, "fft_inv: ctx transform is not FFT64");
+  if (count == 0) return 0;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  const size_t bytes = count * c->p.N * 8;
+  std::vector<void*> d;
+  int rc = stage(c, {{in, bytes}}, d, bytes);
+  if (rc) return rc;
+  HIP_TRY(tfhe::launch_fft_inv((const double*)d[0], count, (double*)d[1], (const double*)c->d_tw, c->stream));
+  HIP_TRY(hipMemcpyAsync(out, d[1], bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
 int tfhe_hip_ntt_inv(tfhe_ctx* c, uint64_t* polys, size_t count) { return ntt_impl(c, polys, count, true); }
 
 int tfhe_hip_nand(tfhe_ctx* c, const uint64_t* c1, const uint64_t* c2, size_t B, uint64_t* out) {

@@ -156,6 +156,9 @@ static void glwe_zero(const tfhe_params& p, const uint64_t* S, ChaCha& r, uint64
   }
 }
 
+static void glwe_native(uint32_t k, uint32_t N, const uint64_t* key, int32_t noise_log2, ChaCha& r, const uint64_t* m,
+                        uint64_t* out);
+
 static void lwe_one(uint32_t dim, const uint64_t* key, int32_t noise_log2, ChaCha& r, uint64_t m, uint64_t* out) {
   uint64_t acc = 0;
   for (uint32_t i = 0; i < dim; i++) {
@@ -188,10 +191,13 @@ void server_keygen(const tfhe_params& p, uint64_t seed, const uint64_t* lwe_key,
       for (uint32_t c = 0; c <= p.k; c++)
         for (uint32_t l = 0; l < p.pbs_level; l++) {
           uint64_t* out = bsk + per_i * i + row * (c * p.pbs_level + l);
-          glwe_zero(p, glwe_key, r, out);
-          if (lwe_key[i]) {
-            const uint64_t g = 1ull << (64 - p.pbs_base_log * (l + 1));
-            out[(size_t)c * p.N] = padd(out[(size_t)c * p.N], g);
+          const uint64_t g = 1ull << (64 - p.pbs_base_log * (l + 1));
+          if (p.transform == TFHE_HIP_TRANSFORM_FFT64) {  // native-torus GGSW
+            glwe_native(p.k, p.N, glwe_key, p.glwe_noise_log2, r, nullptr, out);
+            if (lwe_key[i]) out[(size_t)c * p.N] += g;
+          } else {
+            glwe_zero(p, glwe_key, r, out);
+            if (lwe_key[i]) out[(size_t)c * p.N] = padd(out[(size_t)c * p.N], g);
           }
         }
     });

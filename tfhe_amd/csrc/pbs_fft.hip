@@ -1,0 +1,518 @@
+// pbs_fft.hip — the FFT64 transform of the PBS hot path for gfx950 (P-GATE shape: N = 1024, k = 1,
+// PBS 2^7 x 3): the external product computed the way tfhe-rs computes it, with an f64 negacyclic
+// FFT over the native 2^64 torus, instead of the Goldilocks NTT of pbs_kernels.hip.
+//
+// Why: MI355X runs f64 add / mul / fma at the full VALU rate (~6 cycles per wave-instruction, the
+// same as a 32-bit integer op, tools/microbench/f64_rates.hip), and a complex radix-2 butterfly is ~8
+// such instructions where a Goldilocks butterfly is ~30 integer ones.  Same BSK bytes (N/2 complex
+// doubles = N u64 per polynomial), same workgroup structure (8 ciphertexts walk the CMUX loop in
+// lockstep, the BSK level-step chunks streamed once per workgroup into LDS by global_load_lds,
+// double-buffered).
+//
+// Arithmetic (one fixed f64 operation sequence, restated in oracle/fft_oracle.c, which this file
+// reproduces bit-for-bit — every product is written as an explicit fma or a lone multiply, and
+// contraction is off for the whole file):
+//   fold + twist  z_j = (a_j + i a_{j+512}) * zeta^j,   zeta = e^{i pi / 1024}
+//   DFT           Z_k = sum_j z_j e^{+2 pi i jk / 512}: 3 radix-8 passes over the wave's 64 lanes
+//                 x 8 registers, natural order in and out (lane L, slot e <-> index L + 64 e), two
+//                 LDS transposes (row stride 72 complex, low-3-bit XOR swizzle: conflict-free for
+//                 both the ds_write_b128 and the ds_read_b128 patterns)
+//   MAC           O_j += D_r (.) BSK_i[r][j], 4 fma per complex, r = c*3 + l ascending
+//   inverse       conjugate passes, untwist by conj(zeta^j), rint, mod 2^64, add to the accumulator
+// Coefficient 64 e + L of a u64 register polynomial (slot e of lane L, e < 16) meets coefficient
+// 64 (e + 8) + L in the same lane, so folding and unfolding move no data.
+#pragma clang fp contract(off)
+#include <hip/hip_runtime.h>
+
+#include "gl64.h"
+#include "ntt1024.h"
+#include "pbs_kernels.h"
+
+namespace tfhe {
+namespace fftk {
+
+constexpr int M = 512;
+constexpr int TS = 72;            // transpose row stride (complex)
+constexpr int T_C64 = 8 * TS;     // per-wave transpose scratch (9,216 B; also holds 1024 u64)
+constexpr int TW_TWIST = 0, TW_A = 512, TW_B = 1024, TW_C64 = 1536;  // table offsets (complex)
+constexpr double SQRT1_2 = 0.70710678118654752440;
+
+__device__ __forceinline__ int swz(int c) { return (c & 56) | ((c & 7) ^ (c >> 3)); }
+
+// z * w (INV: z * conj(w)), the oracle's cmul(z, w.re, +-w.im)
+template <bool INV>
+__device__ __forceinline__ void cmul(double& re, double& im, double2 w) {
+  const double p = re, q = im;
+  if (!INV) {
+    re = __builtin_fma(p, w.x, -(q * w.y));
+    im = __builtin_fma(p, w.y, q * w.x);
+  } else {
+    re = __builtin_fma(p, w.x, q * w.y);
+    im = __builtin_fma(p, -w.y, q * w.x);
+  }
+}
+
+// t * e^{+-i pi j / 4} (oracle w8)
+template <bool INV, int J>
+__device__ __forceinline__ void w8(double& re, double& im) {
+  const double p = re, q = im;
+  if (J == 1) {
+    if (!INV) { re = (p - q) * SQRT1_2; im = (p + q) * SQRT1_2; }
+    else { re = (p + q) * SQRT1_2; im = (q - p) * SQRT1_2; }
+  } else if (J == 2) {
+    if (!INV) { re = -q; im = p; }
+    else { re = q; im = -p; }
+  } else {
+    if (!INV) { re = -((p + q) * SQRT1_2); im = (p - q) * SQRT1_2; }
+    else { re = (q - p) * SQRT1_2; im = -((p + q) * SQRT1_2); }
+  }
+}
+
+// 8-point DFT in registers, natural order in and out (radix-2 DIF, bit-reversal by renaming)
+template <bool INV>
+__device__ __forceinline__ void dft8(double (&xr)[8], double (&xi)[8]) {
+  double yr[8], yi[8];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    yr[j] = xr[j] + xr[j + 4];
+    yi[j] = xi[j] + xi[j + 4];
+    yr[j + 4] = xr[j] - xr[j + 4];
+    yi[j + 4] = xi[j] - xi[j + 4];
+  }
+  w8<INV, 1>(yr[5], yi[5]);
+  w8<INV, 2>(yr[6], yi[6]);
+  w8<INV, 3>(yr[7], yi[7]);
+  double zr[8], zi[8];
+#pragma unroll
+  for (int h = 0; h < 8; h += 4)
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      zr[h + j] = yr[h + j] + yr[h + j + 2];
+      zi[h + j] = yi[h + j] + yi[h + j + 2];
+      zr[h + j + 2] = yr[h + j] - yr[h + j + 2];
+      zi[h + j + 2] = yi[h + j] - yi[h + j + 2];
+    }
+  w8<INV, 2>(zr[3], zi[3]);
+  w8<INV, 2>(zr[7], zi[7]);
+  // u[g] = z[g] + z[g+1], u[g+1] = z[g] - z[g+1];  X[k] = u[brv3(k)]
+  xr[0] = zr[0] + zr[1]; xi[0] = zi[0] + zi[1];
+  xr[4] = zr[0] - zr[1]; xi[4] = zi[0] - zi[1];
+  xr[2] = zr[2] + zr[3]; xi[2] = zi[2] + zi[3];
+  xr[6] = zr[2] - zr[3]; xi[6] = zi[2] - zi[3];
+  xr[1] = zr[4] + zr[5]; xi[1] = zi[4] + zi[5];
+  xr[5] = zr[4] - zr[5]; xi[5] = zi[4] - zi[5];
+  xr[3] = zr[6] + zr[7]; xi[3] = zi[6] + zi[7];
+  xr[7] = zr[6] - zr[7]; xi[7] = zi[6] - zi[7];
+}
+
+// the 512-point DFT of the wavefront's complex vector (lane L, slot e <-> index L + 64 e)
+template <bool INV>
+__device__ __forceinline__ void dft512(double (&xr)[8], double (&xi)[8], double2* T, int lane, const double2* tw) {
+  dft8<INV>(xr, xi);
+#pragma unroll
+  for (int e = 1; e < 8; e++) cmul<INV>(xr[e], xi[e], tw[TW_A + 64 * e + lane]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[e * TS + swz(lane)] = make_double2(xr[e], xi[e]);
+  wave_lds_sync();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[(lane >> 3) * TS + swz((lane & 7) + 8 * e)];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  wave_lds_sync();
+  dft8<INV>(xr, xi);
+#pragma unroll
+  for (int e = 1; e < 8; e++) cmul<INV>(xr[e], xi[e], tw[TW_B + 64 * e + lane]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[e * TS + swz(lane)] = make_double2(xr[e], xi[e]);
+  wave_lds_sync();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[(lane >> 3) * TS + swz(e + 8 * (lane & 7))];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  wave_lds_sync();
+  dft8<INV>(xr, xi);
+}
+
+// (double)(int64)x, correctly rounded: exact hi * 2^32 plus exact lo, one rounding
+__device__ __forceinline__ double i64_to_f64(u64 x) {
+  return __builtin_fma((double)(int)(x >> 32), 0x1p32, (double)(u32)x);
+}
+
+// rint(x) mod 2^64 (every step after the rint is exact)
+__device__ __forceinline__ u64 f64_to_torus(double x) {
+  const double t = __builtin_rint(x);
+  const double h = __builtin_floor(t * 0x1p-32);
+  const double l = __builtin_fma(-h, 0x1p32, t);
+  const double hh = __builtin_floor(h * 0x1p-32);
+  const double hm = __builtin_fma(-hh, 0x1p32, h);
+  return ((u64)(u32)hm << 32) | (u64)(u32)l;
+}
+
+// forward transform of a real polynomial held as 16 doubles per lane (slot e <-> coefficient 64 e + L)
+__device__ __forceinline__ void fft_fwd_real(const double (&a)[16], double (&xr)[8], double (&xi)[8], double2* T,
+                                             int lane, const double2* tw) {
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    xr[e] = a[e];
+    xi[e] = a[e + 8];
+    cmul<false>(xr[e], xi[e], tw[TW_TWIST + 64 * e + lane]);
+  }
+  dft512<false>(xr, xi, T, lane, tw);
+}
+
+// inverse transform (no 1/M) + untwist: slot e -> coefficient 64 e + L (re), 64 (e + 8) + L (im)
+__device__ __forceinline__ void fft_inv_real(double (&xr)[8], double (&xi)[8], double2* T, int lane,
+                                             const double2* tw) {
+  dft512<true>(xr, xi, T, lane, tw);
+#pragma unroll
+  for (int e = 0; e < 8; e++) cmul<true>(xr[e], xi[e], tw[TW_TWIST + 64 * e + lane]);
+}
+
+__device__ __forceinline__ int ms2048(u64 x) { return (int)((((x >> 52) + 1) >> 1) & 2047u); }
+
+// (X^s * v)[idx] for a negacyclic length-1024 torus polynomial, s in [0, 2048)
+__device__ __forceinline__ u64 rot_read_torus(const u64* v, int idx, int s) {
+  int d = idx - s;
+  bool neg = false;
+  if (d < 0) { d += N1K; neg = !neg; }
+  if (d < 0) { d += N1K; neg = !neg; }
+  const u64 x = v[d];
+  return neg ? 0 - x : x;
+}
+
+// tfhe-rs SignedDecomposer 2^7 x 3 on a torus value: bytes (d + 64), byte l = level l (0 = MSB)
+__device__ __forceinline__ u32 decomp_7x3_t(u64 x) {
+  u32 state = (u32)(((x >> 42) + 1) >> 1) & 0x1FFFFFu;
+  u32 packed = 0;
+#pragma unroll
+  for (int l = 2; l >= 0; l--) {
+    const u32 res = state & 127u;
+    state >>= 7;
+    const u32 carry = ((((res - 1u) | state) & res) >> 6) & 1u;
+    state += carry;
+    const int d = (int)res - (int)(carry << 7);
+    packed |= (u32)(d + 64) << (8 * l);
+  }
+  return packed;
+}
+
+// ---------------------------------------------------------------------------------------------
+// BSK conversion: one wavefront per polynomial; [i][r][j] order kept, 512 complex natural, x 2^-9
+__global__ __launch_bounds__(64) void bsk_to_fourier_kernel(const u64* __restrict__ bsk_std,
+                                                            double2* __restrict__ bsk_f,
+                                                            const double2* __restrict__ tw) {
+  __shared__ __attribute__((aligned(16))) double2 T[T_C64];
+  const int lane = threadIdx.x;
+  const size_t q = blockIdx.x;
+  const u64* src = bsk_std + q * N1K;
+  double a[16], xr[8], xi[8];
+#pragma unroll
+  for (int e = 0; e < 16; e++) a[e] = i64_to_f64(src[64 * e + lane]);
+  fft_fwd_real(a, xr, xi, T, lane, tw);
+  double2* dst = bsk_f + q * M;
+#pragma unroll
+  for (int e = 0; e < 8; e++) dst[64 * e + lane] = make_double2(xr[e] * 0x1p-9, xi[e] * 0x1p-9);
+}
+
+// natural-order transforms for the parity tests (one wavefront per polynomial)
+__global__ __launch_bounds__(64) void fft_fwd_kernel(const u64* __restrict__ in, double2* __restrict__ out,
+                                                     const double2* __restrict__ tw) {
+  __shared__ __attribute__((aligned(16))) double2 T[T_C64];
+  const int lane = threadIdx.x;
+  const u64* src = in + (size_t)blockIdx.x * N1K;
+  double a[16], xr[8], xi[8];
+#pragma unroll
+  for (int e = 0; e < 16; e++) a[e] = i64_to_f64(src[64 * e + lane]);
+  fft_fwd_real(a, xr, xi, T, lane, tw);
+  double2* dst = out + (size_t)blockIdx.x * M;
+#pragma unroll
+  for (int e = 0; e < 8; e++) dst[64 * e + lane] = make_double2(xr[e], xi[e]);
+}
+
+__global__ __launch_bounds__(64) void fft_inv_kernel(const double2* __restrict__ in, double* __restrict__ out,
+                                                     const double2* __restrict__ tw) {
+  __shared__ __attribute__((aligned(16))) double2 T[T_C64];
+  const int lane = threadIdx.x;
+  const double2* src = in + (size_t)blockIdx.x * M;
+  double xr[8], xi[8];
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = src[64 * e + lane];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  fft_inv_real(xr, xi, T, lane, tw);
+  double* dst = out + (size_t)blockIdx.x * N1K;
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    dst[64 * e + lane] = xr[e];
+    dst[64 * (e + 8) + lane] = xi[e];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Blind rotation + sample extraction (batch kernel): workgroup = 8 wavefronts = 8 ciphertexts.
+constexpr int FB_WAVES = 8;
+constexpr int FB_THREADS = 64 * FB_WAVES;
+constexpr int CHUNK_C64 = 2 * M;                   // one level step: rows (c, l), j = 0, 1 (16 KB)
+constexpr int CHUNK_GLDS = CHUNK_C64 * 16 / 1024;  // 1 KB wave-instructions per chunk (16)
+
+struct FftShared {
+  double2 T[FB_WAVES][T_C64];  // per-wave transpose / rotation scratch  72 KB
+  double2 K[2][CHUNK_C64];     // double-buffered BSK chunk              32 KB
+  double2 tw[TW_C64];          // twist | pass-A | pass-B tables         24 KB
+};
+
+__device__ __forceinline__ void load_chunk(const double2* __restrict__ bsk, int g, double2* dst, int wave, int lane) {
+  const char* src = (const char*)(bsk + (size_t)g * CHUNK_C64);
+#pragma unroll
+  for (int q = 0; q < CHUNK_GLDS / FB_WAVES; q++) {
+    const int blk = wave * (CHUNK_GLDS / FB_WAVES) + q;
+    __builtin_amdgcn_global_load_lds((const void*)(src + blk * 1024 + lane * 16),
+                                     (__attribute__((address_space(3))) void*)((char*)dst + blk * 1024), 16, 0, 0);
+  }
+}
+
+// component c of the external product for CMUX i: decompose (X^a - 1) acc_c; per level l (step
+// g = 6 i + 3 c + l) transform the digit polynomial and accumulate D (.) BSK_i[(c, l)][j] into O_j
+__device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int a, int c, int i, int n_steps,
+                                                   FftShared& sh, double2* T, int wave, int lane,
+                                                   const double2* __restrict__ bsk, double (&o0r)[8],
+                                                   double (&o0i)[8], double (&o1r)[8], double (&o1i)[8]) {
+  u64* Tu = (u64*)T;
+#pragma unroll
+  for (int e = 0; e < 16; e++) Tu[64 * e + lane] = acc[e];
+  wave_lds_sync();
+  u32 dig[16];
+#pragma unroll
+  for (int e = 0; e < 16; e++) dig[e] = decomp_7x3_t(rot_read_torus(Tu, 64 * e + lane, a) - acc[e]);
+  wave_lds_sync();
+#pragma unroll 1
+  for (int l = 0; l < 3; l++) {
+    const int g = i * 6 + c * 3 + l;
+    glds_barrier();
+    if (g + 1 < n_steps) load_chunk(bsk, g + 1, sh.K[(g + 1) & 1], wave, lane);
+    double xr[8], xi[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      xr[e] = (double)((int)((dig[e] >> (8 * l)) & 0xFFu) - 64);
+      xi[e] = (double)((int)((dig[e + 8] >> (8 * l)) & 0xFFu) - 64);
+      cmul<false>(xr[e], xi[e], sh.tw[TW_TWIST + 64 * e + lane]);
+    }
+    dft512<false>(xr, xi, T, lane, sh.tw);
+    const double2* k0 = sh.K[g & 1] + lane;
+    const double2* k1 = sh.K[g & 1] + M + lane;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const double2 u = k0[64 * e], v = k1[64 * e];
+      o0r[e] = __builtin_fma(xr[e], u.x, o0r[e]);
+      o0r[e] = __builtin_fma(-xi[e], u.y, o0r[e]);
+      o0i[e] = __builtin_fma(xr[e], u.y, o0i[e]);
+      o0i[e] = __builtin_fma(xi[e], u.x, o0i[e]);
+      o1r[e] = __builtin_fma(xr[e], v.x, o1r[e]);
+      o1r[e] = __builtin_fma(-xi[e], v.y, o1r[e]);
+      o1i[e] = __builtin_fma(xr[e], v.y, o1i[e]);
+      o1i[e] = __builtin_fma(xi[e], v.x, o1i[e]);
+    }
+  }
+}
+
+// acc_j += round(iFFT(O_j))
+__device__ __forceinline__ void accumulate(u64 (&acc)[16], double (&or_)[8], double (&oi)[8], double2* T, int lane,
+                                           const double2* tw) {
+  fft_inv_real(or_, oi, T, lane, tw);
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    acc[e] += f64_to_torus(or_[e]);
+    acc[e + 8] += f64_to_torus(oi[e]);
+  }
+}
+
+template <bool WRITE_ACC, bool WRITE_BIG>
+__global__ __launch_bounds__(FB_THREADS, 1) void blind_rotate_fft_kernel(
+    const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
+    int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tw_g, u64* __restrict__ out_big,
+    u64* __restrict__ out_acc) {
+  __shared__ __attribute__((aligned(16))) FftShared sh;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t b_raw = (size_t)blockIdx.x * FB_WAVES + wave;
+  const bool live = b_raw < B;
+  const size_t b = live ? b_raw : B - 1;  // padding waves run a copy of the last ciphertext, store nothing
+  const u64* ct = lwe_in + b * (size_t)(n + 1);
+  double2* T = sh.T[wave];
+  const int n_steps = n * 6;
+
+  for (int q = threadIdx.x; q < TW_C64; q += FB_THREADS) sh.tw[q] = tw_g[q];
+  load_chunk(bsk, 0, sh.K[0], wave, lane);
+
+  // acc = (0, X^{-b~} * lut): LUT values arrive in the Z_p encoding, mapped to the torus first
+  u64 accA[16], accB[16];
+  {
+    int li = lut_index ? (int)lut_index[b] : 0;
+    li = (li < 0 || li >= n_lut) ? 0 : li;
+    const u64* lut = luts + (size_t)li * N1K;
+    const int s = (2048 - ms2048(ct[n])) & 2047;
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      int d = 64 * e + lane - s;
+      bool neg = false;
+      if (d < 0) { d += N1K; neg = !neg; }
+      if (d < 0) { d += N1K; neg = !neg; }
+      const u64 v = gl_to_torus(lut[d]);
+      accA[e] = 0;
+      accB[e] = neg ? 0 - v : v;
+    }
+  }
+
+  for (int i = 0; i < n; i++) {
+    const int a = ms2048(ct[i]);
+    double o0r[8], o0i[8], o1r[8], o1i[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) { o0r[e] = 0; o0i[e] = 0; o1r[e] = 0; o1i[e] = 0; }
+    ext_prod_component(accA, a, 0, i, n_steps, sh, T, wave, lane, bsk, o0r, o0i, o1r, o1i);
+    ext_prod_component(accB, a, 1, i, n_steps, sh, T, wave, lane, bsk, o0r, o0i, o1r, o1i);
+    accumulate(accA, o0r, o0i, T, lane, sh.tw);
+    accumulate(accB, o1r, o1i, T, lane, sh.tw);
+  }
+
+  if (!live) return;
+  if (WRITE_ACC) {
+    u64* oa = out_acc + b * 2048;
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      oa[64 * e + lane] = accA[e];
+      oa[N1K + 64 * e + lane] = accB[e];
+    }
+  }
+  if (WRITE_BIG) {
+    // sample extraction at degree 0 (computations.rs:109-132): a'_0 = A[0], a'_j = -A[N-j], b' = B[0]
+    u64* ob = out_big + b * (size_t)(N1K + 1);
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      const int idx = 64 * e + lane;
+      if (idx == 0) ob[0] = accA[e];
+      else ob[N1K - idx] = 0 - accA[e];
+    }
+    if (lane == 0) ob[N1K] = accB[0];
+  }
+}
+
+__global__ void sample_extract_torus_kernel(const u64* __restrict__ acc, size_t B, u64* __restrict__ out) {
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * (N1K + 1)) return;
+  const size_t b = gid / (N1K + 1);
+  const int j = (int)(gid % (N1K + 1));
+  const u64* A = acc + b * 2048;
+  out[gid] = j == N1K ? A[N1K] : j == 0 ? A[0] : 0 - A[N1K - j];
+}
+
+// ---------------------------------------------------------------------------------------------
+// host: tables (fixed series in plain double, octant-reduced — the oracle's or_fft_twiddle)
+static double fs_sin(double x) {
+  double x2 = x * x, term = x, sum = 0.0;
+  for (int i = 1; i <= 21; i += 2) { sum += term; term = -term * x2 / (double)((i + 1) * (i + 2)); }
+  return sum;
+}
+static double fs_cos(double x) {
+  double x2 = x * x, term = 1.0, sum = 0.0;
+  for (int i = 0; i <= 20; i += 2) { sum += term; term = -term * x2 / (double)((i + 1) * (i + 2)); }
+  return sum;
+}
+static void tw_octant(uint32_t t, uint32_t m, double* c, double* s) {
+  const double x = (double)t * (6.28318530717958647692 / (double)m);
+  *c = fs_cos(x);
+  *s = fs_sin(x);
+}
+static void tw_quarter(uint32_t t, uint32_t m, double* c, double* s) {
+  if (8 * t > m) {
+    double cu, su;
+    tw_octant(m / 4 - t, m, &cu, &su);
+    *c = su;
+    *s = cu;
+  } else {
+    tw_octant(t, m, c, s);
+  }
+}
+static void twiddle(uint32_t t, uint32_t m, double* c, double* s) {
+  t %= m;
+  bool neg = false;
+  if (2 * t > m) { t = m - t; neg = true; }
+  double cc, ss;
+  if (4 * t > m) {
+    double cu, su;
+    tw_quarter(t - m / 4, m, &cu, &su);
+    cc = -su;
+    ss = cu;
+  } else {
+    tw_quarter(t, m, &cc, &ss);
+  }
+  *c = cc;
+  *s = neg ? -ss : ss;
+}
+
+}  // namespace fftk
+
+size_t fft_tables_len() { return 2 * fftk::TW_C64; }
+
+void make_fft_tables(double* t) {
+  using namespace fftk;
+  for (uint32_t j = 0; j < (uint32_t)M; j++) twiddle(j, 4 * M, &t[2 * (TW_TWIST + j)], &t[2 * (TW_TWIST + j) + 1]);
+  for (uint32_t e = 0; e < 8; e++)
+    for (uint32_t L = 0; L < 64; L++) {
+      twiddle((L * e) % M, M, &t[2 * (TW_A + 64 * e + L)], &t[2 * (TW_A + 64 * e + L) + 1]);
+      twiddle((8 * (L & 7) * e) % M, M, &t[2 * (TW_B + 64 * e + L)], &t[2 * (TW_B + 64 * e + L) + 1]);
+    }
+}
+
+hipError_t launch_bsk_to_fourier(const u64* bsk_std, double* bsk_f, size_t polys, const double* tw, hipStream_t s) {
+  hipLaunchKernelGGL(fftk::bsk_to_fourier_kernel, dim3((unsigned)polys), dim3(64), 0, s, bsk_std, (double2*)bsk_f,
+                     (const double2*)tw);
+  return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
+                                   int n_lut, const double* bsk_f, const double* tw, u64* out_big, u64* out_acc,
+                                   hipStream_t s) {
+  using namespace fftk;
+  if (B == 0) return hipSuccess;
+  dim3 grid((unsigned)((B + FB_WAVES - 1) / FB_WAVES)), block(FB_THREADS);
+  const double2 *bk = (const double2*)bsk_f, *t = (const double2*)tw;
+  if (out_acc && out_big)
+    hipLaunchKernelGGL((blind_rotate_fft_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index, n_lut,
+                       bk, t, out_big, out_acc);
+  else if (out_acc)
+    hipLaunchKernelGGL((blind_rotate_fft_kernel<true, false>), grid, block, 0, s, lwe_in, n, B, luts, lut_index, n_lut,
+                       bk, t, out_big, out_acc);
+  else
+    hipLaunchKernelGGL((blind_rotate_fft_kernel<false, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                       n_lut, bk, t, out_big, out_acc);
+  return hipGetLastError();
+}
+
+hipError_t launch_sample_extract_torus(const u64* acc, size_t B, u64* out, hipStream_t s) {
+  if (B == 0) return hipSuccess;
+  const size_t total = B * (N1K + 1);
+  hipLaunchKernelGGL(fftk::sample_extract_torus_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, acc, B,
+                     out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fft_fwd(const u64* in, size_t count, double* out, const double* tw, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(fftk::fft_fwd_kernel, dim3((unsigned)count), dim3(64), 0, s, in, (double2*)out,
+                     (const double2*)tw);
+  return hipGetLastError();
+}
+
+hipError_t launch_fft_inv(const double* in, size_t count, double* out, const double* tw, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(fftk::fft_inv_kernel, dim3((unsigned)count), dim3(64), 0, s, (const double2*)in, out,
+                     (const double2*)tw);
+  return hipGetLastError();
+}
+
+}  // namespace tfhe

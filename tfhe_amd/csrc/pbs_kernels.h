@@ -20,6 +20,18 @@ hipError_t launch_keyswitch(const u64* in_big, size_t B, int big_dim, const u64*
 hipError_t launch_ntt_fwd(u64* polys, size_t count, const u64* tw, hipStream_t s);
 hipError_t launch_ntt_inv(u64* polys, size_t count, const u64* tw, u64 ninv, hipStream_t s);
 
+// FFT64 transform (pbs_fft.hip), N = 1024: tables = 1536 complex (twist | pass A | pass B);
+// Fourier BSK = polys x 512 complex
+size_t fft_tables_len();  // doubles
+void make_fft_tables(double* tw);
+hipError_t launch_bsk_to_fourier(const u64* bsk_std, double* bsk_f, size_t polys, const double* tw, hipStream_t s);
+hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
+                                   int n_lut, const double* bsk_f, const double* tw, u64* out_big, u64* out_acc,
+                                   hipStream_t s);
+hipError_t launch_sample_extract_torus(const u64* acc, size_t B, u64* out, hipStream_t s);
+hipError_t launch_fft_fwd(const u64* in, size_t count, double* out, const double* tw, hipStream_t s);
+hipError_t launch_fft_inv(const double* in, size_t count, double* out, const double* tw, hipStream_t s);
+
 // N = 2048 (P-FHEVM, pbs_n2048.hip): tables = [1024-point tables of psi^2 (4096) | combine
 // twiddles psi^(2j+1) (2048) | inverses (2048)]
 void make_ntt2048_tables(u64 psi, u64* tw);
