@@ -18,10 +18,17 @@
  *                    (inverse transforms use w = (w.re, -w.im))
  *   dft8             radix-2 decimation in frequency, 3 stages, natural order in and out; the
  *                    internal rotations by e^{+-i pi/4 j} are the explicit forms in w8() below
- *   3 passes         M = 512 = 8 x 8 x 8 over a 64 x 8 grid (the device's lane x register grid):
+ *   3 passes         M = 512 = 8 x 8 x 8 over a 64 x 8 grid (the device's lane x register grid),
+ *                    w = e^{2 pi i / M}, n = n0 + 8 n1 + 64 n2, k = k0 + 8 k1 + 64 k2:
  *                    A: lane L = n0 + 8 n1 transforms n2, then x[k0] *= w^{L k0}           (k0 > 0)
  *                    B: lane n0 + 8 k0 transforms n1, then x[k1] *= w^{8 n0 k1}            (k1 > 0)
- *                    C: lane k0 + 8 k1 transforms n0 -> Z[k0 + 8 k1 + 64 k2] in slot k2
+ *                    C: lane k1 + 8 k0 transforms n0 -> Z[k] in slot k2
+ *                    so spectra are kept in DEVICE ORDER: slot d = L + 64 e holds frequency
+ *                    k(d) = (L >> 3) + 8 (L & 7) + 64 e (the BSK is converted by the same routine)
+ *   inverse          the passes reversed (decimation in time), device order in, natural order out:
+ *                    C': lane k1 + 8 k0 transforms k2 -> n0, x[n0] *= conj(w^{8 n0 k1})   (n0 > 0)
+ *                    B': lane n0 + 8 k0 transforms k1 -> n1, x[n1] *= conj(w^{k0 (n0 + 8 n1)}) (all)
+ *                    A': lane n0 + 8 n1 transforms k0 -> n2 = z[L + 64 n2]
  *   MAC              re = fma(D.re, K.re, re); re = fma(-D.im, K.im, re);
  *                    im = fma(D.re, K.im, im); im = fma(D.im, K.re, im)   from (0, 0), r ascending
  */
@@ -83,6 +90,7 @@ typedef struct fft_tab {
   or_c64 twist[FFT_M];  /* zeta^j, zeta = e^{i pi / N} */
   or_c64 twA[8][64];    /* w^{L k0}, w = e^{2 pi i / M} */
   or_c64 twB[8][64];    /* w^{8 (L & 7) k1} */
+  or_c64 twI[8][64];    /* w^{(L >> 3) ((L & 7) + 8 e)} (inverse pass B') */
 } fft_tab;
 
 static fft_tab g_tab;
@@ -97,6 +105,7 @@ static const fft_tab* tab(void) {
         for (uint32_t L = 0; L < 64; L++) {
           or_fft_twiddle((L * e) % FFT_M, FFT_M, &g_tab.twA[e][L].re, &g_tab.twA[e][L].im);
           or_fft_twiddle((8 * (L & 7) * e) % FFT_M, FFT_M, &g_tab.twB[e][L].re, &g_tab.twB[e][L].im);
+          or_fft_twiddle(((L >> 3) * ((L & 7) + 8 * e)) % FFT_M, FFT_M, &g_tab.twI[e][L].re, &g_tab.twI[e][L].im);
         }
       __atomic_store_n(&g_tab_ready, 1, __ATOMIC_RELEASE);
     }
@@ -150,26 +159,48 @@ static void dft8(or_c64 x[8], int inv) {
   for (int k = 0; k < 8; k++) x[k] = u[brv3[k]];
 }
 
-/* the 3-pass DFT, natural order in and out (in may alias out) */
-static void dft512(const or_c64* in, or_c64* out, int inv) {
+/* forward 3-pass DFT: natural order in, device order out */
+static void dft512_fwd(const or_c64* in, or_c64* out) {
   const fft_tab* T = tab();
-  const double sg = inv ? -1.0 : 1.0;
   or_c64 A[64][8], Bv[64][8], x[8];
   for (int L = 0; L < 64; L++) {
     for (int e = 0; e < 8; e++) x[e] = in[L + 64 * e];
-    dft8(x, inv);
-    for (int e = 1; e < 8; e++) x[e] = cmul(x[e], T->twA[e][L].re, sg * T->twA[e][L].im);
+    dft8(x, 0);
+    for (int e = 1; e < 8; e++) x[e] = cmul(x[e], T->twA[e][L].re, T->twA[e][L].im);
     memcpy(A[L], x, sizeof(x));
   }
-  for (int L = 0; L < 64; L++) {
+  for (int L = 0; L < 64; L++) { /* lane n0 + 8 k0 */
     for (int e = 0; e < 8; e++) x[e] = A[(L & 7) + 8 * e][L >> 3];
-    dft8(x, inv);
-    for (int e = 1; e < 8; e++) x[e] = cmul(x[e], T->twB[e][L].re, sg * T->twB[e][L].im);
+    dft8(x, 0);
+    for (int e = 1; e < 8; e++) x[e] = cmul(x[e], T->twB[e][L].re, T->twB[e][L].im);
     memcpy(Bv[L], x, sizeof(x));
   }
-  for (int L = 0; L < 64; L++) {
-    for (int e = 0; e < 8; e++) x[e] = Bv[e + 8 * (L & 7)][L >> 3];
-    dft8(x, inv);
+  for (int L = 0; L < 64; L++) { /* lane k1 + 8 k0 */
+    for (int e = 0; e < 8; e++) x[e] = Bv[e + 8 * (L >> 3)][L & 7];
+    dft8(x, 0);
+    for (int e = 0; e < 8; e++) out[L + 64 * e] = x[e];
+  }
+}
+
+/* inverse 3-pass DFT (no 1/M): device order in, natural order out */
+static void dft512_inv(const or_c64* in, or_c64* out) {
+  const fft_tab* T = tab();
+  or_c64 S1[64][8], S2[64][8], x[8];
+  for (int L = 0; L < 64; L++) { /* lane k1 + 8 k0: k2 -> n0 */
+    for (int e = 0; e < 8; e++) x[e] = in[L + 64 * e];
+    dft8(x, 1);
+    for (int e = 1; e < 8; e++) x[e] = cmul(x[e], T->twB[e][L].re, -T->twB[e][L].im);
+    memcpy(S1[L], x, sizeof(x));
+  }
+  for (int L = 0; L < 64; L++) { /* lane n0 + 8 k0: k1 -> n1 */
+    for (int e = 0; e < 8; e++) x[e] = S1[e + 8 * (L >> 3)][L & 7];
+    dft8(x, 1);
+    for (int e = 0; e < 8; e++) x[e] = cmul(x[e], T->twI[e][L].re, -T->twI[e][L].im);
+    memcpy(S2[L], x, sizeof(x));
+  }
+  for (int L = 0; L < 64; L++) { /* lane n0 + 8 n1: k0 -> n2 */
+    for (int e = 0; e < 8; e++) x[e] = S2[(L & 7) + 8 * e][L >> 3];
+    dft8(x, 1);
     for (int e = 0; e < 8; e++) out[L + 64 * e] = x[e];
   }
 }
@@ -182,14 +213,14 @@ void or_fft_fwd(const double* a, uint32_t N, or_c64* out) {
     const or_c64 v = {a[j], a[j + FFT_M]};
     z[j] = cmul(v, T->twist[j].re, T->twist[j].im);
   }
-  dft512(z, out, 0);
+  dft512_fwd(z, out);
 }
 
 void or_fft_inv(const or_c64* in, uint32_t N, double* out) {
   if (N != 2 * FFT_M) abort();
   const fft_tab* T = tab();
   or_c64 z[FFT_M];
-  dft512(in, z, 1);
+  dft512_inv(in, z);
   for (int j = 0; j < FFT_M; j++) {
     const or_c64 v = cmul(z[j], T->twist[j].re, -T->twist[j].im);
     out[j] = v.re;

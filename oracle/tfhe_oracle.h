@@ -221,7 +221,8 @@ void or_sns_phase(const or_sns_params* sp, const uint64_t* glwe_key, const uint6
  * sequence, which the device kernels (pbs_fft.hip) reproduce bit-for-bit:
  *   fold + twist   z_j = (a_j + i a_{j+N/2}) * zeta^j, zeta = e^{i pi/N}       (j < M = N/2)
  *   DFT            Z_k = sum_j z_j e^{+2 pi i jk/M}: three radix-8 passes (M = 512 = 8 x 8 x 8),
- *                  natural order in and out (layout and per-element operation order: fft_oracle.c)
+ *                  spectra in DEVICE ORDER: slot d = L + 64 e holds k = (L>>3) + 8 (L&7) + 64 e
+ *                  (layout and per-element operation order: fft_oracle.c)
  *   BSK            Fourier(BSK) = DFT(twist((double)(int64)bsk)) * 2^-9     (1/M folded in)
  *   MAC            O_j = sum_r D_r (.) BSK[r][j], r = c*l + lvl in order, 4 fma per complex term
  *   inverse        z'_j = sum_k O_k e^{-2 pi i jk/M} (same passes, conjugate twiddles), untwist by
@@ -235,9 +236,9 @@ void or_sns_phase(const or_sns_params* sp, const uint64_t* glwe_key, const uint6
 typedef struct or_c64 { double re, im; } or_c64;
 /* cos(2 pi t / M), sin(2 pi t / M) for 0 <= t < M (M a multiple of 8), fixed-series evaluation */
 void or_fft_twiddle(uint32_t t, uint32_t M, double* c, double* s);
-/* forward: N real values (exact doubles) -> N/2 complex (natural order) */
+/* forward: N real values (exact doubles) -> N/2 complex in device order (see above) */
 void or_fft_fwd(const double* a, uint32_t N, or_c64* out);
-/* inverse WITHOUT the 1/M factor: N/2 complex -> N doubles (not rounded) */
+/* inverse WITHOUT the 1/M factor: N/2 complex in device order -> N doubles (not rounded) */
 void or_fft_inv(const or_c64* in, uint32_t N, double* out);
 /* round(x) mod 2^64 (ties to even) */
 uint64_t or_f64_to_torus(double x);

@@ -15,11 +15,16 @@ from conftest import KEY_SEED
 N, M = 1024, 512
 
 
+# device order: slot d = L + 64 e holds frequency k = (L >> 3) + 8 (L & 7) + 64 e
+_D = np.arange(M)
+DEVICE_ORDER = (_D % 64 >> 3) + 8 * (_D % 8) + 64 * (_D // 64)
+
+
 def _dft_definition(a):
-    """z_j = (a_j + i a_{j+M}) zeta^j, Z_k = sum_j z_j e^{+2 pi i jk/M} in long double-free numpy."""
+    """z_j = (a_j + i a_{j+M}) zeta^j, Z_k = sum_j z_j e^{+2 pi i jk/M}, returned in device order."""
     zeta = np.exp(1j * np.pi * np.arange(M) / N)
     z = (a[:M] + 1j * a[M:]) * zeta
-    return np.fft.ifft(z) * M  # numpy's ifft uses e^{+2 pi i jk/M} / M
+    return (np.fft.ifft(z) * M)[DEVICE_ORDER]  # numpy's ifft uses e^{+2 pi i jk/M} / M
 
 
 def test_twiddles_match_libm(oracle_mod):

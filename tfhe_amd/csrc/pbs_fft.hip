@@ -14,9 +14,11 @@
 // contraction is off for the whole file):
 //   fold + twist  z_j = (a_j + i a_{j+512}) * zeta^j,   zeta = e^{i pi / 1024}
 //   DFT           Z_k = sum_j z_j e^{+2 pi i jk / 512}: 3 radix-8 passes over the wave's 64 lanes
-//                 x 8 registers, natural order in and out (lane L, slot e <-> index L + 64 e), two
-//                 LDS transposes (row stride 72 complex, low-3-bit XOR swizzle: conflict-free for
-//                 both the ds_write_b128 and the ds_read_b128 patterns)
+//                 x 8 registers, natural order in, DEVICE ORDER out (slot e of lane L holds
+//                 k = (L >> 3) + 8 (L & 7) + 64 e); the inverse runs the passes reversed (DIT), device
+//                 order in, natural order out.  Two LDS transposes each way with plain padded rows
+//                 (strides 72 and 65 complex): every ds_write_b128 / ds_read_b128 is conflict-free and
+//                 every address is a per-lane base plus an immediate offset
 //   MAC           O_j += D_r (.) BSK_i[r][j], 4 fma per complex, r = c*3 + l ascending
 //   inverse       conjugate passes, untwist by conj(zeta^j), rint, mod 2^64, add to the accumulator
 // Coefficient 64 e + L of a u64 register polynomial (slot e of lane L, e < 16) meets coefficient
@@ -32,12 +34,10 @@ namespace tfhe {
 namespace fftk {
 
 constexpr int M = 512;
-constexpr int TS = 72;            // transpose row stride (complex)
-constexpr int T_C64 = 8 * TS;     // per-wave transpose scratch (9,216 B; also holds 1024 u64)
-constexpr int TW_TWIST = 0, TW_A = 512, TW_B = 1024, TW_C64 = 1536;  // table offsets (complex)
+constexpr int S1 = 72, S2 = 65;   // transpose row strides (complex): T1 (passes A|B), T2 (passes B|C)
+constexpr int T_C64 = 576;        // per-wave transpose scratch (9,216 B; also holds 1024 u64)
+constexpr int TW_TWIST = 0, TW_A = 512, TW_B = 1024, TW_I = 1536, TW_C64 = 2048;  // table offsets (complex)
 constexpr double SQRT1_2 = 0.70710678118654752440;
-
-__device__ __forceinline__ int swz(int c) { return (c & 56) | ((c & 7) ^ (c >> 3)); }
 
 // z * w (INV: z * conj(w)), the oracle's cmul(z, w.re, +-w.im)
 template <bool INV>
@@ -105,36 +105,75 @@ __device__ __forceinline__ void dft8(double (&xr)[8], double (&xi)[8]) {
   xr[7] = zr[6] - zr[7]; xi[7] = zi[6] - zi[7];
 }
 
-// the 512-point DFT of the wavefront's complex vector (lane L, slot e <-> index L + 64 e)
-template <bool INV>
-__device__ __forceinline__ void dft512(double (&xr)[8], double (&xi)[8], double2* T, int lane, const double2* tw) {
-  dft8<INV>(xr, xi);
+// per-lane transpose bases: b1 = T1 read / inverse write, b2 = T2 read / inverse write
+struct TBase {
+  int b1, b2;
+  __device__ __forceinline__ explicit TBase(int lane)
+      : b1((lane >> 3) * S1 + (lane & 7)), b2((lane & 7) * S2 + 8 * (lane >> 3)) {}
+};
+
+// forward 512-point DFT: natural order in (lane L, slot e <-> L + 64 e), device order out
+__device__ __forceinline__ void dft512_fwd(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
+                                           const double2* tw) {
+  dft8<false>(xr, xi);
 #pragma unroll
-  for (int e = 1; e < 8; e++) cmul<INV>(xr[e], xi[e], tw[TW_A + 64 * e + lane]);
+  for (int e = 1; e < 8; e++) cmul<false>(xr[e], xi[e], tw[TW_A + 64 * e + lane]);
 #pragma unroll
-  for (int e = 0; e < 8; e++) T[e * TS + swz(lane)] = make_double2(xr[e], xi[e]);
+  for (int e = 0; e < 8; e++) T[lane + S1 * e] = make_double2(xr[e], xi[e]);
   wave_lds_sync();
 #pragma unroll
   for (int e = 0; e < 8; e++) {
-    const double2 v = T[(lane >> 3) * TS + swz((lane & 7) + 8 * e)];
+    const double2 v = T[tb.b1 + 8 * e];
     xr[e] = v.x;
     xi[e] = v.y;
   }
   wave_lds_sync();
-  dft8<INV>(xr, xi);
+  dft8<false>(xr, xi);
 #pragma unroll
-  for (int e = 1; e < 8; e++) cmul<INV>(xr[e], xi[e], tw[TW_B + 64 * e + lane]);
+  for (int e = 1; e < 8; e++) cmul<false>(xr[e], xi[e], tw[TW_B + 64 * e + lane]);
 #pragma unroll
-  for (int e = 0; e < 8; e++) T[e * TS + swz(lane)] = make_double2(xr[e], xi[e]);
+  for (int e = 0; e < 8; e++) T[lane + S2 * e] = make_double2(xr[e], xi[e]);
   wave_lds_sync();
 #pragma unroll
   for (int e = 0; e < 8; e++) {
-    const double2 v = T[(lane >> 3) * TS + swz(e + 8 * (lane & 7))];
+    const double2 v = T[tb.b2 + e];
     xr[e] = v.x;
     xi[e] = v.y;
   }
   wave_lds_sync();
-  dft8<INV>(xr, xi);
+  dft8<false>(xr, xi);
+}
+
+// inverse (no 1/M): device order in, natural order out — the forward's passes reversed
+__device__ __forceinline__ void dft512_inv(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
+                                           const double2* tw) {
+  dft8<true>(xr, xi);
+#pragma unroll
+  for (int e = 1; e < 8; e++) cmul<true>(xr[e], xi[e], tw[TW_B + 64 * e + lane]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[tb.b2 + e] = make_double2(xr[e], xi[e]);
+  wave_lds_sync();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[lane + S2 * e];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  wave_lds_sync();
+  dft8<true>(xr, xi);
+#pragma unroll
+  for (int e = 0; e < 8; e++) cmul<true>(xr[e], xi[e], tw[TW_I + 64 * e + lane]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[tb.b1 + 8 * e] = make_double2(xr[e], xi[e]);
+  wave_lds_sync();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[lane + S1 * e];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  wave_lds_sync();
+  dft8<true>(xr, xi);
 }
 
 // (double)(int64)x, correctly rounded: exact hi * 2^32 plus exact lo, one rounding
@@ -161,30 +200,20 @@ __device__ __forceinline__ void fft_fwd_real(const double (&a)[16], double (&xr)
     xi[e] = a[e + 8];
     cmul<false>(xr[e], xi[e], tw[TW_TWIST + 64 * e + lane]);
   }
-  dft512<false>(xr, xi, T, lane, tw);
+  dft512_fwd(xr, xi, T, lane, TBase(lane), tw);
 }
 
 // inverse transform (no 1/M) + untwist: slot e -> coefficient 64 e + L (re), 64 (e + 8) + L (im)
-__device__ __forceinline__ void fft_inv_real(double (&xr)[8], double (&xi)[8], double2* T, int lane,
+__device__ __forceinline__ void fft_inv_real(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
                                              const double2* tw) {
-  dft512<true>(xr, xi, T, lane, tw);
+  dft512_inv(xr, xi, T, lane, tb, tw);
 #pragma unroll
   for (int e = 0; e < 8; e++) cmul<true>(xr[e], xi[e], tw[TW_TWIST + 64 * e + lane]);
 }
 
 __device__ __forceinline__ int ms2048(u64 x) { return (int)((((x >> 52) + 1) >> 1) & 2047u); }
 
-// (X^s * v)[idx] for a negacyclic length-1024 torus polynomial, s in [0, 2048)
-__device__ __forceinline__ u64 rot_read_torus(const u64* v, int idx, int s) {
-  int d = idx - s;
-  bool neg = false;
-  if (d < 0) { d += N1K; neg = !neg; }
-  if (d < 0) { d += N1K; neg = !neg; }
-  const u64 x = v[d];
-  return neg ? 0 - x : x;
-}
-
-// tfhe-rs SignedDecomposer 2^7 x 3 on a torus value: bytes (d + 64), byte l = level l (0 = MSB)
+// tfhe-rs SignedDecomposer 2^7 x 3 on a torus value: signed bytes d, byte l = level l (0 = MSB)
 __device__ __forceinline__ u32 decomp_7x3_t(u64 x) {
   u32 state = (u32)(((x >> 42) + 1) >> 1) & 0x1FFFFFu;
   u32 packed = 0;
@@ -195,7 +224,7 @@ __device__ __forceinline__ u32 decomp_7x3_t(u64 x) {
     const u32 carry = ((((res - 1u) | state) & res) >> 6) & 1u;
     state += carry;
     const int d = (int)res - (int)(carry << 7);
-    packed |= (u32)(d + 64) << (8 * l);
+    packed |= ((u32)d & 0xFFu) << (8 * l);
   }
   return packed;
 }
@@ -245,7 +274,7 @@ __global__ __launch_bounds__(64) void fft_inv_kernel(const double2* __restrict__
     xr[e] = v.x;
     xi[e] = v.y;
   }
-  fft_inv_real(xr, xi, T, lane, tw);
+  fft_inv_real(xr, xi, T, lane, TBase(lane), tw);
   double* dst = out + (size_t)blockIdx.x * N1K;
 #pragma unroll
   for (int e = 0; e < 8; e++) {
@@ -264,7 +293,7 @@ constexpr int CHUNK_GLDS = CHUNK_C64 * 16 / 1024;  // 1 KB wave-instructions per
 struct FftShared {
   double2 T[FB_WAVES][T_C64];  // per-wave transpose / rotation scratch  72 KB
   double2 K[2][CHUNK_C64];     // double-buffered BSK chunk              32 KB
-  double2 tw[TW_C64];          // twist | pass-A | pass-B tables         24 KB
+  double2 tw[TW_C64];          // twist | pass A | pass B | inverse B'   32 KB
 };
 
 __device__ __forceinline__ void load_chunk(const double2* __restrict__ bsk, int g, double2* dst, int wave, int lane) {
@@ -279,17 +308,23 @@ __device__ __forceinline__ void load_chunk(const double2* __restrict__ bsk, int 
 
 // component c of the external product for CMUX i: decompose (X^a - 1) acc_c; per level l (step
 // g = 6 i + 3 c + l) transform the digit polynomial and accumulate D (.) BSK_i[(c, l)][j] into O_j
-__device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int a, int c, int i, int n_steps,
-                                                   FftShared& sh, double2* T, int wave, int lane,
+__device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rbase, int c, int i, int n_steps,
+                                                   FftShared& sh, double2* T, int wave, int lane, TBase tb,
                                                    const double2* __restrict__ bsk, double (&o0r)[8],
                                                    double (&o0i)[8], double (&o1r)[8], double (&o1i)[8]) {
   u64* Tu = (u64*)T;
 #pragma unroll
   for (int e = 0; e < 16; e++) Tu[64 * e + lane] = acc[e];
   wave_lds_sync();
+  // (X^a acc)[64 e + L] = +-acc[(t mod 1024)], t = 64 e + L - a + 2048: negated iff t in [1024, 2048)
   u32 dig[16];
 #pragma unroll
-  for (int e = 0; e < 16; e++) dig[e] = decomp_7x3_t(rot_read_torus(Tu, 64 * e + lane, a) - acc[e]);
+  for (int e = 0; e < 16; e++) {
+    const int t = rbase + 64 * e;
+    const u64 x = Tu[t & (N1K - 1)];
+    const u64 r = (t & N1K) ? 0 - x : x;
+    dig[e] = decomp_7x3_t(r - acc[e]);
+  }
   wave_lds_sync();
 #pragma unroll 1
   for (int l = 0; l < 3; l++) {
@@ -299,11 +334,11 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int a, 
     double xr[8], xi[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) {
-      xr[e] = (double)((int)((dig[e] >> (8 * l)) & 0xFFu) - 64);
-      xi[e] = (double)((int)((dig[e + 8] >> (8 * l)) & 0xFFu) - 64);
+      xr[e] = (double)((int)(dig[e] << (24 - 8 * l)) >> 24);
+      xi[e] = (double)((int)(dig[e + 8] << (24 - 8 * l)) >> 24);
       cmul<false>(xr[e], xi[e], sh.tw[TW_TWIST + 64 * e + lane]);
     }
-    dft512<false>(xr, xi, T, lane, sh.tw);
+    dft512_fwd(xr, xi, T, lane, tb, sh.tw);
     const double2* k0 = sh.K[g & 1] + lane;
     const double2* k1 = sh.K[g & 1] + M + lane;
 #pragma unroll
@@ -323,8 +358,8 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int a, 
 
 // acc_j += round(iFFT(O_j))
 __device__ __forceinline__ void accumulate(u64 (&acc)[16], double (&or_)[8], double (&oi)[8], double2* T, int lane,
-                                           const double2* tw) {
-  fft_inv_real(or_, oi, T, lane, tw);
+                                           TBase tb, const double2* tw) {
+  fft_inv_real(or_, oi, T, lane, tb, tw);
 #pragma unroll
   for (int e = 0; e < 8; e++) {
     acc[e] += f64_to_torus(or_[e]);
@@ -368,15 +403,16 @@ __global__ __launch_bounds__(FB_THREADS, 1) void blind_rotate_fft_kernel(
     }
   }
 
+  const TBase tb(lane);
   for (int i = 0; i < n; i++) {
-    const int a = ms2048(ct[i]);
+    const int rbase = lane - ms2048(ct[i]) + 2 * N1K;
     double o0r[8], o0i[8], o1r[8], o1i[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) { o0r[e] = 0; o0i[e] = 0; o1r[e] = 0; o1i[e] = 0; }
-    ext_prod_component(accA, a, 0, i, n_steps, sh, T, wave, lane, bsk, o0r, o0i, o1r, o1i);
-    ext_prod_component(accB, a, 1, i, n_steps, sh, T, wave, lane, bsk, o0r, o0i, o1r, o1i);
-    accumulate(accA, o0r, o0i, T, lane, sh.tw);
-    accumulate(accB, o1r, o1i, T, lane, sh.tw);
+    ext_prod_component(accA, rbase, 0, i, n_steps, sh, T, wave, lane, tb, bsk, o0r, o0i, o1r, o1i);
+    ext_prod_component(accB, rbase, 1, i, n_steps, sh, T, wave, lane, tb, bsk, o0r, o0i, o1r, o1i);
+    accumulate(accA, o0r, o0i, T, lane, tb, sh.tw);
+    accumulate(accB, o1r, o1i, T, lane, tb, sh.tw);
   }
 
   if (!live) return;
@@ -465,6 +501,7 @@ void make_fft_tables(double* t) {
     for (uint32_t L = 0; L < 64; L++) {
       twiddle((L * e) % M, M, &t[2 * (TW_A + 64 * e + L)], &t[2 * (TW_A + 64 * e + L) + 1]);
       twiddle((8 * (L & 7) * e) % M, M, &t[2 * (TW_B + 64 * e + L)], &t[2 * (TW_B + 64 * e + L) + 1]);
+      twiddle(((L >> 3) * ((L & 7) + 8 * e)) % M, M, &t[2 * (TW_I + 64 * e + L)], &t[2 * (TW_I + 64 * e + L) + 1]);
     }
 }
 
