@@ -30,7 +30,9 @@
  *                    B': lane n0 + 8 k0 transforms k1 -> n1, x[n1] *= conj(w^{k0 (n0 + 8 n1)}) (all)
  *                    A': lane n0 + 8 n1 transforms k0 -> n2 = z[L + 64 n2]
  *   MAC              re = fma(D.re, K.re, re); re = fma(-D.im, K.im, re);
- *                    im = fma(D.re, K.im, im); im = fma(D.im, K.re, im)   from (0, 0), r ascending
+ *                    im = fma(D.re, K.im, im); im = fma(D.im, K.re, im)   from (0, 0), over
+ *                    c = 0..k and, within c, the levels least significant first (l = L-1 .. 0:
+ *                    the order the device produces digits, carry chain upward)
  */
 #include <math.h>
 #include <stdlib.h>
@@ -288,7 +290,7 @@ void or_blind_rotate_fft(const or_params* p, const or_c64* bsk_f, const uint64_t
         or_decompose(rot[j] - acc[(size_t)c * N + j], p->pbs_base_log, L, d);
         for (uint32_t l = 0; l < L; l++) dig[l][j] = (double)d[l];
       }
-      for (uint32_t l = 0; l < L; l++) {
+      for (int l = (int)L - 1; l >= 0; l--) {
         or_fft_fwd(dig[l], N, D);
         const or_c64* row = bsk_f + per_i * i + (size_t)(c * L + l) * (k + 1) * M;
         for (uint32_t j = 0; j <= k; j++) {

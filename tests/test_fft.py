@@ -126,3 +126,37 @@ def test_oracle_blind_rotate_lut_table(oracle_mod, fft_keys):
         big = oracle_mod.sample_extract_torus(prm, acc)
         ph = fft_keys.phase(big, fft_keys.glwe_key, N)[0]
         assert ((int(ph) + delta // 2) // delta) % 16 == table[m]
+
+
+def test_device_decomposition_steps_equal_signed_decomposer(oracle_mod):
+    """pbs_fft.hip decomposes least-significant level first with a running state
+    (W = st + 63 + b, b = bit 13 of st below the top level): equal to the tfhe-rs SignedDecomposer rule
+    for every 21-bit state (exhaustive, numpy), and to or_decompose on sampled torus values."""
+    V = np.arange(1 << 21, dtype=np.int64)
+
+    def sequential(st):
+        out = []
+        for _ in range(3):
+            res = st & 127
+            st = st >> 7
+            carry = ((((res - 1) | st) & res) >> 6) & 1
+            st = st + carry
+            out.append(res - (carry << 7))
+        return out
+
+    def steps(st):
+        out = []
+        for q in range(3):
+            b = (st >> 13) & 1 if q < 2 else np.zeros_like(st)
+            W = st + 63 + b
+            out.append((W & 127) - 63 - b)
+            st = W >> 7
+        return out
+
+    assert all(np.array_equal(a, b) for a, b in zip(sequential(V), steps(V)))
+    rng = np.random.default_rng(8)
+    for x in list(rng.integers(0, 2**64, 3000, dtype=np.uint64)) + [0, 2**64 - 1, 2**63, 2**42, 2**42 - 1]:
+        x = int(x)
+        st = np.array([(((x >> 32) + 1024) % 2**32) >> 11], dtype=np.int64)  # the device's decomp_state
+        lv = [int(v[0]) for v in steps(st)]  # least significant first
+        assert lv[::-1] == oracle_mod.decompose(x, 7, 3)

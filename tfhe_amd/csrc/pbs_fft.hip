@@ -19,7 +19,9 @@
 //                 order in, natural order out.  Two LDS transposes each way with plain padded rows
 //                 (strides 72 and 65 complex): every ds_write_b128 / ds_read_b128 is conflict-free and
 //                 every address is a per-lane base plus an immediate offset
-//   MAC           O_j += D_r (.) BSK_i[r][j], 4 fma per complex, r = c*3 + l ascending
+//   MAC           O_j += D_(c,l) (.) BSK_i[(c,l)][j], 4 fma per complex; c ascending, levels least
+//                 significant first (each level's digits come off a running carry state, so the device
+//                 BSK stores the level rows of each component reversed)
 //   inverse       conjugate passes, untwist by conj(zeta^j), rint, mod 2^64, add to the accumulator
 // Coefficient 64 e + L of a u64 register polynomial (slot e of lane L, e < 16) meets coefficient
 // 64 (e + 8) + L in the same lane, so folding and unfolding move no data.
@@ -182,13 +184,14 @@ __device__ __forceinline__ double i64_to_f64(u64 x) {
 }
 
 // rint(x) mod 2^64 (every step after the rint is exact)
+// h = floor(t / 2^32) is an integer with |h| < 2^51, so h + 1.5 * 2^52 is exact and its low
+// mantissa word is h mod 2^32
 __device__ __forceinline__ u64 f64_to_torus(double x) {
   const double t = __builtin_rint(x);
   const double h = __builtin_floor(t * 0x1p-32);
   const double l = __builtin_fma(-h, 0x1p32, t);
-  const double hh = __builtin_floor(h * 0x1p-32);
-  const double hm = __builtin_fma(-hh, 0x1p32, h);
-  return ((u64)(u32)hm << 32) | (u64)(u32)l;
+  const u32 hm = (u32)__double_as_longlong(h + 0x1.8p52);
+  return ((u64)hm << 32) | (u64)(u32)l;
 }
 
 // forward transform of a real polynomial held as 16 doubles per lane (slot e <-> coefficient 64 e + L)
@@ -213,20 +216,18 @@ __device__ __forceinline__ void fft_inv_real(double (&xr)[8], double (&xi)[8], d
 
 __device__ __forceinline__ int ms2048(u64 x) { return (int)((((x >> 52) + 1) >> 1) & 2047u); }
 
-// tfhe-rs SignedDecomposer 2^7 x 3 on a torus value: signed bytes d, byte l = level l (0 = MSB)
-__device__ __forceinline__ u32 decomp_7x3_t(u64 x) {
-  u32 state = (u32)(((x >> 42) + 1) >> 1) & 0x1FFFFFu;
-  u32 packed = 0;
-#pragma unroll
-  for (int l = 2; l >= 0; l--) {
-    const u32 res = state & 127u;
-    state >>= 7;
-    const u32 carry = ((((res - 1u) | state) & res) >> 6) & 1u;
-    state += carry;
-    const int d = (int)res - (int)(carry << 7);
-    packed |= ((u32)d & 0xFFu) << (8 * l);
-  }
-  return packed;
+// tfhe-rs SignedDecomposer 2^7 x 3 (closest_representable at 21 bits, balanced digits, carry
+// rule carry = (((res - 1) | state) & res) >> 6), restated as one step per level, least significant
+// first, on the running state st (21 bits to start; == or_decompose for every state, tests/test_fft.py):
+//   b = bit 13 of st (level 2 and 1; 0 for the top level), W = st + 63 + b,
+//   digit = (W & 127) - 63 - b, st' = W >> 7
+__device__ __forceinline__ u32 decomp_state(u64 x) { return ((u32)(x >> 32) + 1024u) >> 11; }
+// bmask = 1 below the top level, 0 at the top level
+__device__ __forceinline__ int decomp_step(u32& st, u32 bmask) {
+  const u32 b = (st >> 13) & bmask;
+  const u32 W = st + 63u + b;
+  st = W >> 7;
+  return (int)(W & 127u) - 63 - (int)b;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -236,13 +237,14 @@ __global__ __launch_bounds__(64) void bsk_to_fourier_kernel(const u64* __restric
                                                             const double2* __restrict__ tw) {
   __shared__ __attribute__((aligned(16))) double2 T[T_C64];
   const int lane = threadIdx.x;
-  const size_t q = blockIdx.x;
+  const size_t q = blockIdx.x;  // standard layout [i][c*3 + l][j]
   const u64* src = bsk_std + q * N1K;
   double a[16], xr[8], xi[8];
 #pragma unroll
   for (int e = 0; e < 16; e++) a[e] = i64_to_f64(src[64 * e + lane]);
   fft_fwd_real(a, xr, xi, T, lane, tw);
-  double2* dst = bsk_f + q * M;
+  const size_t j = q % 2, r = (q / 2) % 6, i = q / 12;  // device layout [i][c*3 + (2 - l)][j]
+  double2* dst = bsk_f + ((i * 6 + (r / 3) * 3 + (2 - r % 3)) * 2 + j) * M;
 #pragma unroll
   for (int e = 0; e < 8; e++) dst[64 * e + lane] = make_double2(xr[e] * 0x1p-9, xi[e] * 0x1p-9);
 }
@@ -317,25 +319,26 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rba
   for (int e = 0; e < 16; e++) Tu[64 * e + lane] = acc[e];
   wave_lds_sync();
   // (X^a acc)[64 e + L] = +-acc[(t mod 1024)], t = 64 e + L - a + 2048: negated iff t in [1024, 2048)
-  u32 dig[16];
+  u32 st[16];
 #pragma unroll
   for (int e = 0; e < 16; e++) {
     const int t = rbase + 64 * e;
     const u64 x = Tu[t & (N1K - 1)];
     const u64 r = (t & N1K) ? 0 - x : x;
-    dig[e] = decomp_7x3_t(r - acc[e]);
+    st[e] = decomp_state(r - acc[e]);
   }
   wave_lds_sync();
 #pragma unroll 1
-  for (int l = 0; l < 3; l++) {
-    const int g = i * 6 + c * 3 + l;
+  for (int q = 0; q < 3; q++) {  // level 2 - q: least significant first
+    const int g = i * 6 + c * 3 + q;
     glds_barrier();
     if (g + 1 < n_steps) load_chunk(bsk, g + 1, sh.K[(g + 1) & 1], wave, lane);
+    const u32 bmask = q < 2 ? 1u : 0u;
     double xr[8], xi[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) {
-      xr[e] = (double)((int)(dig[e] << (24 - 8 * l)) >> 24);
-      xi[e] = (double)((int)(dig[e + 8] << (24 - 8 * l)) >> 24);
+      xr[e] = (double)decomp_step(st[e], bmask);
+      xi[e] = (double)decomp_step(st[e + 8], bmask);
       cmul<false>(xr[e], xi[e], sh.tw[TW_TWIST + 64 * e + lane]);
     }
     dft512_fwd(xr, xi, T, lane, tb, sh.tw);
