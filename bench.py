@@ -3,9 +3,11 @@
 
 One step = one full programmable bootstrap (blind rotate -> sample extract -> keyswitch) of a
 batch of 4096 independent LWE ciphertexts per GPU, P-GATE parameters (n=630, k=1, N=1024,
-PBS 2^7 x 3, KS 2^2 x 8), inputs resident in HBM before the timed region.
+PBS 2^7 x 3, KS 2^2 x 8), inputs resident in HBM before the timed region.  The default transform is
+FFT64 (tfhe-rs's arithmetic: f64 negacyclic FFT external product over the native 2^64 torus,
+pbs_fft.hip); --preset gate runs the same workload on the Goldilocks NTT transform (pbs_kernels.hip).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--cpu-sample S] [--preset gate|fhevm]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--cpu-sample S] [--preset gate_fft|gate|fhevm]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 Multi-GPU: weak scaling.  Rank 0 generates the key set, uploads it to its GPU and broadcasts the
@@ -61,13 +63,12 @@ def pmc_traffic(B: int, kernel: str = "blind_rotate_kernel"):
     """HBM bytes per blind-rotate launch from the committed rocprofv3 PMC passes
     (profiles/*_pmc_blind_rotate.json, produced by tools/pmc_summary.py for this same command), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_blind_rotate.json")))
-    if not files or B != 4096:
+    if B != 4096:
         return None
-    d = json.load(open(files[-1]))
-    for k, v in d.items():
-        if kernel in k:
-            return round(v["hbm_bytes_per_launch"])
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_blind_rotate.json")), reverse=True):
+        for k, v in json.load(open(f)).items():  # the newest pass that profiled this kernel
+            if k.split("<")[0].endswith("::" + kernel):
+                return round(v["hbm_bytes_per_launch"])
     return None
 
 
@@ -78,18 +79,20 @@ def valu_profile(B: int, kernel_ms: float, kernel: str = "blind_rotate_kernel"):
     the measured launch (1024 SIMDs at 2.4 GHz, MI355X_MICROARCH.md)."""
     import csv
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_sq.csv")))
-    if not files:
-        return None
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(files[-1]))
-            if r["Counter_Name"] == "SQ_INSTS_VALU" and kernel in r["Kernel_Name"]]
+    vals, src = [], None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_sq.csv")), reverse=True):
+        vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(f)) if r["Counter_Name"] == "SQ_INSTS_VALU"
+                and r["Kernel_Name"].split("(")[0].split("<")[0].endswith("::" + kernel)]
+        if vals:  # the newest pass that profiled this kernel
+            src = f
+            break
     if not vals:
         return None
     insts = sum(vals) / len(vals) / 4096 * B
     frac = insts * 4 / (1024 * 2.4e9 * kernel_ms * 1e-3)
     return {"bound": "valu", "insts_per_launch": round(insts), "insts_per_pbs": round(insts / B),
             "issue_frac": round(frac, 3), "model": "4 cycles per wave64 VALU instruction per SIMD, 1024 SIMDs, 2.4 GHz",
-            "source": os.path.relpath(files[-1], ROOT)}
+            "source": os.path.relpath(src, ROOT)}
 
 
 def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int, preset: int = 0,
@@ -131,9 +134,10 @@ def main() -> int:
     ap.add_argument("--cpu-sample", type=int, default=0, help="PBS in the CPU baseline sample (0 = auto)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on GPUs; gloo only for rehearsals")
-    ap.add_argument("--preset", choices=["gate", "gate_fft", "fhevm"], default="gate",
-                    help="gate = the BASELINE metric (P-GATE, NTT transform); gate_fft = P-GATE on the FFT64 transform "
-                         "(tfhe-rs's f64 FFT); fhevm = production fhEVM parameters (secondary line)")
+    ap.add_argument("--preset", choices=["gate", "gate_fft", "fhevm"], default="gate_fft",
+                    help="gate_fft (default) = the BASELINE metric on the FFT64 transform (P-GATE, tfhe-rs's f64-FFT "
+                         "external product over the native torus); gate = P-GATE on the Goldilocks NTT transform; "
+                         "fhevm = production fhEVM parameters (secondary line)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses device 0 (with --dist-backend gloo)")
     args = ap.parse_args()

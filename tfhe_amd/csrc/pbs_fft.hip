@@ -41,6 +41,22 @@ constexpr int T_C64 = 576;        // per-wave transpose scratch (9,216 B; also h
 constexpr int TW_TWIST = 0, TW_A = 512, TW_B = 1024, TW_I = 1536, TW_C64 = 2048;  // table offsets (complex)
 constexpr double SQRT1_2 = 0.70710678118654752440;
 
+// Order between a wave's own LDS writes and reads of its private scratch.  DS instructions of one
+// wavefront execute in issue order, so a compiler-only fence would do (FFT_LDS_WAIT=0); measured on
+// MI355X it is 4 % SLOWER (31.97 vs 30.71 ms per 4096-PBS blind rotation: hipcc then interleaves the
+// transpose reads with the butterflies and stalls on them one by one), so the full lgkmcnt(0) drain
+// stays the default.
+#ifndef FFT_LDS_WAIT
+#define FFT_LDS_WAIT 1
+#endif
+__device__ __forceinline__ void lds_order() {
+#if FFT_LDS_WAIT
+  wave_lds_sync();
+#else
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#endif
+}
+
 // z * w (INV: z * conj(w)), the oracle's cmul(z, w.re, +-w.im)
 template <bool INV>
 __device__ __forceinline__ void cmul(double& re, double& im, double2 w) {
@@ -122,27 +138,27 @@ __device__ __forceinline__ void dft512_fwd(double (&xr)[8], double (&xi)[8], dou
   for (int e = 1; e < 8; e++) cmul<false>(xr[e], xi[e], tw[TW_A + 64 * e + lane]);
 #pragma unroll
   for (int e = 0; e < 8; e++) T[lane + S1 * e] = make_double2(xr[e], xi[e]);
-  wave_lds_sync();
+  lds_order();
 #pragma unroll
   for (int e = 0; e < 8; e++) {
     const double2 v = T[tb.b1 + 8 * e];
     xr[e] = v.x;
     xi[e] = v.y;
   }
-  wave_lds_sync();
+  lds_order();
   dft8<false>(xr, xi);
 #pragma unroll
   for (int e = 1; e < 8; e++) cmul<false>(xr[e], xi[e], tw[TW_B + 64 * e + lane]);
 #pragma unroll
   for (int e = 0; e < 8; e++) T[lane + S2 * e] = make_double2(xr[e], xi[e]);
-  wave_lds_sync();
+  lds_order();
 #pragma unroll
   for (int e = 0; e < 8; e++) {
     const double2 v = T[tb.b2 + e];
     xr[e] = v.x;
     xi[e] = v.y;
   }
-  wave_lds_sync();
+  lds_order();
   dft8<false>(xr, xi);
 }
 
@@ -154,27 +170,27 @@ __device__ __forceinline__ void dft512_inv(double (&xr)[8], double (&xi)[8], dou
   for (int e = 1; e < 8; e++) cmul<true>(xr[e], xi[e], tw[TW_B + 64 * e + lane]);
 #pragma unroll
   for (int e = 0; e < 8; e++) T[tb.b2 + e] = make_double2(xr[e], xi[e]);
-  wave_lds_sync();
+  lds_order();
 #pragma unroll
   for (int e = 0; e < 8; e++) {
     const double2 v = T[lane + S2 * e];
     xr[e] = v.x;
     xi[e] = v.y;
   }
-  wave_lds_sync();
+  lds_order();
   dft8<true>(xr, xi);
 #pragma unroll
   for (int e = 0; e < 8; e++) cmul<true>(xr[e], xi[e], tw[TW_I + 64 * e + lane]);
 #pragma unroll
   for (int e = 0; e < 8; e++) T[tb.b1 + 8 * e] = make_double2(xr[e], xi[e]);
-  wave_lds_sync();
+  lds_order();
 #pragma unroll
   for (int e = 0; e < 8; e++) {
     const double2 v = T[lane + S1 * e];
     xr[e] = v.x;
     xi[e] = v.y;
   }
-  wave_lds_sync();
+  lds_order();
   dft8<true>(xr, xi);
 }
 
@@ -317,7 +333,7 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rba
   u64* Tu = (u64*)T;
 #pragma unroll
   for (int e = 0; e < 16; e++) Tu[64 * e + lane] = acc[e];
-  wave_lds_sync();
+  lds_order();
   // (X^a acc)[64 e + L] = +-acc[(t mod 1024)], t = 64 e + L - a + 2048: negated iff t in [1024, 2048)
   u32 st[16];
 #pragma unroll
@@ -327,7 +343,7 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rba
     const u64 r = (t & N1K) ? 0 - x : x;
     st[e] = decomp_state(r - acc[e]);
   }
-  wave_lds_sync();
+  lds_order();
 #pragma unroll 1
   for (int q = 0; q < 3; q++) {  // level 2 - q: least significant first
     const int g = i * 6 + c * 3 + q;

@@ -1,13 +1,8 @@
 #!/bin/bash
-# Build a variant of libtfhe_hip.so into build_ab/<name>/ with extra hipcc flags (kernel A/B tests).
+# Build a variant of libtfhe_hip.so into build_ab/<name>/ with extra hipcc flags (kernel A/B tests;
+# tools/ab_run.sh benches every variant on the GPU box).
 # usage: tools/ab_build.sh <name> [extra hipcc flags...]
 set -e
 NAME=$1; shift
-OUT=build_ab/$NAME
-mkdir -p $OUT
-H="/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -mcode-object-version=5"
-$H "$@" -I tfhe_amd/csrc -c ${KSRC:-tfhe_amd/csrc/pbs_kernels.hip} -o $OUT/pbs_kernels.o
-$H -x hip -c tfhe_amd/csrc/api.cpp -o $OUT/api.o
-g++ -O2 -fPIC -std=c++17 -ffp-contract=off -c tfhe_amd/csrc/client.cpp -o $OUT/client.o
-$H -shared -fPIC --offload-arch=gfx950 -o $OUT/libtfhe_hip.so $OUT/pbs_kernels.o $OUT/api.o $OUT/client.o -pthread
-echo built $OUT/libtfhe_hip.so
+make -s -C tfhe_amd -j8 B=../build_ab/$NAME/obj LIB=../build_ab/$NAME/libtfhe_hip.so EXTRA="$*"
+echo built build_ab/$NAME/libtfhe_hip.so
