@@ -2,6 +2,7 @@
 // launch sequencing, error reporting.  Host code; kernels live in pbs_kernels.hip.
 #include <hip/hip_runtime_api.h>
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -80,6 +81,8 @@ struct tfhe_ctx {
   hipStream_t stream = nullptr;
   u64* d_bsk = nullptr;  // NTT layout, x N^-1
   u64* d_ksk = nullptr;
+  void* d_ks_planes = nullptr;  // KSK recoded into 8 signed byte planes (ks_mfma.hip)
+  bool ks_valu = false;         // TFHE_HIP_KS_VALU=1: the VALU keyswitch kernel instead (A/B runs)
   u64* d_tw = nullptr;  // 4 x 1024 twiddle tables of the device NTT layout
   u64 ninv = 0;
   bool keys = false;
@@ -93,6 +96,8 @@ struct tfhe_ctx {
   size_t big_cap = 0;  // u64 elements
   void* d_stage = nullptr;
   size_t stage_cap = 0;  // bytes
+  void* d_ks_dig = nullptr;
+  size_t ks_dig_cap = 0;  // bytes
   std::mutex mu;
   // timing
   bool timing = false;
@@ -182,8 +187,14 @@ hipError_t launch_ms(tfhe_ctx* c, u64* small, size_t B, int* picks, hipStream_t 
 }
 
 hipError_t launch_ks(tfhe_ctx* c, const u64* in_big, size_t B, u64* out, hipStream_t s) {
-  return tfhe::launch_keyswitch(in_big, B, (int)(c->p.k * c->p.N), c->d_ksk, (int)c->p.n, (int)c->p.ks_base_log,
-                                (int)c->p.ks_level, out, s);
+  const int big_dim = (int)(c->p.k * c->p.N);
+  if (c->ks_valu || !c->d_ks_planes)
+    return tfhe::launch_keyswitch(in_big, B, big_dim, c->d_ksk, (int)c->p.n, (int)c->p.ks_base_log,
+                                  (int)c->p.ks_level, out, s);
+  if (grow(&c->d_ks_dig, &c->ks_dig_cap, tfhe::ks_digits_bytes(B, big_dim, (int)c->p.ks_level)))
+    return hipErrorOutOfMemory;
+  return tfhe::launch_keyswitch_mfma(in_big, B, big_dim, c->d_ks_planes, (int)c->p.n, (int)c->p.ks_base_log,
+                                     (int)c->p.ks_level, c->d_ks_dig, out, s);
 }
 
 // PBS on device buffers (caller holds c->mu, device set).  Order 0 (P-GATE): BR + SE -> KS;
@@ -346,6 +357,10 @@ int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out) {
   c->p = *p;
   c->device = device;
   c->lat_max = p->N == 2048 ? 512 : 1024;  // measured crossovers (tools/latency_sweep.py)
+  {
+    const char* e = getenv("TFHE_HIP_KS_VALU");
+    c->ks_valu = e && e[0] == '1';
+  }
   auto cleanup = [&](int rc) {
     tfhe_hip_destroy(c);
     return rc;
@@ -388,6 +403,8 @@ void tfhe_hip_destroy(tfhe_ctx* c) {
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     (void)hipFree(c->d_bsk);
     (void)hipFree(c->d_ksk);
+    (void)hipFree(c->d_ks_planes);
+    (void)hipFree(c->d_ks_dig);
     (void)hipFree(c->d_tw);
     (void)hipFree(c->d_ms_zeros);
     (void)hipFree(c->d_big);
@@ -411,6 +428,12 @@ static int load_keys_impl(tfhe_ctx* c, const uint64_t* bsk, size_t bsk_len, cons
   if (!c->d_bsk) HIP_TRY(hipMalloc(&c->d_bsk, bsk_len * 8));
   if (!c->d_ksk) HIP_TRY(hipMalloc(&c->d_ksk, ksk_len * 8));
   HIP_TRY(hipMemcpyAsync(c->d_ksk, ksk, ksk_len * 8, kind, c->stream));
+  if (!c->ks_valu) {  // byte planes of the KSK for the matrix-core keyswitch
+    const int big_dim = (int)(c->p.k * c->p.N);
+    if (!c->d_ks_planes)
+      HIP_TRY(hipMalloc(&c->d_ks_planes, tfhe::ks_planes_bytes(big_dim, (int)c->p.ks_level, (int)c->p.n)));
+    HIP_TRY(tfhe::launch_ksk_planes(c->d_ksk, big_dim, (int)c->p.ks_level, (int)c->p.n, c->d_ks_planes, c->stream));
+  }
   // standard-domain BSK staged in the workspace, converted in one launch
   void* tmp = nullptr;
   if (kind == hipMemcpyHostToDevice) {

@@ -19,6 +19,13 @@ hipError_t launch_keyswitch(const u64* in_big, size_t B, int big_dim, const u64*
                            u64* out, hipStream_t s);
 hipError_t launch_ntt_fwd(u64* polys, size_t count, const u64* tw, hipStream_t s);
 hipError_t launch_ntt_inv(u64* polys, size_t count, const u64* tw, u64 ninv, hipStream_t s);
+// keyswitch as eight int8 GEMMs on the matrix cores (ks_mfma.hip): KSK byte planes built once per key
+// load, digits staged in a workspace of ks_digits_bytes(B, ...) bytes
+size_t ks_planes_bytes(int big_dim, int levels, int n);
+size_t ks_digits_bytes(size_t B, int big_dim, int levels);
+hipError_t launch_ksk_planes(const u64* ksk, int big_dim, int levels, int n, void* planes, hipStream_t s);
+hipError_t launch_keyswitch_mfma(const u64* in_big, size_t B, int big_dim, const void* planes, int n, int base_log,
+                                 int levels, void* digits, u64* out, hipStream_t s);
 
 // FFT64 transform (pbs_fft.hip), N = 1024: tables = 1536 complex (twist | pass A | pass B);
 // Fourier BSK = polys x 512 complex
