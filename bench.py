@@ -292,8 +292,10 @@ def main() -> int:
         }
         if world == 1 and not args.no_cpu:
             threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-            # ~10-20 s of CPU work: the oracle does ~3.5 PBS/s per thread at P-GATE (~1.3 at P-FHEVM)
-            sample = args.cpu_sample or (max(16 * threads, 32) if fhevm else max(40 * threads, 64))
+            # ~10-20 s of CPU work: the oracle does ~3.5 PBS/s per thread on the NTT at P-GATE, ~23 on
+            # FFT64, ~1.3 at P-FHEVM
+            sample = args.cpu_sample or (max(16 * threads, 32) if fhevm else max(240 * threads, 64) if fft
+                                         else max(40 * threads, 64))
             cb, exact = cpu_baseline(cts, out, min(sample, B), threads, 1 if fhevm else 2 if fft else 0,
                                      lut_host if fhevm else None)
             result["cpu_baseline"] = cb

@@ -303,14 +303,24 @@ __global__ __launch_bounds__(64) void fft_inv_kernel(const double2* __restrict__
 
 // ---------------------------------------------------------------------------------------------
 // Blind rotation + sample extraction (batch kernel): workgroup = 8 wavefronts = 8 ciphertexts.
+// BSK chunk buffers: 2 = one level step in flight (default); 3 keeps two in flight (chunk g + 2 issued
+// while step g computes, the barrier before step g waits only for chunk g with a counted vmcnt):
+// measured 3 % slower on MI355X (31.2 vs 30.35 ms per 4096; the chunk arrives in time either way and
+// the third buffer costs registers), kept for A/B runs.
+#ifndef FFT_KBUF
+#define FFT_KBUF 2
+#endif
 constexpr int FB_WAVES = 8;
 constexpr int FB_THREADS = 64 * FB_WAVES;
 constexpr int CHUNK_C64 = 2 * M;                   // one level step: rows (c, l), j = 0, 1 (16 KB)
 constexpr int CHUNK_GLDS = CHUNK_C64 * 16 / 1024;  // 1 KB wave-instructions per chunk (16)
+// s_waitcnt vmcnt(CHUNK_GLDS / FB_WAVES): a wave issues that many global_load_lds per chunk
+// (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] = 7 | lgkmcnt[11:8] = 15 | vmcnt[5:4] in [15:14])
+[[maybe_unused]] constexpr int VMCNT_CHUNK = 0x0F70 | (CHUNK_GLDS / 8);
 
 struct FftShared {
   double2 T[FB_WAVES][T_C64];  // per-wave transpose / rotation scratch  72 KB
-  double2 K[2][CHUNK_C64];     // double-buffered BSK chunk              32 KB
+  double2 K[FFT_KBUF][CHUNK_C64];  // BSK level-step chunks in flight   16 KB each
   double2 tw[TW_C64];          // twist | pass A | pass B | inverse B'   32 KB
 };
 
@@ -347,8 +357,18 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rba
 #pragma unroll 1
   for (int q = 0; q < 3; q++) {  // level 2 - q: least significant first
     const int g = i * 6 + c * 3 + q;
+#if FFT_KBUF == 3
+    // chunk g is complete once at most chunk g + 1's loads (issued one step ago) are outstanding
+    // raw s_barrier: __syncthreads()'s fence would drain vmcnt(0), chunk g + 1 included
+    if (g + 1 < n_steps) __builtin_amdgcn_s_waitcnt(VMCNT_CHUNK);
+    else __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    if (g + 2 < n_steps) load_chunk(bsk, g + 2, sh.K[(g + 2) % 3], wave, lane);
+#else
     glds_barrier();
     if (g + 1 < n_steps) load_chunk(bsk, g + 1, sh.K[(g + 1) & 1], wave, lane);
+#endif
     const u32 bmask = q < 2 ? 1u : 0u;
     double xr[8], xi[8];
 #pragma unroll
@@ -358,8 +378,8 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rba
       cmul<false>(xr[e], xi[e], sh.tw[TW_TWIST + 64 * e + lane]);
     }
     dft512_fwd(xr, xi, T, lane, tb, sh.tw);
-    const double2* k0 = sh.K[g & 1] + lane;
-    const double2* k1 = sh.K[g & 1] + M + lane;
+    const double2* k0 = sh.K[g % FFT_KBUF] + lane;
+    const double2* k1 = sh.K[g % FFT_KBUF] + M + lane;
 #pragma unroll
     for (int e = 0; e < 8; e++) {
       const double2 u = k0[64 * e], v = k1[64 * e];
@@ -402,6 +422,9 @@ __global__ __launch_bounds__(FB_THREADS, 1) void blind_rotate_fft_kernel(
 
   for (int q = threadIdx.x; q < TW_C64; q += FB_THREADS) sh.tw[q] = tw_g[q];
   load_chunk(bsk, 0, sh.K[0], wave, lane);
+#if FFT_KBUF == 3
+  if (n_steps > 1) load_chunk(bsk, 1, sh.K[1], wave, lane);
+#endif
 
   // acc = (0, X^{-b~} * lut): LUT values arrive in the Z_p encoding, mapped to the torus first
   u64 accA[16], accB[16];

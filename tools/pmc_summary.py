@@ -16,7 +16,7 @@ def per_kernel(path):
     rows = list(csv.DictReader(open(path + "/run_counter_collection.csv")))
     agg = {}
     for r in rows:
-        k = (r["Kernel_Name"].split("(")[0], r["Counter_Name"])
+        k = (r["Kernel_Name"].replace("(anonymous namespace)", "anon").split("(")[0], r["Counter_Name"])
         agg.setdefault(k, []).append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
