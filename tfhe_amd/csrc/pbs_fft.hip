@@ -239,11 +239,13 @@ __device__ __forceinline__ int ms2048(u64 x) { return (int)((((x >> 52) + 1) >> 
 //   digit = (W & 127) - 63 - b, st' = W >> 7
 __device__ __forceinline__ u32 decomp_state(u64 x) { return ((u32)(x >> 32) + 1024u) >> 11; }
 // bmask = 1 below the top level, 0 at the top level
+// (W & 127) - 63 - b = st - (W & ~127): the digit is the old state minus the new one shifted back
 __device__ __forceinline__ int decomp_step(u32& st, u32 bmask) {
-  const u32 b = (st >> 13) & bmask;
+  const u32 b = __builtin_amdgcn_ubfe(st, 13, bmask);
   const u32 W = st + 63u + b;
+  const int d = (int)(st - (W & ~127u));  // 5 VALU per digit with the bfe, add3 and shift
   st = W >> 7;
-  return (int)(W & 127u) - 63 - (int)b;
+  return d;
 }
 
 // ---------------------------------------------------------------------------------------------
