@@ -7,7 +7,7 @@ PBS 2^7 x 3, KS 2^2 x 8), inputs resident in HBM before the timed region.  The d
 FFT64 (tfhe-rs's arithmetic: f64 negacyclic FFT external product over the native 2^64 torus,
 pbs_fft.hip); --preset gate runs the same workload on the Goldilocks NTT transform (pbs_kernels.hip).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--cpu-sample S] [--preset gate_fft|gate|fhevm]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--cpu-sample S] [--preset gate_fft|gate|fhevm|fhevm_fft]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 Multi-GPU: weak scaling.  Rank 0 generates the key set, uploads it to its GPU and broadcasts the
@@ -118,8 +118,9 @@ def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int
         "unit": "PBS/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{sample} PBS of the same {('P-GATE', 'P-FHEVM', 'P-GATE FFT64')[preset]} batch (first {sample} "
-                  f"ciphertexts), C oracle ({'oracle/fft_oracle.c' if preset == 2 else 'oracle/tfhe_oracle.c'}, -O3 "
+        "sample": f"{sample} PBS of the same {('P-GATE', 'P-FHEVM', 'P-GATE FFT64', 'P-FHEVM FFT64')[preset]} batch "
+                  f"(first {sample} ciphertexts), C oracle "
+                  f"({'oracle/fft_oracle.c' if prm.transform == 1 else 'oracle/tfhe_oracle.c'}, -O3 "
                   f"-march=x86-64-v3, OpenMP {threads} threads, one PBS per thread), "
                   f"{dt:.1f}s",
     }, bool(np.array_equal(ref, gpu_out[:sample]))
@@ -134,10 +135,10 @@ def main() -> int:
     ap.add_argument("--cpu-sample", type=int, default=0, help="PBS in the CPU baseline sample (0 = auto)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on GPUs; gloo only for rehearsals")
-    ap.add_argument("--preset", choices=["gate", "gate_fft", "fhevm"], default="gate_fft",
+    ap.add_argument("--preset", choices=["gate", "gate_fft", "fhevm", "fhevm_fft"], default="gate_fft",
                     help="gate_fft (default) = the BASELINE metric on the FFT64 transform (P-GATE, tfhe-rs's f64-FFT "
                          "external product over the native torus); gate = P-GATE on the Goldilocks NTT transform; "
-                         "fhevm = production fhEVM parameters (secondary line)")
+                         "fhevm / fhevm_fft = production fhEVM parameters on the NTT / FFT64 transform (secondary line)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses device 0 (with --dist-backend gloo)")
     args = ap.parse_args()
@@ -158,11 +159,13 @@ def main() -> int:
         else:
             dist.init_process_group(args.dist_backend)
 
-    fhevm = args.preset == "fhevm"
-    fft = args.preset == "gate_fft"
-    params = tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM if fhevm else
-                                    tfhe_amd.PRESET_GATE_FFT if fft else tfhe_amd.PRESET_GATE)
-    br_kernel = "blind_rotate2048_kernel" if fhevm else "blind_rotate_fft_kernel" if fft else "blind_rotate_kernel"
+    fhevm = args.preset in ("fhevm", "fhevm_fft")
+    fft = args.preset in ("gate_fft", "fhevm_fft")
+    preset_id = {"gate": tfhe_amd.PRESET_GATE, "gate_fft": tfhe_amd.PRESET_GATE_FFT, "fhevm": tfhe_amd.PRESET_FHEVM,
+                 "fhevm_fft": tfhe_amd.PRESET_FHEVM_FFT}[args.preset]
+    params = tfhe_amd.Params.preset(preset_id)
+    br_kernel = {"gate": "blind_rotate_kernel", "gate_fft": "blind_rotate_fft_kernel",
+                 "fhevm": "blind_rotate2048_kernel", "fhevm_fft": "blind_rotate_fft2k_kernel"}[args.preset]
     br_bytes = BR_BYTES_PER_PBS_FHEVM if fhevm else BR_BYTES_PER_PBS
     B = args.batch
 
@@ -267,7 +270,8 @@ def main() -> int:
                              + (", FFT64 transform (f64 FFT over the 2^64 torus)" if fft else ", NTT transform (Z_p)"))
                             if not fhevm else
                             ("P-FHEVM PBS (keyswitch + blind rotate + sample extract), n=918 k=1 N=2048, "
-                             f"PBS 2^23x1, KS 2^4x4, batch {B} per GPU"),
+                             f"PBS 2^23x1, KS 2^4x4, batch {B} per GPU"
+                             + (", FFT64 transform (f64 FFT over the 2^64 torus)" if fft else ", NTT transform (Z_p)")),
                 "batch_per_gpu": B,
                 "params": params.as_dict(),
                 "parallelism": f"batch-sharded x{world}, BSK/KSK RCCL broadcast once",
@@ -294,9 +298,10 @@ def main() -> int:
             threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
             # ~10-20 s of CPU work: the oracle does ~3.5 PBS/s per thread on the NTT at P-GATE, ~23 on
             # FFT64, ~1.3 at P-FHEVM
-            sample = args.cpu_sample or (max(16 * threads, 32) if fhevm else max(240 * threads, 64) if fft
+            sample = args.cpu_sample or (max(96 * threads, 32) if fhevm and fft else max(16 * threads, 32) if fhevm
+                                         else max(240 * threads, 64) if fft
                                          else max(40 * threads, 64))
-            cb, exact = cpu_baseline(cts, out, min(sample, B), threads, 1 if fhevm else 2 if fft else 0,
+            cb, exact = cpu_baseline(cts, out, min(sample, B), threads, preset_id,
                                      lut_host if fhevm else None)
             result["cpu_baseline"] = cb
             result["sample_bitexact"] = exact

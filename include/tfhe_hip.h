@@ -44,6 +44,7 @@ extern "C" {
 #define TFHE_HIP_PRESET_GATE 0   /* n=630 k=1 N=1024, PBS 7x3, KS 2x8 (TFHE 128-bit default) */
 #define TFHE_HIP_PRESET_FHEVM 1  /* n=918 k=1 N=2048, PBS 23x1, KS 4x4 (PARAM_MESSAGE_2_CARRY_2_KS_PBS) */
 #define TFHE_HIP_PRESET_GATE_FFT 2 /* P-GATE on the FFT64 transform (native-torus BSK, f64 FFT) */
+#define TFHE_HIP_PRESET_FHEVM_FFT 3 /* P-FHEVM on the FFT64 transform (N = 2048 as two 512-point halves) */
 
 #define TFHE_HIP_TRANSFORM_NTT 0   /* GLWE/BSK over Z_p, Goldilocks NTT (exact integer arithmetic) */
 #define TFHE_HIP_TRANSFORM_FFT64 1 /* GLWE/BSK over Z_2^64, f64 FFT (tfhe-rs FFT64; oracle/fft_oracle.c) */

@@ -29,6 +29,13 @@
  *                    C': lane k1 + 8 k0 transforms k2 -> n0, x[n0] *= conj(w^{8 n0 k1})   (n0 > 0)
  *                    B': lane n0 + 8 k0 transforms k1 -> n1, x[n1] *= conj(w^{k0 (n0 + 8 n1)}) (all)
  *                    A': lane n0 + 8 n1 transforms k0 -> n2 = z[L + 64 n2]
+ *   N = 2048         (P-FHEVM, preset 3) two 512-point halves: z_j = (a_j + i a_{j+1024}) zeta^j,
+ *                    zeta = e^{i pi/2048}; E_h = the 512-point DFT above of z_{2m+h} (h = 0, 1), then
+ *                    t = cmul(E_1[k'], w^k'), w = e^{2 pi i/1024}: Z[k'] = E_0 + t, Z[k'+512] = E_0 - t.
+ *                    Device order of the spectrum (two waves per polynomial): index h*512 + 64 s + L
+ *                    holds frequency k'(L, 4h + (s & 3)) + 512 (s >> 2), k'(L, e) = (L>>3) + 8 (L&7) + 64 e.
+ *                    Inverse: E_0 = lo + hi, E_1 = cmul(lo - hi, conj(w^k')), the 512-point inverses,
+ *                    untwist by conj(zeta^{2m+h}).  1/M = 2^-10 folded into the BSK.
  *   MAC              re = fma(D.re, K.re, re); re = fma(-D.im, K.im, re);
  *                    im = fma(D.re, K.im, im); im = fma(D.im, K.re, im)   from (0, 0), over
  *                    c = 0..k and, within c, the levels least significant first (l = L-1 .. 0:
@@ -207,7 +214,76 @@ static void dft512_inv(const or_c64* in, or_c64* out) {
   }
 }
 
+/* ---- N = 2048: two 512-point halves + one combine pass ------------------------------------ */
+typedef struct fft2k_tab {
+  or_c64 twist[2 * FFT_M];  /* zeta^j, zeta = e^{i pi / 2048} */
+  or_c64 wc[2][4][64];      /* w^{k'(L, 4h + p)}, w = e^{2 pi i / 1024} */
+} fft2k_tab;
+static fft2k_tab g_tab2k;
+static int g_tab2k_ready = 0;
+
+static int kdev(int L, int e) { return (L >> 3) + 8 * (L & 7) + 64 * e; } /* device-order frequency */
+
+static const fft2k_tab* tab2k(void) {
+#pragma omp critical(or_fft_tab2k)
+  {
+    if (!g_tab2k_ready) {
+      for (uint32_t j = 0; j < 2 * FFT_M; j++) or_fft_twiddle(j, 4096, &g_tab2k.twist[j].re, &g_tab2k.twist[j].im);
+      for (int h = 0; h < 2; h++)
+        for (int q = 0; q < 4; q++)
+          for (int L = 0; L < 64; L++)
+            or_fft_twiddle((uint32_t)kdev(L, 4 * h + q), 1024, &g_tab2k.wc[h][q][L].re, &g_tab2k.wc[h][q][L].im);
+      __atomic_store_n(&g_tab2k_ready, 1, __ATOMIC_RELEASE);
+    }
+  }
+  return &g_tab2k;
+}
+
+static void fft2k_fwd(const double* a, or_c64* out) {
+  const fft2k_tab* T = tab2k();
+  or_c64 z[2][FFT_M], E[2][FFT_M];
+  for (int h = 0; h < 2; h++) {
+    for (int m = 0; m < FFT_M; m++) {
+      const int j = 2 * m + h;
+      const or_c64 v = {a[j], a[j + 2 * FFT_M]};
+      z[h][m] = cmul(v, T->twist[j].re, T->twist[j].im);
+    }
+    dft512_fwd(z[h], E[h]);
+  }
+  for (int h = 0; h < 2; h++)
+    for (int q = 0; q < 4; q++)
+      for (int L = 0; L < 64; L++) {
+        const int d = L + 64 * (4 * h + q);
+        const or_c64 t = cmul(E[1][d], T->wc[h][q][L].re, T->wc[h][q][L].im);
+        out[h * FFT_M + 64 * q + L] = cadd(E[0][d], t);
+        out[h * FFT_M + 64 * (q + 4) + L] = csub(E[0][d], t);
+      }
+}
+
+static void fft2k_inv(const or_c64* in, double* out) {
+  const fft2k_tab* T = tab2k();
+  or_c64 E[2][FFT_M], z[2][FFT_M];
+  for (int h = 0; h < 2; h++)
+    for (int q = 0; q < 4; q++)
+      for (int L = 0; L < 64; L++) {
+        const or_c64 lo = in[h * FFT_M + 64 * q + L], hi = in[h * FFT_M + 64 * (q + 4) + L];
+        const int d = L + 64 * (4 * h + q);
+        E[0][d] = cadd(lo, hi);
+        E[1][d] = cmul(csub(lo, hi), T->wc[h][q][L].re, -T->wc[h][q][L].im);
+      }
+  for (int h = 0; h < 2; h++) {
+    dft512_inv(E[h], z[h]);
+    for (int m = 0; m < FFT_M; m++) {
+      const int j = 2 * m + h;
+      const or_c64 v = cmul(z[h][m], T->twist[j].re, -T->twist[j].im);
+      out[j] = v.re;
+      out[j + 2 * FFT_M] = v.im;
+    }
+  }
+}
+
 void or_fft_fwd(const double* a, uint32_t N, or_c64* out) {
+  if (N == 4 * FFT_M) { fft2k_fwd(a, out); return; }
   if (N != 2 * FFT_M) abort();
   const fft_tab* T = tab();
   or_c64 z[FFT_M];
@@ -219,6 +295,7 @@ void or_fft_fwd(const double* a, uint32_t N, or_c64* out) {
 }
 
 void or_fft_inv(const or_c64* in, uint32_t N, double* out) {
+  if (N == 4 * FFT_M) { fft2k_inv(in, out); return; }
   if (N != 2 * FFT_M) abort();
   const fft_tab* T = tab();
   or_c64 z[FFT_M];
@@ -245,13 +322,14 @@ void or_bsk_to_fourier(const or_params* p, const uint64_t* bsk, or_c64* bsk_f) {
   const size_t polys = or_bsk_len(p) / N;
 #pragma omp parallel for schedule(static)
   for (size_t q = 0; q < polys; q++) {
-    double a[2 * FFT_M];
+    double a[4 * FFT_M];
+    const double inv_m = 1.0 / (double)M; /* 2^-9 (N = 1024) or 2^-10 (N = 2048): exact */
     for (uint32_t j = 0; j < N; j++) a[j] = (double)(int64_t)bsk[q * N + j];
     or_c64* o = bsk_f + q * M;
     or_fft_fwd(a, N, o);
     for (uint32_t j = 0; j < M; j++) {
-      o[j].re = o[j].re * 0x1p-9;
-      o[j].im = o[j].im * 0x1p-9;
+      o[j].re = o[j].re * inv_m;
+      o[j].im = o[j].im * inv_m;
     }
   }
 }
@@ -269,16 +347,16 @@ static void monomial_torus(uint64_t* out, const uint64_t* in, uint32_t N, uint32
 void or_blind_rotate_fft(const or_params* p, const or_c64* bsk_f, const uint64_t* lwe_in, const uint64_t* lut,
                          uint64_t* acc) {
   const uint32_t N = p->N, M = N / 2, k = p->k, L = p->pbs_level, n = p->n;
-  if (k != 1 || N != 2 * FFT_M || L > 8) abort();
+  if (k != 1 || (N != 2 * FFT_M && N != 4 * FFT_M) || L > 8) abort();
   const size_t per_i = (size_t)(k + 1) * L * (k + 1) * M;
-  uint64_t lt[2 * FFT_M], rot[2 * FFT_M];
+  uint64_t lt[4 * FFT_M], rot[4 * FFT_M];
   for (uint32_t i = 0; i < N; i++) lt[i] = or_p_to_tor(lut[i]); /* convert, then rotate */
   memset(acc, 0, (size_t)N * 8);
   const uint32_t bt = or_mod_switch(lwe_in[n], 2 * N);
   monomial_torus(acc + N, lt, N, (2 * N - bt) % (2 * N));
-  double dig[8][2 * FFT_M];
-  or_c64 D[FFT_M], O[2][FFT_M];
-  double res[2 * FFT_M];
+  static _Thread_local double dig[8][4 * FFT_M];
+  or_c64 D[2 * FFT_M], O[2][2 * FFT_M];
+  double res[4 * FFT_M];
   int64_t d[64];
   for (uint32_t i = 0; i < n; i++) {
     const uint32_t a = or_mod_switch(lwe_in[i], 2 * N);
@@ -323,8 +401,16 @@ void or_sample_extract_torus(const or_params* p, const uint64_t* acc, uint64_t* 
 
 void or_pbs_batch_fft(const or_params* p, const or_c64* bsk_f, const uint64_t* ksk, const uint64_t* lwe_in, size_t B,
                       const uint64_t* luts, size_t n_lut, const uint32_t* lut_index, uint64_t* lwe_out, int threads) {
-  if (p->order != 0) abort();
-  const size_t din = (size_t)p->n + 1, big = (size_t)p->k * p->N + 1, row = (size_t)(p->k + 1) * p->N;
+  or_pbs_batch_fft_ex(p, bsk_f, ksk, NULL, lwe_in, B, luts, n_lut, lut_index, lwe_out, threads);
+}
+
+/* order 0 (P-GATE): BR -> SE -> KS; order 1 (P-FHEVM): KS -> MS noise reduction (ms, nullable) -> BR -> SE,
+ * the same sequence as or_pbs_ex with the FFT64 blind rotation */
+void or_pbs_batch_fft_ex(const or_params* p, const or_c64* bsk_f, const uint64_t* ksk, const or_ms_key* ms,
+                         const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
+                         const uint32_t* lut_index, uint64_t* lwe_out, int threads) {
+  const size_t big = (size_t)p->k * p->N + 1, small = (size_t)p->n + 1, row = (size_t)(p->k + 1) * p->N;
+  const size_t din = p->order == 0 ? small : big, dout = p->order == 0 ? small : big;
 #ifdef _OPENMP
   if (threads <= 0) threads = omp_get_max_threads();
 #pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
@@ -333,12 +419,21 @@ void or_pbs_batch_fft(const or_params* p, const or_c64* bsk_f, const uint64_t* k
     size_t li = lut_index ? lut_index[q] : 0;
     if (li >= n_lut) li = 0;
     uint64_t* acc = (uint64_t*)malloc(row * 8);
-    uint64_t* ext = (uint64_t*)malloc(big * 8);
-    or_blind_rotate_fft(p, bsk_f, lwe_in + q * din, luts + li * p->N, acc);
-    or_sample_extract_torus(p, acc, ext);
-    or_keyswitch(p, ksk, ext, lwe_out + q * din);
+    if (p->order == 0) {
+      uint64_t* ext = (uint64_t*)malloc(big * 8);
+      or_blind_rotate_fft(p, bsk_f, lwe_in + q * din, luts + li * p->N, acc);
+      or_sample_extract_torus(p, acc, ext);
+      or_keyswitch(p, ksk, ext, lwe_out + q * dout);
+      free(ext);
+    } else {
+      uint64_t* sm = (uint64_t*)malloc(small * 8);
+      or_keyswitch(p, ksk, lwe_in + q * din, sm);
+      or_ms_reduce(p, ms, sm);
+      or_blind_rotate_fft(p, bsk_f, sm, luts + li * p->N, acc);
+      or_sample_extract_torus(p, acc, lwe_out + q * dout);
+      free(sm);
+    }
     free(acc);
-    free(ext);
   }
   (void)threads;
 }

@@ -267,7 +267,7 @@ def ms_reduce(prm: Params, keys: Keys, small: np.ndarray):
 def pbs_batch(prm: Params, keys: Keys, lwe_in: np.ndarray, luts: np.ndarray, lut_index=None,
               threads: int = 0, ms: bool = True) -> np.ndarray:
     if prm.transform == 1:
-        return pbs_batch_fft(prm, keys, lwe_in, luts, lut_index, threads)
+        return pbs_batch_fft(prm, keys, lwe_in, luts, lut_index, threads, ms)
     lwe_in = np.ascontiguousarray(lwe_in, dtype=np.uint64)
     luts = np.ascontiguousarray(luts, dtype=np.uint64).reshape(-1, prm.N)
     B = lwe_in.shape[0]
@@ -338,15 +338,19 @@ def sample_extract_torus(prm: Params, acc: np.ndarray) -> np.ndarray:
 
 
 def pbs_batch_fft(prm: Params, keys: Keys, lwe_in: np.ndarray, luts: np.ndarray, lut_index=None,
-                  threads: int = 0) -> np.ndarray:
+                  threads: int = 0, ms: bool = True) -> np.ndarray:
+    """FFT64 PBS (or_pbs_batch_fft_ex): P-GATE BR -> SE -> KS, P-FHEVM KS -> MS -> BR -> SE."""
     lwe_in = np.ascontiguousarray(lwe_in, dtype=np.uint64)
     luts = np.ascontiguousarray(luts, dtype=np.uint64).reshape(-1, prm.N)
     B = lwe_in.shape[0]
-    out = np.zeros((B, prm.n + 1), dtype=np.uint64)
+    dout = (prm.n if prm.order == 0 else prm.k * prm.N) + 1
+    out = np.zeros((B, dout), dtype=np.uint64)
     li = np.ascontiguousarray(lut_index, dtype=np.uint32) if lut_index is not None else None
-    lib().or_pbs_batch_fft(ctypes.byref(prm), _p(keys.bsk_fourier, ctypes.c_void_p), _p(keys.ksk), _p(lwe_in),
-                           ctypes.c_size_t(B), _p(luts), ctypes.c_size_t(luts.shape[0]),
-                           _p(li, U32P) if li is not None else None, _p(out), ctypes.c_int(threads))
+    msk = keys.ms_key(ms)
+    lib().or_pbs_batch_fft_ex(ctypes.byref(prm), _p(keys.bsk_fourier, ctypes.c_void_p), _p(keys.ksk),
+                              ctypes.byref(msk) if msk else None, _p(lwe_in),
+                              ctypes.c_size_t(B), _p(luts), ctypes.c_size_t(luts.shape[0]),
+                              _p(li, U32P) if li is not None else None, _p(out), ctypes.c_int(threads))
     return out
 
 

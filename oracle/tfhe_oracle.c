@@ -37,6 +37,11 @@ int or_params_preset(int preset, or_params* o) {
     o->transform = 1;
     return 0;
   }
+  if (preset == 3) { /* P-FHEVM, FFT64 transform (native torus BSK, N = 2048 as two 512-point halves) */
+    or_params_preset(1, o);
+    o->transform = 1;
+    return 0;
+  }
   if (preset == 1) {
     o->n = 918; o->k = 1; o->N = 2048;
     o->pbs_base_log = 23; o->pbs_level = 1;

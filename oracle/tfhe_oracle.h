@@ -52,7 +52,7 @@ typedef struct or_params {
 } or_params;
 
 /* preset 0 = P-GATE (n=630,k=1,N=1024, 7x3, 2x8), preset 1 = P-FHEVM (918,1,2048, 23x1, 4x4),
- * preset 2 = P-GATE on the FFT64 transform (fft_oracle.c). */
+ * preset 2 = P-GATE on the FFT64 transform (fft_oracle.c); preset 3 = P-FHEVM on the FFT64 transform. */
 int or_params_preset(int preset, or_params* out);
 
 /* ---- PRNG (ChaCha20, RFC 8439 block function) -------------------------------------- */
@@ -250,6 +250,9 @@ void or_blind_rotate_fft(const or_params* p, const or_c64* bsk_f, const uint64_t
 void or_sample_extract_torus(const or_params* p, const uint64_t* acc, uint64_t* lwe_big_out);
 void or_pbs_batch_fft(const or_params* p, const or_c64* bsk_f, const uint64_t* ksk, const uint64_t* lwe_in, size_t B,
                       const uint64_t* luts, size_t n_lut, const uint32_t* lut_index, uint64_t* lwe_out, int threads);
+void or_pbs_batch_fft_ex(const or_params* p, const or_c64* bsk_f, const uint64_t* ksk, const or_ms_key* ms,
+                         const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
+                         const uint32_t* lut_index, uint64_t* lwe_out, int threads);
 /* exact negacyclic product over Z_2^64 (wrapping): the independent arbiter of the FFT's rounding */
 void or_poly_mul_torus_schoolbook(uint64_t* out, const int64_t* a, const uint64_t* b, uint32_t N);
 

@@ -25,7 +25,7 @@ import numpy as np
 
 __all__ = [
     "Params", "TfheError", "lib", "ClientKey", "ServerKey", "gen_keys", "Engine", "FheBool", "FheUint8",
-    "PRESET_GATE", "PRESET_FHEVM", "PRESET_GATE_FFT", "TRANSFORM_NTT", "TRANSFORM_FFT64", "MU", "encode_bool",
+    "PRESET_GATE", "PRESET_FHEVM", "PRESET_GATE_FFT", "PRESET_FHEVM_FFT", "TRANSFORM_NTT", "TRANSFORM_FFT64", "MU", "encode_bool",
     "decode_bool",
 ]
 
@@ -35,6 +35,7 @@ LIB_PATH = os.environ.get("TFHE_HIP_LIB") or os.path.join(_HERE, "libtfhe_hip.so
 PRESET_GATE = 0
 PRESET_FHEVM = 1
 PRESET_GATE_FFT = 2  # P-GATE on the FFT64 transform (tfhe-rs's f64-FFT external product)
+PRESET_FHEVM_FFT = 3  # P-FHEVM on the FFT64 transform (N = 2048 as two 512-point halves)
 TRANSFORM_NTT = 0
 TRANSFORM_FFT64 = 1
 MU = 1 << 61  # gate encoding: true = +1/8, false = -1/8 of the 2^64 torus

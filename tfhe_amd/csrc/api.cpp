@@ -46,14 +46,13 @@ bool params_valid(const tfhe_params* p) {
          p->ks_base_log * p->ks_level < 64 && p->transform <= TFHE_HIP_TRANSFORM_FFT64;
 }
 
-// The device kernels of this build: P-GATE shape (k=1, N=1024, PBS 7x3, KS 2x8, PBS then KS).
 // the device kernels of this build: P-GATE (N = 1024, PBS -> KS) and P-FHEVM (N = 2048, KS -> PBS)
 bool params_on_device(const tfhe_params* p) {
   const bool gate = p->k == 1 && p->N == 1024 && p->pbs_base_log == 7 && p->pbs_level == 3 && p->ks_base_log == 2 &&
                     p->ks_level == 8 && p->order == 0;
   const bool fhevm = p->k == 1 && p->N == 2048 && p->pbs_base_log == 23 && p->pbs_level == 1 &&
                      p->ks_base_log == 4 && p->ks_level == 4 && p->order == 1;
-  return gate || (fhevm && p->transform == TFHE_HIP_TRANSFORM_NTT);
+  return gate || fhevm;
 }
 
 bool is_fft(const tfhe_params& p) { return p.transform == TFHE_HIP_TRANSFORM_FFT64; }
@@ -165,6 +164,9 @@ uint32_t io_dim(const tfhe_params& p) { return p.order == 0 ? p.n : p.k * p.N; }
 
 hipError_t launch_br(tfhe_ctx* c, const u64* in, size_t B, const u64* luts, const u32* idx, size_t n_lut, u64* out_big,
                      u64* out_acc, hipStream_t s) {
+  if (is_fft(c->p) && c->p.N == 2048)
+    return tfhe::launch_blind_rotate_fft2k(in, B, (int)c->p.n, luts, idx, (int)n_lut, (const double*)c->d_bsk,
+                                           (const double*)c->d_tw, out_big, out_acc, s);
   if (is_fft(c->p))
     return tfhe::launch_blind_rotate_fft(in, B, (int)c->p.n, luts, idx, (int)n_lut, (const double*)c->d_bsk,
                                          (const double*)c->d_tw, out_big, out_acc, s);
@@ -279,6 +281,10 @@ int tfhe_hip_params_preset(int preset, tfhe_params* o) {
     *o = tfhe_params{630, 1, 1024, 7, 3, 2, 8, -15, -25, 0, TFHE_HIP_TRANSFORM_FFT64};
     return 0;
   }
+  if (preset == TFHE_HIP_PRESET_FHEVM_FFT) {
+    *o = tfhe_params{918, 1, 2048, 23, 1, 4, 4, -19, -47, 1, TFHE_HIP_TRANSFORM_FFT64};
+    return 0;
+  }
   return fail(TFHE_HIP_EINVAL, "unknown preset %d", preset);
 }
 
@@ -346,7 +352,7 @@ int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out) {
   if (!params_on_device(p))
     return fail(TFHE_HIP_EUNSUPPORTED,
                 "create: device kernels of this build cover P-GATE (k=1, N=1024, PBS 7x3, KS 2x8, PBS->KS; NTT or "
-                "FFT64) and P-FHEVM (k=1, N=2048, PBS 23x1, KS 4x4, KS->PBS; NTT); got "
+                "FFT64) and P-FHEVM (k=1, N=2048, PBS 23x1, KS 4x4, KS->PBS; NTT or FFT64); got "
                 "k=%u N=%u pbs %ux%u ks %ux%u order %u transform %u",
                 p->k, p->N, p->pbs_base_log, p->pbs_level, p->ks_base_log, p->ks_level, p->order, p->transform);
   int ndev = 0;
@@ -370,8 +376,9 @@ int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out) {
   using namespace tfhe;
   if (is_fft(*p)) {  // FFT64: twist / pass tables (pbs_fft.hip: make_fft_tables); no latency kernel
     c->lat_max = 0;
-    std::vector<double> tw(fft_tables_len());
-    make_fft_tables(tw.data());
+    std::vector<double> tw(p->N == 2048 ? fft2k_tables_len() : fft_tables_len());
+    if (p->N == 2048) make_fft2k_tables(tw.data());
+    else make_fft_tables(tw.data());
     if (hipMalloc(&c->d_tw, tw.size() * 8) != hipSuccess)
       return cleanup(fail(TFHE_HIP_ENOMEM, "create: twiddle allocation failed"));
     if (hipMemcpy(c->d_tw, tw.data(), tw.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
@@ -445,7 +452,9 @@ static int load_keys_impl(tfhe_ctx* c, const uint64_t* bsk, size_t bsk_len, cons
     tmp = (void*)bsk;
   }
   const size_t polys = bsk_len / c->p.N;
-  if (is_fft(c->p))
+  if (is_fft(c->p) && c->p.N == 2048)
+    HIP_TRY(tfhe::launch_bsk_to_fourier2k((const u64*)tmp, (double*)c->d_bsk, polys, (const double*)c->d_tw, c->stream));
+  else if (is_fft(c->p))
     HIP_TRY(tfhe::launch_bsk_to_fourier((const u64*)tmp, (double*)c->d_bsk, polys, (const double*)c->d_tw, c->stream));
   else if (c->p.N == 2048)
     HIP_TRY(tfhe::launch_bsk_to_ntt_2048((const u64*)tmp, c->d_bsk, polys, c->d_tw, c->ninv, c->stream));
@@ -571,7 +580,9 @@ int tfhe_hip_sample_extract(tfhe_ctx* c, const uint64_t* acc, size_t B, uint64_t
   std::vector<void*> d;
   int rc = stage(c, {{acc, B * acc_len * 8}}, d, B * big * 8);
   if (rc) return rc;
-  if (is_fft(c->p)) HIP_TRY(tfhe::launch_sample_extract_torus((const u64*)d[0], B, (u64*)d[1], c->stream));
+  if (is_fft(c->p) && c->p.N == 2048)
+    HIP_TRY(tfhe::launch_sample_extract_torus2k((const u64*)d[0], B, (u64*)d[1], c->stream));
+  else if (is_fft(c->p)) HIP_TRY(tfhe::launch_sample_extract_torus((const u64*)d[0], B, (u64*)d[1], c->stream));
   else if (c->p.N == 2048) HIP_TRY(tfhe::launch_sample_extract_2048((const u64*)d[0], B, (u64*)d[1], c->stream));
   else HIP_TRY(tfhe::launch_sample_extract((const u64*)d[0], B, (u64*)d[1], c->stream));
   HIP_TRY(hipMemcpyAsync(out, d[1], B * big * 8, hipMemcpyDeviceToHost, c->stream));
@@ -631,7 +642,9 @@ int tfhe_hip_fft_fwd(tfhe_ctx* c, const uint64_t* polys, size_t count, double* o
   std::vector<void*> d;
   int rc = stage(c, {{polys, bytes}}, d, bytes);
   if (rc) return rc;
-  HIP_TRY(tfhe::launch_fft_fwd((const u64*)d[0], count, (double*)d[1], (const double*)c->d_tw, c->stream));
+  if (c->p.N == 2048)
+    HIP_TRY(tfhe::launch_fft2k_fwd((const u64*)d[0], count, (double*)d[1], (const double*)c->d_tw, c->stream));
+  else HIP_TRY(tfhe::launch_fft_fwd((const u64*)d[0], count, (double*)d[1], (const double*)c->d_tw, c->stream));
   HIP_TRY(hipMemcpyAsync(out, d[1], bytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return 0;
@@ -647,7 +660,9 @@ int tfhe_hip_fft_inv(tfhe_ctx* c, const double* in, size_t count, double* out) {
   std::vector<void*> d;
   int rc = stage(c, {{in, bytes}}, d, bytes);
   if (rc) return rc;
-  HIP_TRY(tfhe::launch_fft_inv((const double*)d[0], count, (double*)d[1], (const double*)c->d_tw, c->stream));
+  if (c->p.N == 2048)
+    HIP_TRY(tfhe::launch_fft2k_inv((const double*)d[0], count, (double*)d[1], (const double*)c->d_tw, c->stream));
+  else HIP_TRY(tfhe::launch_fft_inv((const double*)d[0], count, (double*)d[1], (const double*)c->d_tw, c->stream));
   HIP_TRY(hipMemcpyAsync(out, d[1], bytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return 0;

@@ -28,187 +28,13 @@
 #pragma clang fp contract(off)
 #include <hip/hip_runtime.h>
 
+#include "fft512.h"
 #include "gl64.h"
 #include "ntt1024.h"
 #include "pbs_kernels.h"
 
 namespace tfhe {
 namespace fftk {
-
-constexpr int M = 512;
-constexpr int S1 = 72, S2 = 65;   // transpose row strides (complex): T1 (passes A|B), T2 (passes B|C)
-constexpr int T_C64 = 576;        // per-wave transpose scratch (9,216 B; also holds 1024 u64)
-constexpr int TW_TWIST = 0, TW_A = 512, TW_B = 1024, TW_I = 1536, TW_C64 = 2048;  // table offsets (complex)
-constexpr double SQRT1_2 = 0.70710678118654752440;
-
-// Order between a wave's own LDS writes and reads of its private scratch.  DS instructions of one
-// wavefront execute in issue order, so a compiler-only fence would do (FFT_LDS_WAIT=0); measured on
-// MI355X it is 4 % SLOWER (31.97 vs 30.71 ms per 4096-PBS blind rotation: hipcc then interleaves the
-// transpose reads with the butterflies and stalls on them one by one), so the full lgkmcnt(0) drain
-// stays the default.
-#ifndef FFT_LDS_WAIT
-#define FFT_LDS_WAIT 1
-#endif
-__device__ __forceinline__ void lds_order() {
-#if FFT_LDS_WAIT
-  wave_lds_sync();
-#else
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#endif
-}
-
-// z * w (INV: z * conj(w)), the oracle's cmul(z, w.re, +-w.im)
-template <bool INV>
-__device__ __forceinline__ void cmul(double& re, double& im, double2 w) {
-  const double p = re, q = im;
-  if (!INV) {
-    re = __builtin_fma(p, w.x, -(q * w.y));
-    im = __builtin_fma(p, w.y, q * w.x);
-  } else {
-    re = __builtin_fma(p, w.x, q * w.y);
-    im = __builtin_fma(p, -w.y, q * w.x);
-  }
-}
-
-// t * e^{+-i pi j / 4} (oracle w8)
-template <bool INV, int J>
-__device__ __forceinline__ void w8(double& re, double& im) {
-  const double p = re, q = im;
-  if (J == 1) {
-    if (!INV) { re = (p - q) * SQRT1_2; im = (p + q) * SQRT1_2; }
-    else { re = (p + q) * SQRT1_2; im = (q - p) * SQRT1_2; }
-  } else if (J == 2) {
-    if (!INV) { re = -q; im = p; }
-    else { re = q; im = -p; }
-  } else {
-    if (!INV) { re = -((p + q) * SQRT1_2); im = (p - q) * SQRT1_2; }
-    else { re = (q - p) * SQRT1_2; im = -((p + q) * SQRT1_2); }
-  }
-}
-
-// 8-point DFT in registers, natural order in and out (radix-2 DIF, bit-reversal by renaming)
-template <bool INV>
-__device__ __forceinline__ void dft8(double (&xr)[8], double (&xi)[8]) {
-  double yr[8], yi[8];
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    yr[j] = xr[j] + xr[j + 4];
-    yi[j] = xi[j] + xi[j + 4];
-    yr[j + 4] = xr[j] - xr[j + 4];
-    yi[j + 4] = xi[j] - xi[j + 4];
-  }
-  w8<INV, 1>(yr[5], yi[5]);
-  w8<INV, 2>(yr[6], yi[6]);
-  w8<INV, 3>(yr[7], yi[7]);
-  double zr[8], zi[8];
-#pragma unroll
-  for (int h = 0; h < 8; h += 4)
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-      zr[h + j] = yr[h + j] + yr[h + j + 2];
-      zi[h + j] = yi[h + j] + yi[h + j + 2];
-      zr[h + j + 2] = yr[h + j] - yr[h + j + 2];
-      zi[h + j + 2] = yi[h + j] - yi[h + j + 2];
-    }
-  w8<INV, 2>(zr[3], zi[3]);
-  w8<INV, 2>(zr[7], zi[7]);
-  // u[g] = z[g] + z[g+1], u[g+1] = z[g] - z[g+1];  X[k] = u[brv3(k)]
-  xr[0] = zr[0] + zr[1]; xi[0] = zi[0] + zi[1];
-  xr[4] = zr[0] - zr[1]; xi[4] = zi[0] - zi[1];
-  xr[2] = zr[2] + zr[3]; xi[2] = zi[2] + zi[3];
-  xr[6] = zr[2] - zr[3]; xi[6] = zi[2] - zi[3];
-  xr[1] = zr[4] + zr[5]; xi[1] = zi[4] + zi[5];
-  xr[5] = zr[4] - zr[5]; xi[5] = zi[4] - zi[5];
-  xr[3] = zr[6] + zr[7]; xi[3] = zi[6] + zi[7];
-  xr[7] = zr[6] - zr[7]; xi[7] = zi[6] - zi[7];
-}
-
-// per-lane transpose bases: b1 = T1 read / inverse write, b2 = T2 read / inverse write
-struct TBase {
-  int b1, b2;
-  __device__ __forceinline__ explicit TBase(int lane)
-      : b1((lane >> 3) * S1 + (lane & 7)), b2((lane & 7) * S2 + 8 * (lane >> 3)) {}
-};
-
-// forward 512-point DFT: natural order in (lane L, slot e <-> L + 64 e), device order out
-__device__ __forceinline__ void dft512_fwd(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
-                                           const double2* tw) {
-  dft8<false>(xr, xi);
-#pragma unroll
-  for (int e = 1; e < 8; e++) cmul<false>(xr[e], xi[e], tw[TW_A + 64 * e + lane]);
-#pragma unroll
-  for (int e = 0; e < 8; e++) T[lane + S1 * e] = make_double2(xr[e], xi[e]);
-  lds_order();
-#pragma unroll
-  for (int e = 0; e < 8; e++) {
-    const double2 v = T[tb.b1 + 8 * e];
-    xr[e] = v.x;
-    xi[e] = v.y;
-  }
-  lds_order();
-  dft8<false>(xr, xi);
-#pragma unroll
-  for (int e = 1; e < 8; e++) cmul<false>(xr[e], xi[e], tw[TW_B + 64 * e + lane]);
-#pragma unroll
-  for (int e = 0; e < 8; e++) T[lane + S2 * e] = make_double2(xr[e], xi[e]);
-  lds_order();
-#pragma unroll
-  for (int e = 0; e < 8; e++) {
-    const double2 v = T[tb.b2 + e];
-    xr[e] = v.x;
-    xi[e] = v.y;
-  }
-  lds_order();
-  dft8<false>(xr, xi);
-}
-
-// inverse (no 1/M): device order in, natural order out — the forward's passes reversed
-__device__ __forceinline__ void dft512_inv(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
-                                           const double2* tw) {
-  dft8<true>(xr, xi);
-#pragma unroll
-  for (int e = 1; e < 8; e++) cmul<true>(xr[e], xi[e], tw[TW_B + 64 * e + lane]);
-#pragma unroll
-  for (int e = 0; e < 8; e++) T[tb.b2 + e] = make_double2(xr[e], xi[e]);
-  lds_order();
-#pragma unroll
-  for (int e = 0; e < 8; e++) {
-    const double2 v = T[lane + S2 * e];
-    xr[e] = v.x;
-    xi[e] = v.y;
-  }
-  lds_order();
-  dft8<true>(xr, xi);
-#pragma unroll
-  for (int e = 0; e < 8; e++) cmul<true>(xr[e], xi[e], tw[TW_I + 64 * e + lane]);
-#pragma unroll
-  for (int e = 0; e < 8; e++) T[tb.b1 + 8 * e] = make_double2(xr[e], xi[e]);
-  lds_order();
-#pragma unroll
-  for (int e = 0; e < 8; e++) {
-    const double2 v = T[lane + S1 * e];
-    xr[e] = v.x;
-    xi[e] = v.y;
-  }
-  lds_order();
-  dft8<true>(xr, xi);
-}
-
-// (double)(int64)x, correctly rounded: exact hi * 2^32 plus exact lo, one rounding
-__device__ __forceinline__ double i64_to_f64(u64 x) {
-  return __builtin_fma((double)(int)(x >> 32), 0x1p32, (double)(u32)x);
-}
-
-// rint(x) mod 2^64 (every step after the rint is exact)
-// h = floor(t / 2^32) is an integer with |h| < 2^51, so h + 1.5 * 2^52 is exact and its low
-// mantissa word is h mod 2^32
-__device__ __forceinline__ u64 f64_to_torus(double x) {
-  const double t = __builtin_rint(x);
-  const double h = __builtin_floor(t * 0x1p-32);
-  const double l = __builtin_fma(-h, 0x1p32, t);
-  const u32 hm = (u32)__double_as_longlong(h + 0x1.8p52);
-  return ((u64)hm << 32) | (u64)(u32)l;
-}
 
 // forward transform of a real polynomial held as 16 doubles per lane (slot e <-> coefficient 64 e + L)
 __device__ __forceinline__ void fft_fwd_real(const double (&a)[16], double (&xr)[8], double (&xi)[8], double2* T,
@@ -535,6 +361,8 @@ static void twiddle(uint32_t t, uint32_t m, double* c, double* s) {
 }
 
 }  // namespace fftk
+
+void fft_twiddle(uint32_t t, uint32_t m, double* c, double* s) { fftk::twiddle(t, m, c, s); }
 
 size_t fft_tables_len() { return 2 * fftk::TW_C64; }
 

@@ -1,0 +1,425 @@
+// pbs_fft2k.hip — the FFT64 engine for N = 2048 (P-FHEVM: n = 918, k = 1, PBS 2^23 x 1, KS 2^4 x 4,
+// KS -> PBS; sdk/relayer/src/tfhe.ts:14-19): tfhe-rs's f64 negacyclic FFT external product over the
+// native 2^64 torus, restated bit-for-bit in oracle/fft_oracle.c (fft2k_fwd / fft2k_inv).
+//
+// A polynomial is held by TWO waves: wave h owns the coefficients of parity h,
+//   slot e < 8: coefficient 2 (L + 64 e) + h,   slot e >= 8: the same + 1024,
+// so its folded half z_{2m+h} = (a_{2m+h} + i a_{2m+h+1024}) zeta^{2m+h} (m = L + 64 e) is exactly the
+// natural-order input of the 512-point DFT of fft512.h.  The two half spectra E_0, E_1 meet in one
+// radix-2 combine, Z[k'] = E_0 + w^k' E_1, Z[k' + 512] = E_0 - w^k' E_1, after an LDS exchange of the
+// pair (both waves write their 8 slots, each reads E_0 and E_1 at its 4 slots 4h + q); wave h then
+// holds frequencies k'(L, 4h + (s & 3)) + 512 (s >> 2) in slot s — the device order of the BSK.
+//
+// Blind rotation: workgroup = 4 ciphertexts x 2 waves.  LDS (152 KB of a gfx950 CU's 160):
+//   T   8 x 9,216 B   per-wave transpose scratch; a pair's two regions also hold the 2048-u64
+//                     rotation image and the combine / uncombine exchanges
+//   tw  48 KB         all tables: 512-point passes A | B | I, twist (both parities), combine
+//   K   2 x 16 KB     BSK_i[c][0..1] of the component in flight, loaded by global_load_lds one phase
+//                     ahead (K_{1,*} during component 1's rotation and transform, K_{0,*} of the next
+//                     CMUX during the inverse transforms), published by the transform's barriers
+// Per CMUX: rotate + decompose both components (23 x 1 digits, no exchange of digits needed: each
+// wave decomposes its own coefficients), two forward transforms, the MAC
+//   O_j = fma chain over c = 0, 1 of D_c (.) BSK_i[c][j]   (the oracle's order, from (0, 0)),
+// and two inverse transforms back to this wave's coefficients of acc_0 and acc_1.
+#include "fft512.h"
+#include "pbs_kernels.h"
+
+namespace tfhe {
+namespace fft2k {
+using namespace fftk;
+
+constexpr int N2 = 2048, M2 = 1024;
+// table (complex, the same layout in global memory and in LDS): twist of parity 0 | pass tables A | B | I
+// at fft512.h's TW_A / TW_B / TW_I (so the pass-table base is the table itself: no negative LDS offsets)
+// | twist of parity 1 | combine twiddles [h][q][L]
+constexpr int G_TW0 = 0, G_PASS = TW_A, G_TW1 = 2048, G_WC = 2560, G_C64 = 3072;
+static_assert(TW_A == 512 && TW_B == 1024 && TW_I == 1536, "fft512.h pass-table offsets");
+constexpr int F2_PAIRS = 4, F2_WAVES = 8, F2_THREADS = 64 * F2_WAVES;
+constexpr int CHUNK_GLDS = M2 * 16 / 1024;  // 1 KB wave-instructions per BSK polynomial (16)
+
+__device__ __forceinline__ int ms4096(u64 x) { return (int)((((x >> 51) + 1) >> 1) & 4095u); }
+__device__ __forceinline__ int kdev(int L, int e) { return (L >> 3) + 8 * (L & 7) + 64 * e; }
+// coefficient held by wave h, lane L, slot e
+__device__ __forceinline__ int coef(int h, int L, int e) { return 2 * (L + 64 * (e & 7)) + h + 1024 * (e >> 3); }
+
+// tfhe-rs SignedDecomposer 2^23 x 1: closest representable at 23 bits, digit in [-2^22, 2^22]
+__device__ __forceinline__ int decomp_23x1(u64 x) {
+  const u32 state = (u32)(((x >> 40) + 1) >> 1) & 0x7FFFFFu;
+  const u32 carry = (((state - 1u) & state) >> 22) & 1u;
+  return (int)state - (int)(carry << 23);
+}
+
+// forward: 16 reals per lane (slot e < 8 real part, e + 8 imaginary part) -> half spectrum in xr/xi
+// (slot s: frequency k'(L, 4h + (s & 3)) + 512 (s >> 2)).  Contains two pair barriers: every wave of
+// the workgroup calls it in lockstep.  T0 / T1: the pair's regions (wave 0 / wave 1).
+__device__ __forceinline__ void fwd_half(double (&xr)[8], double (&xi)[8], int h, int lane, TBase tb,
+                                         double2* T0, double2* T1, const double2* twp, const double2* tg) {
+  double2* Tm = h ? T1 : T0;
+  const double2* twist = tg + (h ? G_TW1 : G_TW0);
+#pragma unroll
+  for (int e = 0; e < 8; e++) cmul<false>(xr[e], xi[e], twist[64 * e + lane]);
+  dft512_fwd(xr, xi, Tm, lane, tb, twp);
+#pragma unroll
+  for (int e = 0; e < 8; e++) Tm[64 * e + lane] = make_double2(xr[e], xi[e]);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int e = 4 * h + q;
+    const double2 e0 = T0[64 * e + lane], e1 = T1[64 * e + lane];
+    double tr = e1.x, ti = e1.y;
+    cmul<false>(tr, ti, tg[G_WC + 256 * h + 64 * q + lane]);
+    xr[q] = e0.x + tr;
+    xi[q] = e0.y + ti;
+    xr[q + 4] = e0.x - tr;
+    xi[q + 4] = e0.y - ti;
+  }
+  __syncthreads();
+}
+
+// inverse, first half: uncombine this wave's 4 slot pairs into the pair's exchange (E_0 -> T0,
+// E_1 -> T1, slot 4h + q), then each wave reads its full E_h.  Two pair barriers.
+__device__ __forceinline__ void inv_exchange(double (&xr)[8], double (&xi)[8], int h, int lane, double2* T0,
+                                             double2* T1, const double2* tg) {
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int e = 4 * h + q;
+    const double lr = xr[q], li = xi[q], hr = xr[q + 4], hi = xi[q + 4];
+    double dr = lr - hr, di = li - hi;
+    cmul<true>(dr, di, tg[G_WC + 256 * h + 64 * q + lane]);
+    T0[64 * e + lane] = make_double2(lr + hr, li + hi);
+    T1[64 * e + lane] = make_double2(dr, di);
+  }
+  __syncthreads();
+  const double2* Tm = h ? T1 : T0;
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = Tm[64 * e + lane];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  __syncthreads();
+}
+
+// inverse, second half (wave-private): 512-point inverse + untwist -> reals (slot e < 8: re, e + 8: im)
+__device__ __forceinline__ void inv_half(double (&xr)[8], double (&xi)[8], int h, int lane, TBase tb, double2* Tm,
+                                         const double2* twp, const double2* tg) {
+  dft512_inv(xr, xi, Tm, lane, tb, twp);
+  const double2* twist = tg + (h ? G_TW1 : G_TW0);
+#pragma unroll
+  for (int e = 0; e < 8; e++) cmul<true>(xr[e], xi[e], twist[64 * e + lane]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// transform kernels (one polynomial per 2-wave workgroup): BSK conversion and the parity tests
+__global__ __launch_bounds__(128) void fwd2k_kernel(const u64* __restrict__ in, double2* __restrict__ out,
+                                                    const double2* __restrict__ tg, double scale) {
+  __shared__ __attribute__((aligned(16))) double2 T[2][T_C64];
+  const int h = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const u64* src = in + (size_t)blockIdx.x * N2;
+  double xr[8], xi[8];
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    xr[e] = i64_to_f64(src[coef(h, lane, e)]);
+    xi[e] = i64_to_f64(src[coef(h, lane, e + 8)]);
+  }
+  fwd_half(xr, xi, h, lane, TBase(lane), T[0], T[1], tg + G_PASS - TW_A, tg);
+  double2* dst = out + (size_t)blockIdx.x * M2 + h * 512;
+#pragma unroll
+  for (int s = 0; s < 8; s++) dst[64 * s + lane] = make_double2(xr[s] * scale, xi[s] * scale);
+}
+
+__global__ __launch_bounds__(128) void inv2k_kernel(const double2* __restrict__ in, double* __restrict__ out,
+                                                    const double2* __restrict__ tg) {
+  __shared__ __attribute__((aligned(16))) double2 T[2][T_C64];
+  const int h = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const double2* src = in + (size_t)blockIdx.x * M2 + h * 512;
+  double xr[8], xi[8];
+#pragma unroll
+  for (int s = 0; s < 8; s++) {
+    const double2 v = src[64 * s + lane];
+    xr[s] = v.x;
+    xi[s] = v.y;
+  }
+  inv_exchange(xr, xi, h, lane, T[0], T[1], tg);
+  inv_half(xr, xi, h, lane, TBase(lane), T[h], tg + G_PASS - TW_A, tg);
+  double* dst = out + (size_t)blockIdx.x * N2;
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    dst[coef(h, lane, e)] = xr[e];
+    dst[coef(h, lane, e + 8)] = xi[e];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// the whole table first (every twiddle read: a per-lane base plus a 16-bit DS immediate offset), then
+// the transpose scratch, then two BSK polynomials (K_{c,0}, K_{c,1} of the component in flight)
+struct F2Shared {
+  double2 tw[G_C64];           // 49,152 B (G_* layout)
+  double2 T[F2_WAVES][T_C64];  // 73,728 B
+  double2 K[2][M2];            // 32,768 B
+};
+typedef __attribute__((address_space(3))) const double lds_f64;
+
+// BSK_i[c][0..1] (32 KB) into K: wave w loads the 1 KB blocks 4w .. 4w + 3 (wave-uniform scalar bases)
+__device__ __forceinline__ void load_pair(const double2* __restrict__ bsk, int i, int c, F2Shared& sh, int wave_s,
+                                          int lane) {
+  constexpr int PER_WAVE = 2 * CHUNK_GLDS / F2_WAVES;
+  const char* src = (const char*)(bsk + ((size_t)i * 4 + 2 * c) * M2) + wave_s * (PER_WAVE * 1024);
+  char* dst = (char*)sh.K + wave_s * (PER_WAVE * 1024);
+#pragma unroll
+  for (int q = 0; q < PER_WAVE; q++)
+    __builtin_amdgcn_global_load_lds((const void*)(src + q * 1024 + lane * 16),
+                                     (__attribute__((address_space(3))) void*)(dst + q * 1024), 16, 0, 0);
+}
+
+// (X^a acc - acc) of this wave's coefficients, decomposed: the pair's 2048-u64 image in LDS (natural
+// coefficient order), written by both waves, read rotated.  Two barriers.
+__device__ __forceinline__ void rotate_decompose(const u64 (&acc)[16], int a, int h, int lane, u64* R, int (&dig)[16]) {
+#pragma unroll
+  for (int e = 0; e < 16; e++) R[coef(h, lane, e)] = acc[e];
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < 16; g += 8) {  // two batches of 8 reads in flight (register pressure)
+#pragma unroll
+    for (int e = g; e < g + 8; e++) {
+      int d = coef(h, lane, e) - a;
+      bool neg = false;
+      if (d < 0) { d += N2; neg = !neg; }
+      if (d < 0) { d += N2; neg = !neg; }
+      const u64 x = R[d];
+      dig[e] = decomp_23x1((neg ? 0 - x : x) - acc[e]);
+    }
+    asm volatile("" ::: "memory");
+  }
+  __syncthreads();
+}
+
+// LDS address of this wave's slot 0 in K, laundered: with K's absolute offset folded in, the MAC's
+// reads would exceed the 16-bit DS immediate and each take a VGPR of its own
+__device__ __forceinline__ lds_f64* kbase(F2Shared& sh, int h, int lane) {
+  u32 a = (u32)(uintptr_t)(lds_f64*)&sh.K[0][h * 512 + lane];
+  asm volatile("" : "+v"(a));
+  return (lds_f64*)(uintptr_t)a;
+}
+
+template <bool WRITE_ACC, bool WRITE_BIG>
+__global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
+    const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
+    int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tg, u64* __restrict__ out_big,
+    u64* __restrict__ out_acc) {
+  __shared__ __attribute__((aligned(16))) F2Shared sh;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = wave & 1, pr = wave >> 1;
+  const size_t b_raw = (size_t)blockIdx.x * F2_PAIRS + pr;
+  const bool live = b_raw < B;
+  const size_t b = live ? b_raw : B - 1;  // padding pairs run a copy of the last ciphertext, store nothing
+  const u64* ct = lwe_in + b * (size_t)(n + 1);
+  double2* T0 = sh.T[2 * pr];
+  double2* T1 = sh.T[2 * pr + 1];
+  double2* Tm = sh.T[wave];
+  u64* R = (u64*)T0;  // 16 KB across the pair's two regions
+  const double2* tt = sh.tw;
+  const double2* twp = sh.tw + G_PASS - TW_A;
+  const TBase tb(lane);
+
+  for (int q = threadIdx.x; q < G_C64; q += F2_THREADS) sh.tw[q] = tg[q];
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  load_pair(bsk, 0, 0, sh, wave_s, lane);
+
+  u64 accA[16], accB[16];
+  {
+    int li = lut_index ? (int)lut_index[b] : 0;
+    li = (li < 0 || li >= n_lut) ? 0 : li;
+    const u64* lut = luts + (size_t)li * N2;
+    const int s = (4096 - ms4096(ct[n])) & 4095;
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      int d = coef(h, lane, e) - s;
+      bool neg = false;
+      if (d < 0) { d += N2; neg = !neg; }
+      if (d < 0) { d += N2; neg = !neg; }
+      const u64 v = gl_to_torus(lut[d]);
+      accA[e] = 0;
+      accB[e] = neg ? 0 - v : v;
+    }
+  }
+
+  for (int i = 0; i < n; i++) {
+    const int a = ms4096(ct[i]);
+    int dg[16];
+    double xr[8], xi[8], o0r[8], o0i[8], o1r[8], o1i[8];
+    __syncthreads();  // the previous CMUX's inverse transforms are done with T
+    rotate_decompose(accA, a, h, lane, R, dg);
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      xr[e] = (double)dg[e];
+      xi[e] = (double)dg[e + 8];
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's share of K_{0,*}; fwd_half's barriers publish it
+    fwd_half(xr, xi, h, lane, tb, T0, T1, twp, tt);
+    {  // MAC, c = 0 (oracle order: from (0, 0)); slot s of this wave = BSK index h * 512 + 64 s + L
+      lds_f64* kp = kbase(sh, h, lane);
+#pragma unroll
+      for (int s = 0; s < 8; s++) {
+        const double k0r = kp[128 * s], k0i = kp[128 * s + 1], k1r = kp[2 * M2 + 128 * s], k1i = kp[2 * M2 + 128 * s + 1];
+        o0r[s] = __builtin_fma(xr[s], k0r, 0.0);
+        o0r[s] = __builtin_fma(-xi[s], k0i, o0r[s]);
+        o0i[s] = __builtin_fma(xr[s], k0i, 0.0);
+        o0i[s] = __builtin_fma(xi[s], k0r, o0i[s]);
+        o1r[s] = __builtin_fma(xr[s], k1r, 0.0);
+        o1r[s] = __builtin_fma(-xi[s], k1i, o1r[s]);
+        o1i[s] = __builtin_fma(xr[s], k1i, 0.0);
+        o1i[s] = __builtin_fma(xi[s], k1r, o1i[s]);
+      }
+    }
+    __syncthreads();  // every wave is done with K_{0,*}
+    load_pair(bsk, i, 1, sh, wave_s, lane);
+    rotate_decompose(accB, a, h, lane, R, dg);
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      xr[e] = (double)dg[e];
+      xi[e] = (double)dg[e + 8];
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): K_{1,*}
+    fwd_half(xr, xi, h, lane, tb, T0, T1, twp, tt);
+
+    {  // MAC, c = 1
+      lds_f64* kp = kbase(sh, h, lane);
+#pragma unroll
+      for (int s = 0; s < 8; s++) {
+        const double k0r = kp[128 * s], k0i = kp[128 * s + 1], k1r = kp[2 * M2 + 128 * s], k1i = kp[2 * M2 + 128 * s + 1];
+        o0r[s] = __builtin_fma(xr[s], k0r, o0r[s]);
+        o0r[s] = __builtin_fma(-xi[s], k0i, o0r[s]);
+        o0i[s] = __builtin_fma(xr[s], k0i, o0i[s]);
+        o0i[s] = __builtin_fma(xi[s], k0r, o0i[s]);
+        o1r[s] = __builtin_fma(xr[s], k1r, o1r[s]);
+        o1r[s] = __builtin_fma(-xi[s], k1i, o1r[s]);
+        o1i[s] = __builtin_fma(xr[s], k1i, o1i[s]);
+        o1i[s] = __builtin_fma(xi[s], k1r, o1i[s]);
+      }
+    }
+    __syncthreads();  // every wave is done with K_{1,*} and with the pair exchanges
+    if (i + 1 < n) load_pair(bsk, i + 1, 0, sh, wave_s, lane);
+    inv_exchange(o0r, o0i, h, lane, T0, T1, tt);
+    inv_half(o0r, o0i, h, lane, tb, Tm, twp, tt);
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      accA[e] += f64_to_torus_wide(o0r[e]);
+      accA[e + 8] += f64_to_torus_wide(o0i[e]);
+    }
+    __syncthreads();  // the partner's inverse transposes are done with its region
+    inv_exchange(o1r, o1i, h, lane, T0, T1, tt);
+    inv_half(o1r, o1i, h, lane, tb, Tm, twp, tt);
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      accB[e] += f64_to_torus_wide(o1r[e]);
+      accB[e + 8] += f64_to_torus_wide(o1i[e]);
+    }
+  }
+
+  if (!live) return;
+  if (WRITE_ACC) {
+    u64* oa = out_acc + b * (2 * N2);
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      oa[coef(h, lane, e)] = accA[e];
+      oa[N2 + coef(h, lane, e)] = accB[e];
+    }
+  }
+  if (WRITE_BIG) {
+    // sample extraction at degree 0: a'_0 = A[0], a'_j = -A[N-j], b' = B[0]
+    u64* ob = out_big + b * (size_t)(N2 + 1);
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      const int c = coef(h, lane, e);
+      if (c == 0) ob[0] = accA[e];
+      else ob[N2 - c] = 0 - accA[e];
+    }
+    if (h == 0 && lane == 0) ob[N2] = accB[0];
+  }
+}
+
+__global__ void sample_extract_torus2k_kernel(const u64* __restrict__ acc, size_t B, u64* __restrict__ out) {
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * (N2 + 1)) return;
+  const size_t b = gid / (N2 + 1);
+  const int j = (int)(gid % (N2 + 1));
+  const u64* A = acc + b * (2 * N2);
+  out[gid] = j == N2 ? A[N2] : j == 0 ? A[0] : 0 - A[N2 - j];
+}
+
+}  // namespace fft2k
+
+hipError_t launch_sample_extract_torus2k(const u64* acc, size_t B, u64* out, hipStream_t s) {
+  if (B == 0) return hipSuccess;
+  const size_t total = B * (fft2k::N2 + 1);
+  hipLaunchKernelGGL(fft2k::sample_extract_torus2k_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, acc,
+                     B, out);
+  return hipGetLastError();
+}
+
+size_t fft2k_tables_len() { return 2 * fft2k::G_C64; }
+
+void make_fft2k_tables(double* t) {
+  using namespace fft2k;
+  constexpr int Mh = 512;
+  for (uint32_t e = 0; e < 8; e++)
+    for (uint32_t L = 0; L < 64; L++) {
+      const int q = 64 * e + L;
+      fft_twiddle((L * e) % Mh, Mh, &t[2 * (fftk::TW_A + q)], &t[2 * (fftk::TW_A + q) + 1]);
+      fft_twiddle((8 * (L & 7) * e) % Mh, Mh, &t[2 * (fftk::TW_B + q)], &t[2 * (fftk::TW_B + q) + 1]);
+      fft_twiddle(((L >> 3) * ((L & 7) + 8 * e)) % Mh, Mh, &t[2 * (fftk::TW_I + q)], &t[2 * (fftk::TW_I + q) + 1]);
+    }
+  for (uint32_t m = 0; m < 512; m++) {
+    fft_twiddle(2 * m, 4096, &t[2 * (G_TW0 + m)], &t[2 * (G_TW0 + m) + 1]);
+    fft_twiddle(2 * m + 1, 4096, &t[2 * (G_TW1 + m)], &t[2 * (G_TW1 + m) + 1]);
+  }
+  for (int h = 0; h < 2; h++)
+    for (int q = 0; q < 4; q++)
+      for (int L = 0; L < 64; L++) {
+        const int k = (L >> 3) + 8 * (L & 7) + 64 * (4 * h + q);
+        const int o = G_WC + 256 * h + 64 * q + L;
+        fft_twiddle((uint32_t)k, 1024, &t[2 * o], &t[2 * o + 1]);
+      }
+}
+
+hipError_t launch_bsk_to_fourier2k(const u64* bsk_std, double* bsk_f, size_t polys, const double* tw, hipStream_t s) {
+  if (polys == 0) return hipSuccess;
+  hipLaunchKernelGGL(fft2k::fwd2k_kernel, dim3((unsigned)polys), dim3(128), 0, s, bsk_std, (double2*)bsk_f,
+                     (const double2*)tw, 0x1p-10);
+  return hipGetLastError();
+}
+
+hipError_t launch_fft2k_fwd(const u64* in, size_t count, double* out, const double* tw, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(fft2k::fwd2k_kernel, dim3((unsigned)count), dim3(128), 0, s, in, (double2*)out,
+                     (const double2*)tw, 1.0);
+  return hipGetLastError();
+}
+
+hipError_t launch_fft2k_inv(const double* in, size_t count, double* out, const double* tw, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(fft2k::inv2k_kernel, dim3((unsigned)count), dim3(128), 0, s, (const double2*)in, out,
+                     (const double2*)tw);
+  return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate_fft2k(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
+                                     int n_lut, const double* bsk_f, const double* tw, u64* out_big, u64* out_acc,
+                                     hipStream_t s) {
+  using namespace fft2k;
+  if (B == 0) return hipSuccess;
+  dim3 grid((unsigned)((B + F2_PAIRS - 1) / F2_PAIRS)), block(F2_THREADS);
+  const double2 *bk = (const double2*)bsk_f, *t = (const double2*)tw;
+  if (out_acc && out_big)
+    hipLaunchKernelGGL((blind_rotate_fft2k_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                       n_lut, bk, t, out_big, out_acc);
+  else if (out_acc)
+    hipLaunchKernelGGL((blind_rotate_fft2k_kernel<true, false>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                       n_lut, bk, t, out_big, out_acc);
+  else
+    hipLaunchKernelGGL((blind_rotate_fft2k_kernel<false, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                       n_lut, bk, t, out_big, out_acc);
+  return hipGetLastError();
+}
+
+}  // namespace tfhe
