@@ -160,3 +160,18 @@ def test_device_decomposition_steps_equal_signed_decomposer(oracle_mod):
         st = np.array([(((x >> 32) + 1024) % 2**32) >> 11], dtype=np.int64)  # the device's decomp_state
         lv = [int(v[0]) for v in steps(st)]  # least significant first
         assert lv[::-1] == oracle_mod.decompose(x, 7, 3)
+
+
+def test_decomp_23x1_high_word_restatement(oracle_mod):
+    """pbs_fft2k.hip decomposes 2^23 x 1 from the high word alone: st = (hi + 2^8) >> 9,
+    digit = ((st + 2^22 - 1) mod 2^23) - (2^22 - 1).  Equal to or_decompose on edge and random words."""
+    rng = np.random.default_rng(23)
+    his = [0, 1, 255, 256, 511, 512, 2**31, 2**32 - 1, 2**32 - 256, 2**32 - 257, 2**32 - 512, 2**30 + 2**9 - 1,
+           2**30 + 2**8, (2**22) << 9, ((2**22) << 9) - 256, ((2**22) << 9) + 255, ((2**22 + 1) << 9) - 256]
+    his += [int(v) for v in rng.integers(0, 2**32, 4000, dtype=np.uint64)]
+    for hi in his:
+        for lo in (0, 2**32 - 1, int(rng.integers(0, 2**32))):
+            x = (hi << 32) | lo
+            st = ((hi + 256) % 2**32) >> 9
+            d = ((st + 0x3FFFFF) & 0x7FFFFF) - 0x3FFFFF
+            assert [d] == oracle_mod.decompose(x, 23, 1), (hi, lo)

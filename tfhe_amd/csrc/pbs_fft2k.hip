@@ -42,11 +42,13 @@ __device__ __forceinline__ int kdev(int L, int e) { return (L >> 3) + 8 * (L & 7
 // coefficient held by wave h, lane L, slot e
 __device__ __forceinline__ int coef(int h, int L, int e) { return 2 * (L + 64 * (e & 7)) + h + 1024 * (e >> 3); }
 
-// tfhe-rs SignedDecomposer 2^23 x 1: closest representable at 23 bits, digit in [-2^22, 2^22]
-__device__ __forceinline__ int decomp_23x1(u64 x) {
-  const u32 state = (u32)(((x >> 40) + 1) >> 1) & 0x7FFFFFu;
-  const u32 carry = (((state - 1u) & state) >> 22) & 1u;
-  return (int)state - (int)(carry << 23);
+// tfhe-rs SignedDecomposer 2^23 x 1: closest representable at 23 bits, state st = round(x / 2^41) mod
+// 2^23, digit = st - 2^23 if st > 2^22 else st (carry rule ((st - 1) & st) >> 22; the tie 2^22 stays
+// positive).  Restated on the high word alone: st = (hi + 2^8) >> 9 (a wrap of hi + 2^8 past 2^32 only
+// happens when st = 2^23, i.e. 0 mod 2^23), digit = ((st + 2^22 - 1) mod 2^23) - (2^22 - 1).
+__device__ __forceinline__ int decomp_23x1_hi(u32 hi) {
+  const u32 st = (hi + 256u) >> 9;
+  return (int)((st + 0x3FFFFFu) & 0x7FFFFFu) - 0x3FFFFF;
 }
 
 // forward: 16 reals per lane (slot e < 8 real part, e + 8 imaginary part) -> half spectrum in xr/xi
@@ -178,18 +180,15 @@ __device__ __forceinline__ void rotate_decompose(const u64 (&acc)[16], int a, in
 #pragma unroll
   for (int e = 0; e < 16; e++) R[coef(h, lane, e)] = acc[e];
   __syncthreads();
+  // (X^a v)[c] = (-1)^bit11(t) v[t mod 2048], t = c - a + 4096 (a < 4096)
+  const int t0 = coef(h, lane, 0) + 2 * N2 - a;
 #pragma unroll
-  for (int g = 0; g < 16; g += 8) {  // two batches of 8 reads in flight (register pressure)
-#pragma unroll
-    for (int e = g; e < g + 8; e++) {
-      int d = coef(h, lane, e) - a;
-      bool neg = false;
-      if (d < 0) { d += N2; neg = !neg; }
-      if (d < 0) { d += N2; neg = !neg; }
-      const u64 x = R[d];
-      dig[e] = decomp_23x1((neg ? 0 - x : x) - acc[e]);
-    }
-    asm volatile("" ::: "memory");
+  for (int e = 0; e < 16; e++) {
+    const int t = t0 + (coef(h, 0, e) - h);
+    const u64 x = R[t & (N2 - 1)];
+    const u64 m = 0ull - (u64)((t >> 11) & 1);  // all ones iff negated
+    const u64 y = ((x ^ m) - m) - acc[e];
+    dig[e] = decomp_23x1_hi((u32)(y >> 32));
   }
   __syncthreads();
 }
