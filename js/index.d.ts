@@ -6,6 +6,8 @@ export interface TfheParams {
 }
 export const PRESET_GATE: 0;
 export const PRESET_FHEVM: 1;
+export const PRESET_GATE_FFT: 2;
+export const PRESET_FHEVM_FFT: 3;
 export const MU: bigint;
 export function paramsPreset(which?: number): TfheParams;
 

@@ -20,6 +20,8 @@ const radix = require('./radix.js');
 
 const PRESET_GATE = 0;
 const PRESET_FHEVM = 1;
+const PRESET_GATE_FFT = 2;  // P-GATE on the FFT64 transform (tfhe-rs's f64-FFT external product)
+const PRESET_FHEVM_FFT = 3; // P-FHEVM on the FFT64 transform
 const TORUS = 1n << 64n;
 const MU = 1n << 61n; // gate encoding: true = +1/8, false = -1/8
 
@@ -228,12 +230,14 @@ const FheUint64 = UINT_CLASSES[64];
  * the POST /evaluate shape (e2e/test/fhe.test.ts:105-175) and runs every fhEVM operator on the GPU.
  * Requests submitted concurrently are evaluated in lockstep (one PBS launch per circuit level).
  * config.params: a params object, or 'gate' (default: boolean gates, js/integer.js) or 'fhevm'
- * (P-FHEVM radix blocks, js/radix.js — fhEVM's own representation).
+ * (P-FHEVM radix blocks, js/radix.js — fhEVM's own representation); 'gate_fft' / 'fhevm_fft' select
+ * the same parameter sets on the FFT64 transform.
  */
 class LuxFHELocalClient {
   constructor(config = {}) {
     const pr = config.params;
-    this.params = pr === 'fhevm' ? paramsPreset(PRESET_FHEVM) : (!pr || pr === 'gate') ? paramsPreset(PRESET_GATE) : pr;
+    const named = { gate: PRESET_GATE, fhevm: PRESET_FHEVM, gate_fft: PRESET_GATE_FFT, fhevm_fft: PRESET_FHEVM_FFT };
+    this.params = !pr ? paramsPreset(PRESET_GATE) : typeof pr === 'string' ? paramsPreset(named[pr]) : pr;
     this.radix = this.params.order === 1;
     this.dim = this.radix ? this.params.k * this.params.N : this.params.n;
     this.seed = BigInt(config.seed || 0x7F4E0001n);
@@ -368,7 +372,7 @@ class LuxFHELocalClient {
 }
 
 module.exports = {
-  native, integer, radix, KIND, PRESET_GATE, PRESET_FHEVM, MU, paramsPreset, genKeys, ClientKey, ServerKey, Engine,
+  native, integer, radix, KIND, PRESET_GATE, PRESET_FHEVM, PRESET_GATE_FFT, PRESET_FHEVM_FFT, MU, paramsPreset, genKeys, ClientKey, ServerKey, Engine,
   FheBool, FheUint8, FheUint16, FheUint32, FheUint64, UINT_CLASSES, LuxFHELocalClient,
   serializeCiphertext, parseCiphertext,
 };

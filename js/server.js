@@ -18,7 +18,7 @@
  * --params fhevm serves fhEVM's own representation instead (P-FHEVM radix blocks, js/radix.js:
  * KS -> PBS at N = 2048, every fhEVM operator).
  *
- *   node js/server.js [--port 8448] [--host 127.0.0.1] [--device 0] [--seed 0x7F4E0001] [--params gate|fhevm]
+ *   node js/server.js [--port 8448] [--host 127.0.0.1] [--device 0] [--seed 0x7F4E0001] [--params gate|fhevm|gate_fft|fhevm_fft]
  */
 const http = require('http');
 

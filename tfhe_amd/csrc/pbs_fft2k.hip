@@ -174,18 +174,21 @@ __device__ __forceinline__ void load_pair(const double2* __restrict__ bsk, int i
                                      (__attribute__((address_space(3))) void*)(dst + q * 1024), 16, 0, 0);
 }
 
-// (X^a acc - acc) of this wave's coefficients, decomposed: the pair's 2048-u64 image in LDS (natural
-// coefficient order), written by both waves, read rotated.  Two barriers.
+// (X^a acc - acc) of this wave's coefficients, decomposed: the pair's 2048-u64 image in LDS, written by
+// both waves, read rotated.  Split layout (coefficient c at R[(c & 1) * 1024 + (c >> 1)]): every write
+// and every rotated read is 64 consecutive u64, free of bank conflicts (the natural layout's stride-2
+// accesses conflicted 4-way).  Two barriers.
+__device__ __forceinline__ int rsplit(int c) { return ((c & 1) << 10) | ((c >> 1) & 1023); }
 __device__ __forceinline__ void rotate_decompose(const u64 (&acc)[16], int a, int h, int lane, u64* R, int (&dig)[16]) {
 #pragma unroll
-  for (int e = 0; e < 16; e++) R[coef(h, lane, e)] = acc[e];
+  for (int e = 0; e < 16; e++) R[rsplit(coef(h, lane, e))] = acc[e];
   __syncthreads();
   // (X^a v)[c] = (-1)^bit11(t) v[t mod 2048], t = c - a + 4096 (a < 4096)
   const int t0 = coef(h, lane, 0) + 2 * N2 - a;
 #pragma unroll
   for (int e = 0; e < 16; e++) {
     const int t = t0 + (coef(h, 0, e) - h);
-    const u64 x = R[t & (N2 - 1)];
+    const u64 x = R[rsplit(t)];
     const u64 m = 0ull - (u64)((t >> 11) & 1);  // all ones iff negated
     const u64 y = ((x ^ m) - m) - acc[e];
     dig[e] = decomp_23x1_hi((u32)(y >> 32));
