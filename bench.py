@@ -90,9 +90,19 @@ def valu_profile(B: int, kernel_ms: float, kernel: str = "blind_rotate_kernel"):
         return None
     insts = sum(vals) / len(vals) / 4096 * B
     frac = insts * 4 / (1024 * 2.4e9 * kernel_ms * 1e-3)
-    return {"bound": "valu", "insts_per_launch": round(insts), "insts_per_pbs": round(insts / B),
-            "issue_frac": round(frac, 3), "model": "4 cycles per wave64 VALU instruction per SIMD, 1024 SIMDs, 2.4 GHz",
-            "source": os.path.relpath(src, ROOT)}
+    out = {"bound": "valu", "insts_per_launch": round(insts), "insts_per_pbs": round(insts / B),
+           "issue_frac": round(frac, 3), "model": "4 cycles per wave64 VALU instruction per SIMD, 1024 SIMDs, 2.4 GHz",
+           "source": os.path.relpath(src, ROOT)}
+    # the same instructions priced at the f64 rate measured on this hardware (independent v_fma_f64 /
+    # v_add_f64 chains, 2 waves per SIMD: tools/microbench/f64_rates.hip -> profiles/r01_f64_rates.txt)
+    rates = os.path.join(ROOT, "profiles", "r01_f64_rates.txt")
+    if "fft" in kernel and os.path.exists(rates):
+        cyc = [float(l.split()[3]) for l in open(rates) if l.split() and l.split()[0] in ("v_fma_f64", "v_add_f64")]
+        if cyc:
+            c = sum(cyc) / len(cyc)
+            out["measured_rate_frac"] = round(insts * c / (1024 * 2.4e9 * kernel_ms * 1e-3), 3)
+            out["measured_rate_model"] = f"{c:.2f} nominal cycles per f64 wave64 instruction (microbenchmark)"
+    return out
 
 
 def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int, preset: int = 0,
