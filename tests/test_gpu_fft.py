@@ -109,3 +109,27 @@ def test_batch_4096_decrypts_and_sampled_bitexact(fft_engine, fft_keys, oracle_m
     sample = np.r_[0:16, 4080:4096]
     ref = oracle_mod.pbs_batch_fft(fft_params, fft_okeys, cts[sample], oracle_mod.lut_constant(N, 1 << 61)[None])
     assert np.array_equal(out[sample], ref)
+
+
+@pytest.mark.parametrize("B", [1, 9, 300])
+def test_latency_and_batch_kernels_agree(fft_engine, fft_keys, oracle_mod, fft_params, fft_okeys, B):
+    """The latency-mode kernel (one ciphertext per workgroup, 6 transforms in parallel) and the batch
+    kernel (8 ciphertexts per workgroup) produce identical accumulators and PBS outputs."""
+    ck, _ = fft_keys
+    rng = np.random.default_rng(B + 1024)
+    msgs = rng.integers(0, 8, B).astype(np.uint64) * np.uint64((1 << 63) // 8)
+    cts = ck.encrypt_torus(msgs, seed=0xC0FFEE90 + B)
+    lut = oracle_mod.lut_from_table(N, 8, [(3 * m + 1) % 8 for m in range(8)], (1 << 63) // 8)
+    try:
+        fft_engine.set_latency_batch(0)
+        acc_b = fft_engine.blind_rotate(cts, lut)
+        out_b = fft_engine.pbs(cts, lut)
+        fft_engine.set_latency_batch(1 << 20)
+        acc_l = fft_engine.blind_rotate(cts, lut)
+        out_l = fft_engine.pbs(cts, lut)
+    finally:
+        fft_engine.set_latency_batch(768)
+    assert np.array_equal(acc_l, acc_b)
+    assert np.array_equal(out_l, out_b)
+    i = B // 2
+    assert np.array_equal(acc_l[i], oracle_mod.blind_rotate_fft(fft_params, fft_okeys, cts[i], lut))

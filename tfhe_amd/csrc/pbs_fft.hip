@@ -307,6 +307,142 @@ __global__ __launch_bounds__(FB_THREADS, 1) void blind_rotate_fft_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Latency-mode blind rotation (small batches): ONE ciphertext per workgroup of 8 waves.  Per CMUX:
+//   A  waves 0..5: wave r = chain position (c, q) (c = r / 3; q = 0, 1, 2: levels least significant
+//      first) rotates + decomposes accumulator polynomial c, keeps step q's digits and transforms
+//      them -> F[r]                                                     (6 transforms in parallel)
+//   B  all 8 waves: O_j = fma chain over r = 0..5 of F[r] (.) BSK_i[r][j] (the oracle's order) on 2
+//      of the 8 slots each (j = wave >> 2); the BSK words come straight from L2, loaded into
+//      registers before phase A so their latency hides behind the transforms
+//   C  waves 0, 1: inverse transform of O_j, acc_j += rint mod 2^64      (2 transforms in parallel)
+// Three barriers per CMUX; the critical path is 1 forward + 1 inverse transform + 1/4 of the MAC
+// instead of 6 + 2 + all of it.  LDS (tables first: small DS immediates): tw 32 KB | acc 16 KB |
+// F 48 KB | 6 transpose areas 54 KB (O_0, O_1 alias areas 2, 3, dead after phase A) = 150 KB.
+constexpr int FL_THREADS = 512;
+struct FftLatShared {
+  double2 tw[TW_C64];
+  u64 A[2][N1K];
+  double2 F[6][M];
+  double2 T[6][T_C64];
+};
+
+template <bool WRITE_ACC, bool WRITE_BIG>
+__global__ __launch_bounds__(FL_THREADS, 1) void blind_rotate_fft_lat_kernel(
+    const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
+    int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tw_g, u64* __restrict__ out_big,
+    u64* __restrict__ out_acc) {
+  __shared__ __attribute__((aligned(16))) FftLatShared sh;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t b = blockIdx.x;
+  const u64* ct = lwe_in + b * (size_t)(n + 1);
+  const TBase tb(lane);
+
+  for (int q = threadIdx.x; q < TW_C64; q += FL_THREADS) sh.tw[q] = tw_g[q];
+  {
+    int li = lut_index ? (int)lut_index[b] : 0;
+    li = (li < 0 || li >= n_lut) ? 0 : li;
+    const u64* lut = luts + (size_t)li * N1K;
+    const int s = (2048 - ms2048(ct[n])) & 2047;
+    for (int q = threadIdx.x; q < N1K; q += FL_THREADS) {
+      int d = q - s;
+      bool neg = false;
+      if (d < 0) { d += N1K; neg = !neg; }
+      if (d < 0) { d += N1K; neg = !neg; }
+      const u64 v = gl_to_torus(lut[d]);
+      sh.A[0][q] = 0;
+      sh.A[1][q] = neg ? 0 - v : v;
+    }
+  }
+  __syncthreads();
+
+  const int j = wave >> 2, s0 = (wave & 3) * 2;  // phase B: output j, slots s0, s0 + 1
+  for (int i = 0; i < n; i++) {
+    const int a = ms2048(ct[i]);
+    // phase-B key words of this CMUX, requested now, consumed after phase A
+    double2 kv[6][2];
+#pragma unroll
+    for (int r = 0; r < 6; r++)
+#pragma unroll
+      for (int t = 0; t < 2; t++) kv[r][t] = bsk[((size_t)(i * 6 + r) * 2 + j) * M + 64 * (s0 + t) + lane];
+    if (wave < 6) {  // phase A
+      const int c = wave / 3, q = wave % 3;
+      const u64* acc = sh.A[c];
+      u32 st[16];
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        const int t = 64 * e + lane - a + 2 * N1K;
+        const u64 x = acc[t & (N1K - 1)];
+        const u64 r = (t & N1K) ? 0 - x : x;
+        st[e] = decomp_state(r - acc[64 * e + lane]);
+      }
+      int dg[16];
+      for (int qq = 0; qq <= q; qq++) {
+        const u32 bmask = qq < 2 ? 1u : 0u;
+#pragma unroll
+        for (int e = 0; e < 16; e++) dg[e] = decomp_step(st[e], bmask);
+      }
+      double xr[8], xi[8];
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        xr[e] = (double)dg[e];
+        xi[e] = (double)dg[e + 8];
+        cmul<false>(xr[e], xi[e], sh.tw[TW_TWIST + 64 * e + lane]);
+      }
+      dft512_fwd(xr, xi, sh.T[wave], lane, tb, sh.tw);
+#pragma unroll
+      for (int e = 0; e < 8; e++) sh.F[wave][64 * e + lane] = make_double2(xr[e], xi[e]);
+    }
+    __syncthreads();
+    {  // phase B
+      double2* O = sh.T[2 + j];
+#pragma unroll
+      for (int t = 0; t < 2; t++) {
+        const int e = s0 + t;
+        double re = 0.0, im = 0.0;
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+          const double2 D = sh.F[r][64 * e + lane], K = kv[r][t];
+          re = __builtin_fma(D.x, K.x, re);
+          re = __builtin_fma(-D.y, K.y, re);
+          im = __builtin_fma(D.x, K.y, im);
+          im = __builtin_fma(D.y, K.x, im);
+        }
+        O[64 * e + lane] = make_double2(re, im);
+      }
+    }
+    __syncthreads();
+    if (wave < 2) {  // phase C
+      const double2* O = sh.T[2 + wave];
+      double xr[8], xi[8];
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const double2 v = O[64 * e + lane];
+        xr[e] = v.x;
+        xi[e] = v.y;
+      }
+      fft_inv_real(xr, xi, sh.T[wave], lane, tb, sh.tw);
+      u64* acc = sh.A[wave];
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        acc[64 * e + lane] += f64_to_torus(xr[e]);
+        acc[64 * (e + 8) + lane] += f64_to_torus(xi[e]);
+      }
+    }
+    __syncthreads();
+  }
+
+  if (WRITE_ACC) {
+    u64* oa = out_acc + b * 2048;
+    for (int q = threadIdx.x; q < 2 * N1K; q += FL_THREADS) oa[q] = sh.A[q >> 10][q & (N1K - 1)];
+  }
+  if (WRITE_BIG) {  // sample extraction at degree 0
+    u64* ob = out_big + b * (size_t)(N1K + 1);
+    for (int q = threadIdx.x; q <= N1K; q += FL_THREADS)
+      ob[q] = q == N1K ? sh.A[1][0] : q == 0 ? sh.A[0][0] : 0 - sh.A[0][N1K - q];
+  }
+}
+
 __global__ void sample_extract_torus_kernel(const u64* __restrict__ acc, size_t B, u64* __restrict__ out) {
   const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * (N1K + 1)) return;
@@ -385,11 +521,24 @@ hipError_t launch_bsk_to_fourier(const u64* bsk_std, double* bsk_f, size_t polys
 
 hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
                                    int n_lut, const double* bsk_f, const double* tw, u64* out_big, u64* out_acc,
-                                   hipStream_t s) {
+                                   hipStream_t s, size_t latency_max_batch) {
   using namespace fftk;
   if (B == 0) return hipSuccess;
-  dim3 grid((unsigned)((B + FB_WAVES - 1) / FB_WAVES)), block(FB_THREADS);
   const double2 *bk = (const double2*)bsk_f, *t = (const double2*)tw;
+  if (B <= latency_max_batch) {
+    dim3 grid((unsigned)B), block(FL_THREADS);
+    if (out_acc && out_big)
+      hipLaunchKernelGGL((blind_rotate_fft_lat_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                         n_lut, bk, t, out_big, out_acc);
+    else if (out_acc)
+      hipLaunchKernelGGL((blind_rotate_fft_lat_kernel<true, false>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                         n_lut, bk, t, out_big, out_acc);
+    else
+      hipLaunchKernelGGL((blind_rotate_fft_lat_kernel<false, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                         n_lut, bk, t, out_big, out_acc);
+    return hipGetLastError();
+  }
+  dim3 grid((unsigned)((B + FB_WAVES - 1) / FB_WAVES)), block(FB_THREADS);
   if (out_acc && out_big)
     hipLaunchKernelGGL((blind_rotate_fft_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index, n_lut,
                        bk, t, out_big, out_acc);

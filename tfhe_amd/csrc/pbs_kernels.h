@@ -32,9 +32,10 @@ hipError_t launch_keyswitch_mfma(const u64* in_big, size_t B, int big_dim, const
 size_t fft_tables_len();  // doubles
 void make_fft_tables(double* tw);
 hipError_t launch_bsk_to_fourier(const u64* bsk_std, double* bsk_f, size_t polys, const double* tw, hipStream_t s);
+// batches of at most latency_max_batch ciphertexts use the latency kernel (one ciphertext per workgroup)
 hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
                                    int n_lut, const double* bsk_f, const double* tw, u64* out_big, u64* out_acc,
-                                   hipStream_t s);
+                                   hipStream_t s, size_t latency_max_batch = 0);
 hipError_t launch_sample_extract_torus(const u64* acc, size_t B, u64* out, hipStream_t s);
 hipError_t launch_fft_fwd(const u64* in, size_t count, double* out, const double* tw, hipStream_t s);
 hipError_t launch_fft_inv(const double* in, size_t count, double* out, const double* tw, hipStream_t s);
