@@ -72,3 +72,36 @@ def fhevm_engine(fhevm_keys):
     eng.load_keys(sk)
     yield eng
     eng.close()
+
+
+# ---- FFT64 engines (tfhe-rs's f64-FFT arithmetic) for message-level suites -------------------
+@pytest.fixture(scope="session")
+def gate_fft_keys():
+    import tfhe_amd
+    return tfhe_amd.gen_keys(tfhe_amd.Params.preset(tfhe_amd.PRESET_GATE_FFT), KEY_SEED)
+
+
+@pytest.fixture(scope="session")
+def gate_fft_engine(gate_fft_keys):
+    import tfhe_amd
+    ck, sk = gate_fft_keys
+    eng = tfhe_amd.Engine(ck.params, 0)
+    eng.load_keys(sk)
+    yield eng
+    eng.close()
+
+
+@pytest.fixture(scope="session")
+def fhevm_fft_keys():
+    import tfhe_amd
+    return tfhe_amd.gen_keys(tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM_FFT), KEY_SEED)
+
+
+@pytest.fixture(scope="session")
+def fhevm_fft_engine(fhevm_fft_keys):
+    import tfhe_amd
+    ck, sk = fhevm_fft_keys
+    eng = tfhe_amd.Engine(ck.params, 0)
+    eng.load_keys(sk)
+    yield eng
+    eng.close()

@@ -23,8 +23,10 @@ def _width(t):
     return 1 if t == "ebool" else int(t.lstrip("e").replace("uint", ""))
 
 
-def test_fhevm_kats_gpu(engine, product_keys):
-    ck, _ = product_keys
+@pytest.mark.parametrize("transform", ["ntt", "fft64"])
+def test_fhevm_kats_gpu(request, transform):
+    engine = request.getfixturevalue("engine" if transform == "ntt" else "gate_fft_engine")
+    ck, _ = request.getfixturevalue("product_keys" if transform == "ntt" else "gate_fft_keys")
     with open(GOLDEN) as f:
         kats = json.load(f)
     c = I.Circuit(engine)

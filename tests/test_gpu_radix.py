@@ -13,8 +13,10 @@ from test_radix import GOLDEN, _w, supported
 pytestmark = pytest.mark.gpu
 
 
-def test_radix_kats_gpu(fhevm_engine, fhevm_keys):
-    ck, _ = fhevm_keys
+@pytest.mark.parametrize("transform", ["ntt", "fft64"])
+def test_radix_kats_gpu(request, transform):
+    fhevm_engine = request.getfixturevalue("fhevm_engine" if transform == "ntt" else "fhevm_fft_engine")
+    ck, _ = request.getfixturevalue("fhevm_keys" if transform == "ntt" else "fhevm_fft_keys")
     with open(GOLDEN) as f:
         kats = [k for k in json.load(f) if supported(k)]
     c = R.RadixCircuit(fhevm_engine)
