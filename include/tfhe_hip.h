@@ -163,14 +163,15 @@ int tfhe_hip_fft_inv(tfhe_ctx* ctx, const double* in, size_t count, double* out)
 /* Gate bootstrapping (FheBool NAND): out = PBS((0, 1/8) - c1 - c2, LUT == 1/8), B gates. */
 int tfhe_hip_nand(tfhe_ctx* ctx, const uint64_t* c1, const uint64_t* c2, size_t B, uint64_t* out);
 
-/* Wait for all work on the ctx stream. */
 /* Batches of at most max_batch ciphertexts run the latency blind-rotate kernel (one ciphertext per
  * workgroup: 4.5x (N=1024) / 2.5x (N=2048) lower PBS latency — the lockstep levels of integer
  * circuits, single /evaluate requests, packages/luxfhejs/src/index.ts:56-141 call patterns); larger
- * batches the throughput kernel.  Defaults = the measured crossovers on MI355X (tools/latency_sweep.py):
- * 1024 for N=1024 (55 vs 61 ms at B=1024, 69 vs 62 at 1280), 512 for N=2048 (42 vs 53 ms at 512,
- * 63 vs 53 at 768); 0 disables the latency kernel. */
+ * batches the throughput kernel.  Defaults = the measured crossovers on MI355X (tools/latency_sweep.py,
+ * tools/latency_sweep_fft.sh): NTT engine 1024 for N=1024 (55 vs 61 ms at B=1024, 69 vs 62 at 1280),
+ * 512 for N=2048 (42 vs 53 ms at 512, 63 vs 53 at 768); FFT64 engine 768 for N=1024 (3.7 ms for 1-64
+ * ciphertexts, 7.6 vs 14.9 ms at 512), none for N=2048 (0); 0 disables the latency kernel. */
 int tfhe_hip_set_latency_batch(tfhe_ctx* ctx, size_t max_batch);
+/* Wait for all work on the ctx stream. */
 int tfhe_hip_sync(tfhe_ctx* ctx);
 /* Per-kernel device timing (HIP events recorded on the launch stream around every blind-rotate /
  * keyswitch launch).  reset clears the record; stats waits for the recorded events and returns the
