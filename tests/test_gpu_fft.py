@@ -128,7 +128,7 @@ def test_latency_and_batch_kernels_agree(fft_engine, fft_keys, oracle_mod, fft_p
         acc_l = fft_engine.blind_rotate(cts, lut)
         out_l = fft_engine.pbs(cts, lut)
     finally:
-        fft_engine.set_latency_batch(768)
+        fft_engine.set_latency_batch(1024)
     assert np.array_equal(acc_l, acc_b)
     assert np.array_equal(out_l, out_b)
     i = B // 2

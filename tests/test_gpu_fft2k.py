@@ -100,3 +100,27 @@ def test_pbs2k_batch_4096_decrypts_and_sampled_bitexact(f2_engine, f2_keys, orac
     assert np.array_equal(out[sample], oracle_mod.pbs_batch_fft(f2_prm, f2_okeys, cts[sample], acc[None]))
     out2 = f2_engine.pbs(out[:512], acc)  # chained: f(f(m))
     assert np.array_equal(ck.decrypt(out2, MM), np.array([f(f(int(m))) for m in msgs[:512]], dtype=np.uint64))
+
+
+@pytest.mark.parametrize("B", [1, 7, 100])
+def test_latency_and_batch_kernels_agree_2k(f2_engine, f2_keys, oracle_mod, f2_prm, f2_okeys, B):
+    ck, _ = f2_keys
+    rng = np.random.default_rng(B + 4096)
+    msgs = rng.integers(0, MM, B).astype(np.uint64)
+    cts = ck.encrypt(msgs, MM, seed=0xC0FFEEA0 + B)
+    lut = oracle_mod.lut_from_table(N, MM, [(7 * m + 2) % MM for m in range(MM)], DELTA)
+    small = f2_engine.keyswitch(cts)
+    try:
+        f2_engine.set_latency_batch(0)
+        acc_b = f2_engine.blind_rotate(small, lut)
+        out_b = f2_engine.pbs(cts, lut)
+        f2_engine.set_latency_batch(1 << 20)
+        acc_l = f2_engine.blind_rotate(small, lut)
+        out_l = f2_engine.pbs(cts, lut)
+    finally:
+        f2_engine.set_latency_batch(1024)
+    assert np.array_equal(acc_l, acc_b)
+    assert np.array_equal(out_l, out_b)
+    i = B // 2
+    assert np.array_equal(acc_l[i], oracle_mod.blind_rotate_fft(f2_prm, f2_okeys, small[i], lut))
+    assert np.array_equal(ck.decrypt(out_l, MM), (7 * msgs + 2) % MM)

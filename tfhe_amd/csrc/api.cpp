@@ -166,7 +166,7 @@ hipError_t launch_br(tfhe_ctx* c, const u64* in, size_t B, const u64* luts, cons
                      u64* out_acc, hipStream_t s) {
   if (is_fft(c->p) && c->p.N == 2048)
     return tfhe::launch_blind_rotate_fft2k(in, B, (int)c->p.n, luts, idx, (int)n_lut, (const double*)c->d_bsk,
-                                           (const double*)c->d_tw, out_big, out_acc, s);
+                                           (const double*)c->d_tw, out_big, out_acc, s, c->lat_max);
   if (is_fft(c->p))
     return tfhe::launch_blind_rotate_fft(in, B, (int)c->p.n, luts, idx, (int)n_lut, (const double*)c->d_bsk,
                                          (const double*)c->d_tw, out_big, out_acc, s, c->lat_max);
@@ -375,7 +375,7 @@ int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out) {
     return cleanup(fail(TFHE_HIP_EDEVICE, "create: hipStreamCreate failed"));
   using namespace tfhe;
   if (is_fft(*p)) {  // FFT64: twist / pass tables (pbs_fft.hip: make_fft_tables); latency kernel at N = 1024
-    c->lat_max = p->N == 1024 ? 768 : 0;  // measured crossover (tools/latency_sweep_fft.sh)
+    c->lat_max = 1024;  // measured crossover, both N (tools/latency_sweep_fft.sh, tools/debug/lat_anomaly.py)
     std::vector<double> tw(p->N == 2048 ? fft2k_tables_len() : fft_tables_len());
     if (p->N == 2048) make_fft2k_tables(tw.data());
     else make_fft_tables(tw.data());

@@ -340,6 +340,166 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Latency-mode blind rotation at N = 2048 (small batches: the radix layer's lockstep levels): ONE
+// ciphertext per workgroup of 8 waves; the accumulator lives in LDS (split by parity), so no wave
+// pair exchanges the rotation.  Per CMUX:
+//   A  waves 0..3: wave (c, h) rotates + decomposes the parity-h coefficients of component c,
+//      transforms its 512-point half and, after one pair exchange, writes its half of the combined
+//      spectrum D_c to F[c]                                           (2 transforms in parallel)
+//   B  all 8 waves: O_j = D_0 (.) BSK_i[0][j] then + D_1 (.) BSK_i[1][j] (the oracle's fma chain) on
+//      4 of the 16 slots each (j = wave >> 2); key words prefetched into registers before phase A
+//   C  waves 0..3: wave (j, h) uncombines O_j straight from LDS into E_h, runs the 512-point inverse
+//      and adds the parity-h coefficients to acc_j                      (2 inverses in parallel)
+// Five barriers per CMUX.  LDS: table 48 KB | acc 32 KB | F 32 KB | 4 transpose areas 36 KB (O
+// aliases them between phase B and the uncombine) = 148 KB.
+constexpr int F2L_THREADS = 512;
+struct F2LatShared {
+  double2 tw[G_C64];
+  u64 A[2][N2];        // split layout: coefficient c at (c & 1) * 1024 + (c >> 1)
+  double2 F[2][M2];    // spectra, device order (index h * 512 + 64 s + L)
+  double2 T[4][T_C64];  // transposes; O_0, O_1 (2 x 1024 complex) alias T[0..3] after phase A
+};
+
+template <bool WRITE_ACC, bool WRITE_BIG>
+__global__ __launch_bounds__(F2L_THREADS, 1) void blind_rotate_fft2k_lat_kernel(
+    const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
+    int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tg, u64* __restrict__ out_big,
+    u64* __restrict__ out_acc) {
+  __shared__ __attribute__((aligned(16))) F2LatShared sh;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t b = blockIdx.x;
+  const u64* ct = lwe_in + b * (size_t)(n + 1);
+  const TBase tb(lane);
+  const double2* tt = sh.tw;
+  const double2* twp = sh.tw + G_PASS - TW_A;
+  double2* O = sh.T[0];  // 2 x 1024 complex across the four transpose areas
+
+  for (int q = threadIdx.x; q < G_C64; q += F2L_THREADS) sh.tw[q] = tg[q];
+  {
+    int li = lut_index ? (int)lut_index[b] : 0;
+    li = (li < 0 || li >= n_lut) ? 0 : li;
+    const u64* lut = luts + (size_t)li * N2;
+    const int s = (4096 - ms4096(ct[n])) & 4095;
+    for (int q = threadIdx.x; q < N2; q += F2L_THREADS) {
+      int d = q - s;
+      bool neg = false;
+      if (d < 0) { d += N2; neg = !neg; }
+      if (d < 0) { d += N2; neg = !neg; }
+      const u64 v = gl_to_torus(lut[d]);
+      sh.A[0][rsplit(q)] = 0;
+      sh.A[1][rsplit(q)] = neg ? 0 - v : v;
+    }
+  }
+  __syncthreads();
+
+  const int j = wave >> 2, sb = (wave & 3) * 4;  // phase B: output j, slots sb .. sb + 3 of 16
+  const int c = (wave >> 1) & 1, h = wave & 1;   // phases A / C (waves 0..3): component or output, parity
+  for (int i = 0; i < n; i++) {
+    const int a = ms4096(ct[i]);
+    double2 kv[2][4];
+#pragma unroll
+    for (int cc = 0; cc < 2; cc++)
+#pragma unroll
+      for (int t = 0; t < 4; t++) kv[cc][t] = bsk[((size_t)(i * 2 + cc) * 2 + j) * M2 + 64 * (sb + t) + lane];
+    // ---- phase A
+    double xr[8], xi[8];
+    if (wave < 4) {
+      const u64* acc = sh.A[c];
+      const int t0 = coef(h, lane, 0) + 2 * N2 - a;
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+          const int ee = e + 8 * u;
+          const int t = t0 + (coef(h, 0, ee) - h);
+          const u64 x = acc[rsplit(t)];
+          const u64 m = 0ull - (u64)((t >> 11) & 1);
+          const u64 y = ((x ^ m) - m) - acc[rsplit(coef(h, lane, ee))];
+          const double dv = (double)decomp_23x1_hi((u32)(y >> 32));
+          if (u == 0) xr[e] = dv;
+          else xi[e] = dv;
+        }
+        cmul<false>(xr[e], xi[e], tt[(h ? G_TW1 : G_TW0) + 64 * e + lane]);
+      }
+      dft512_fwd(xr, xi, sh.T[wave], lane, tb, twp);
+#pragma unroll
+      for (int e = 0; e < 8; e++) sh.T[wave][64 * e + lane] = make_double2(xr[e], xi[e]);
+    }
+    __syncthreads();
+    if (wave < 4) {
+      const double2* T0 = sh.T[2 * c];
+      const double2* T1 = sh.T[2 * c + 1];
+      double2* F = sh.F[c] + h * 512;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int e = 4 * h + q;
+        const double2 e0 = T0[64 * e + lane], e1 = T1[64 * e + lane];
+        double tr = e1.x, ti = e1.y;
+        cmul<false>(tr, ti, tt[G_WC + 256 * h + 64 * q + lane]);
+        F[64 * q + lane] = make_double2(e0.x + tr, e0.y + ti);
+        F[64 * (q + 4) + lane] = make_double2(e0.x - tr, e0.y - ti);
+      }
+    }
+    __syncthreads();
+    // ---- phase B (O overwrites the transpose areas: every exchange read is done)
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int q = 64 * (sb + t) + lane;
+      const double2 d0 = sh.F[0][q], d1 = sh.F[1][q], k0 = kv[0][t], k1 = kv[1][t];
+      double re = __builtin_fma(d0.x, k0.x, 0.0);
+      re = __builtin_fma(-d0.y, k0.y, re);
+      double im = __builtin_fma(d0.x, k0.y, 0.0);
+      im = __builtin_fma(d0.y, k0.x, im);
+      re = __builtin_fma(d1.x, k1.x, re);
+      re = __builtin_fma(-d1.y, k1.y, re);
+      im = __builtin_fma(d1.x, k1.y, im);
+      im = __builtin_fma(d1.y, k1.x, im);
+      O[j * M2 + q] = make_double2(re, im);
+    }
+    __syncthreads();
+    // ---- phase C: uncombine O_j into E_h (all 8 slots of the 512-point half), then the inverse
+    if (wave < 4) {
+      const double2* Oj = O + c * M2;  // here c = output j
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const int hh = e >> 2, q = e & 3;
+        const double2 lo = Oj[hh * 512 + 64 * q + lane], hi = Oj[hh * 512 + 64 * (q + 4) + lane];
+        if (h == 0) {
+          xr[e] = lo.x + hi.x;
+          xi[e] = lo.y + hi.y;
+        } else {
+          double dr = lo.x - hi.x, di = lo.y - hi.y;
+          cmul<true>(dr, di, tt[G_WC + 256 * hh + 64 * q + lane]);
+          xr[e] = dr;
+          xi[e] = di;
+        }
+      }
+    }
+    __syncthreads();  // O is read before the inverse transposes overwrite the areas
+    if (wave < 4) {
+      inv_half(xr, xi, h, lane, tb, sh.T[wave], twp, tt);
+      u64* acc = sh.A[c];
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        acc[rsplit(coef(h, lane, e))] += f64_to_torus_wide(xr[e]);
+        acc[rsplit(coef(h, lane, e + 8))] += f64_to_torus_wide(xi[e]);
+      }
+    }
+    __syncthreads();
+  }
+
+  if (WRITE_ACC) {
+    u64* oa = out_acc + b * (2 * N2);
+    for (int q = threadIdx.x; q < 2 * N2; q += F2L_THREADS) oa[q] = sh.A[q >> 11][rsplit(q & (N2 - 1))];
+  }
+  if (WRITE_BIG) {  // sample extraction at degree 0
+    u64* ob = out_big + b * (size_t)(N2 + 1);
+    for (int q = threadIdx.x; q <= N2; q += F2L_THREADS)
+      ob[q] = q == N2 ? sh.A[1][0] : q == 0 ? sh.A[0][0] : 0 - sh.A[0][rsplit(N2 - q)];
+  }
+}
+
 __global__ void sample_extract_torus2k_kernel(const u64* __restrict__ acc, size_t B, u64* __restrict__ out) {
   const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * (N2 + 1)) return;
@@ -407,11 +567,24 @@ hipError_t launch_fft2k_inv(const double* in, size_t count, double* out, const d
 
 hipError_t launch_blind_rotate_fft2k(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
                                      int n_lut, const double* bsk_f, const double* tw, u64* out_big, u64* out_acc,
-                                     hipStream_t s) {
+                                     hipStream_t s, size_t latency_max_batch) {
   using namespace fft2k;
   if (B == 0) return hipSuccess;
-  dim3 grid((unsigned)((B + F2_PAIRS - 1) / F2_PAIRS)), block(F2_THREADS);
   const double2 *bk = (const double2*)bsk_f, *t = (const double2*)tw;
+  if (B <= latency_max_batch) {
+    dim3 grid((unsigned)B), block(F2L_THREADS);
+    if (out_acc && out_big)
+      hipLaunchKernelGGL((blind_rotate_fft2k_lat_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                         n_lut, bk, t, out_big, out_acc);
+    else if (out_acc)
+      hipLaunchKernelGGL((blind_rotate_fft2k_lat_kernel<true, false>), grid, block, 0, s, lwe_in, n, B, luts,
+                         lut_index, n_lut, bk, t, out_big, out_acc);
+    else
+      hipLaunchKernelGGL((blind_rotate_fft2k_lat_kernel<false, true>), grid, block, 0, s, lwe_in, n, B, luts,
+                         lut_index, n_lut, bk, t, out_big, out_acc);
+    return hipGetLastError();
+  }
+  dim3 grid((unsigned)((B + F2_PAIRS - 1) / F2_PAIRS)), block(F2_THREADS);
   if (out_acc && out_big)
     hipLaunchKernelGGL((blind_rotate_fft2k_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
                        n_lut, bk, t, out_big, out_acc);

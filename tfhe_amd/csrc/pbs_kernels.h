@@ -46,7 +46,7 @@ void make_fft2k_tables(double* tw);
 hipError_t launch_bsk_to_fourier2k(const u64* bsk_std, double* bsk_f, size_t polys, const double* tw, hipStream_t s);
 hipError_t launch_blind_rotate_fft2k(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
                                      int n_lut, const double* bsk_f, const double* tw, u64* out_big, u64* out_acc,
-                                     hipStream_t s);
+                                     hipStream_t s, size_t latency_max_batch = 0);
 hipError_t launch_sample_extract_torus2k(const u64* acc, size_t B, u64* out, hipStream_t s);
 hipError_t launch_fft2k_fwd(const u64* in, size_t count, double* out, const double* tw, hipStream_t s);
 hipError_t launch_fft2k_inv(const double* in, size_t count, double* out, const double* tw, hipStream_t s);
