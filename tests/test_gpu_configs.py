@@ -6,6 +6,8 @@ C3: "FheUint8 LUT eval (8 PBS per ciphertext), batch=4096" — 4096 FheUint8 val
 C5: "FheUint32 comparison tree, 256 bidders" — tfhe_amd.auction.max_tree: 255 FheUint32 max
     comparisons in 8 dependent levels (lockstep per level), with the winner's index.
 """
+import time
+
 import numpy as np
 import pytest
 
@@ -37,9 +39,12 @@ def test_c3_fheuint8_lut_eval_4096(engine, product_keys, oracle_mod, gate_params
     assert np.array_equal(Y.bits[sel].reshape(-1, X.bits.shape[-1]), ref)
 
 
-def test_c5_auction_max_tree_256(engine, product_keys):
-    ck, _ = product_keys
+@pytest.mark.parametrize("transform", ["ntt", "fft64"])
+def test_c5_auction_max_tree_256(request, transform):
+    engine = request.getfixturevalue("engine" if transform == "ntt" else "gate_fft_engine")
+    ck, _ = request.getfixturevalue("product_keys" if transform == "ntt" else "gate_fft_keys")
     B = 256
+    t0 = time.time()
     v = np.random.default_rng(5).integers(0, 2**32, B, dtype=np.uint64)
     v[77] = v[200] = np.uint64(2**32 - 3)            # tie at the top: the lower index wins
     c = I.Circuit(engine)
@@ -48,3 +53,4 @@ def test_c5_auction_max_tree_256(engine, product_keys):
     assert int(mx.decrypt(ck)[0]) == 2**32 - 3
     assert int(idx.decrypt(ck)[0]) == 77
     assert c.pbs_count > 255 * 100                   # really ran the comparator circuits
+    print(f"C5 {transform}: {time.time() - t0:.2f} s, {c.pbs_count} PBS in {c.launches} launches")
