@@ -4,7 +4,7 @@ const assert = require('assert');
 const t = require('../../js');
 
 (async () => {
-  const p = t.paramsPreset(t.PRESET_GATE);
+  const p = t.paramsPreset(Number(process.argv[2] || t.PRESET_GATE));  // 0: NTT engine, 2: FFT64 engine
   const [ck, sk] = t.genKeys(p, 0x7F4E0001n);
   const eng = new t.Engine(p, 0).loadKeys(sk);
   const a = [false, false, true, true], b = [false, true, false, true];

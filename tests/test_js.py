@@ -22,9 +22,9 @@ def _ensure_addon():
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "js")], check=True)
 
 
-def _run(script, timeout):
+def _run(script, timeout, *args):
     _ensure_addon()
-    r = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", script)], capture_output=True, text=True,
+    r = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", script), *args], capture_output=True, text=True,
                        timeout=timeout, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     return json.loads(r.stdout.strip().splitlines()[-1])
@@ -47,8 +47,9 @@ def test_js_addon_cpu(product_keys):
 
 
 @pytest.mark.gpu
-def test_js_addon_gpu():
-    assert _run("gpu_check.js", 600)["ok"] is True
+@pytest.mark.parametrize("preset", ["0", "2"])  # P-GATE on the NTT and on the FFT64 engine
+def test_js_addon_gpu(preset):
+    assert _run("gpu_check.js", 600, preset)["ok"] is True
 
 
 def _run_plain(script, *args, timeout=600):
