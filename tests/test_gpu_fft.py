@@ -133,3 +133,39 @@ def test_latency_and_batch_kernels_agree(fft_engine, fft_keys, oracle_mod, fft_p
     assert np.array_equal(out_l, out_b)
     i = B // 2
     assert np.array_equal(acc_l[i], oracle_mod.blind_rotate_fft(fft_params, fft_okeys, cts[i], lut))
+
+
+def test_fft_edge_cases(fft_engine, oracle_mod, fft_params, fft_okeys):
+    """Empty batch, trivial ciphertexts (every CMUX skipped by the oracle, all-zero digits on the
+    device), mask values on the modulus-switch rounding boundaries, and a bad lut_index (EINVAL)."""
+    gate = fft_engine.gate_lut()
+    lut = oracle_mod.lut_constant(N, 1 << 61)[None]
+    assert fft_engine.pbs(np.zeros((0, 631), dtype=np.uint64), gate).shape == (0, 631)
+    triv = np.zeros((3, 631), dtype=np.uint64)
+    triv[:, 630] = [1 << 61, (1 << 64) - (1 << 61), (1 << 63) - 1]
+    edge = np.zeros((2, 631), dtype=np.uint64)
+    edge[0, :630] = np.uint64((1 << 52) - 1)
+    edge[1, :630] = np.uint64((1 << 64) - (1 << 52))
+    edge[:, 630] = 1 << 61
+    for lat in (0, 1024):  # batch kernel and latency kernel
+        fft_engine.set_latency_batch(lat)
+        assert np.array_equal(fft_engine.pbs(triv, gate), oracle_mod.pbs_batch_fft(fft_params, fft_okeys, triv, lut))
+        assert np.array_equal(fft_engine.pbs(edge, gate), oracle_mod.pbs_batch_fft(fft_params, fft_okeys, edge, lut))
+    fft_engine.set_latency_batch(1024)
+    with pytest.raises(tfhe_amd.TfheError) as e:
+        fft_engine.pbs(triv, gate, lut_index=[0, 1, 0])
+    assert e.value.code == -1
+
+
+def test_fft_large_batch_decrypts(fft_engine, fft_keys, oracle_mod, fft_params, fft_okeys):
+    """C4-sized shard on one GPU (16,384 PBS = 4 rounds of the batch kernel's grid): every output
+    decrypts, a sampled subset is bit-exact (size-independent properties)."""
+    ck, _ = fft_keys
+    B = 16384
+    bits = np.random.default_rng(36).integers(0, 2, B).astype(bool)
+    cts = ck.encrypt_bool(bits, seed=0xC0FFEE04)
+    out = fft_engine.pbs(cts, fft_engine.gate_lut())
+    assert np.array_equal(ck.decrypt_bool(out), bits)
+    sample = np.r_[0:4, 8190:8194, B - 4:B]
+    ref = oracle_mod.pbs_batch_fft(fft_params, fft_okeys, cts[sample], oracle_mod.lut_constant(N, 1 << 61)[None])
+    assert np.array_equal(out[sample], ref)
