@@ -135,6 +135,12 @@ __global__ __launch_bounds__(64) void fft_inv_kernel(const double2* __restrict__
 // while step g computes, the barrier before step g waits only for chunk g with a counted vmcnt):
 // measured 3 % slower on MI355X (31.2 vs 30.35 ms per 4096; the chunk arrives in time either way and
 // the third buffer costs registers), kept for A/B runs.
+// FFT_PRIO: s_setprio 1 for waves 4-7 (the second-dispatched wave of each SIMD pair) for the whole
+// CMUX loop; measured 29.36 -> 29.25 ms per 4096 (both waves of a SIMD run the same lockstep program, the
+// younger one otherwise loses VALU arbitration after every barrier).  2 = odd waves (same result).
+#ifndef FFT_PRIO
+#define FFT_PRIO 1
+#endif
 #ifndef FFT_KBUF
 #define FFT_KBUF 2
 #endif
@@ -274,6 +280,11 @@ __global__ __launch_bounds__(FB_THREADS, 1) void blind_rotate_fft_kernel(
   }
 
   const TBase tb(lane);
+#if FFT_PRIO == 1
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#elif FFT_PRIO == 2
+  if (wave & 1) __builtin_amdgcn_s_setprio(1);
+#endif
   for (int i = 0; i < n; i++) {
     const int rbase = lane - ms2048(ct[i]) + 2 * N1K;
     double o0r[8], o0i[8], o1r[8], o1i[8];

@@ -161,6 +161,8 @@ struct F2Shared {
   double2 K[2][M2];            // 32,768 B
 };
 typedef __attribute__((address_space(3))) const double lds_f64;
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const f64x2 lds_c64;  // one complex: a single ds_read_b128
 
 // BSK_i[c][0..1] (32 KB) into K: wave w loads the 1 KB blocks 4w .. 4w + 3 (wave-uniform scalar bases)
 __device__ __forceinline__ void load_pair(const double2* __restrict__ bsk, int i, int c, F2Shared& sh, int wave_s,
@@ -198,10 +200,10 @@ __device__ __forceinline__ void rotate_decompose(const u64 (&acc)[16], int a, in
 
 // LDS address of this wave's slot 0 in K, laundered: with K's absolute offset folded in, the MAC's
 // reads would exceed the 16-bit DS immediate and each take a VGPR of its own
-__device__ __forceinline__ lds_f64* kbase(F2Shared& sh, int h, int lane) {
+__device__ __forceinline__ lds_c64* kbase(F2Shared& sh, int h, int lane) {
   u32 a = (u32)(uintptr_t)(lds_f64*)&sh.K[0][h * 512 + lane];
   asm volatile("" : "+v"(a));
-  return (lds_f64*)(uintptr_t)a;
+  return (lds_c64*)(uintptr_t)a;
 }
 
 template <bool WRITE_ACC, bool WRITE_BIG>
@@ -259,10 +261,11 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's share of K_{0,*}; fwd_half's barriers publish it
     fwd_half(xr, xi, h, lane, tb, T0, T1, twp, tt);
     {  // MAC, c = 0 (oracle order: from (0, 0)); slot s of this wave = BSK index h * 512 + 64 s + L
-      lds_f64* kp = kbase(sh, h, lane);
+      lds_c64* kp = kbase(sh, h, lane);
 #pragma unroll
       for (int s = 0; s < 8; s++) {
-        const double k0r = kp[128 * s], k0i = kp[128 * s + 1], k1r = kp[2 * M2 + 128 * s], k1i = kp[2 * M2 + 128 * s + 1];
+        const f64x2 k0 = kp[64 * s], k1 = kp[M2 + 64 * s];  // whole complexes: two separate b64 reads 16 B apart conflict 2-way
+        const double k0r = k0.x, k0i = k0.y, k1r = k1.x, k1i = k1.y;
         o0r[s] = __builtin_fma(xr[s], k0r, 0.0);
         o0r[s] = __builtin_fma(-xi[s], k0i, o0r[s]);
         o0i[s] = __builtin_fma(xr[s], k0i, 0.0);
@@ -285,10 +288,11 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     fwd_half(xr, xi, h, lane, tb, T0, T1, twp, tt);
 
     {  // MAC, c = 1
-      lds_f64* kp = kbase(sh, h, lane);
+      lds_c64* kp = kbase(sh, h, lane);
 #pragma unroll
       for (int s = 0; s < 8; s++) {
-        const double k0r = kp[128 * s], k0i = kp[128 * s + 1], k1r = kp[2 * M2 + 128 * s], k1i = kp[2 * M2 + 128 * s + 1];
+        const f64x2 k0 = kp[64 * s], k1 = kp[M2 + 64 * s];  // whole complexes: two separate b64 reads 16 B apart conflict 2-way
+        const double k0r = k0.x, k0i = k0.y, k1r = k1.x, k1i = k1.y;
         o0r[s] = __builtin_fma(xr[s], k0r, o0r[s]);
         o0r[s] = __builtin_fma(-xi[s], k0i, o0r[s]);
         o0i[s] = __builtin_fma(xr[s], k0i, o0i[s]);
