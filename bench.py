@@ -31,6 +31,7 @@ compared bit-for-bit with the GPU's ("sample_bitexact").
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -121,8 +122,14 @@ def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int
     sel = cts[:sample]
     O.pbs_batch(prm, keys, sel[: max(1, threads // 4)], lut, threads=threads)  # warm tables
     t = time.time()
+    O.pbs_batch(prm, keys, sel[:1], lut, threads=1)  # single-thread latency of one PBS
+    lat_ms = (time.time() - t) * 1e3
+    t = time.time()
     ref = O.pbs_batch(prm, keys, sel, lut, threads=threads)
     dt = time.time() - t
+    exact = bool(np.array_equal(ref, gpu_out[:sample]))
+    digest = {"bitexact_pbs": sample, "gpu_sha256": hashlib.sha256(np.ascontiguousarray(gpu_out[:sample])).hexdigest(),
+              "oracle_sha256": hashlib.sha256(np.ascontiguousarray(ref)).hexdigest()}
     return {
         "value": round(sample / dt, 3),
         "unit": "PBS/s",
@@ -133,7 +140,8 @@ def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int
                   f"({'oracle/fft_oracle.c' if prm.transform == 1 else 'oracle/tfhe_oracle.c'}, -O3 "
                   f"-march=x86-64-v3, OpenMP {threads} threads, one PBS per thread), "
                   f"{dt:.1f}s",
-    }, bool(np.array_equal(ref, gpu_out[:sample]))
+        "single_thread_ms_per_pbs": round(lat_ms, 2),
+    }, exact, digest
 
 
 def main() -> int:
@@ -257,6 +265,11 @@ def main() -> int:
     br_avg = br_ms / max(br_n, 1)
     achieved = B * br_bytes / (br_avg * 1e-3) / 1e9
 
+    pd = params.as_dict()
+    bsk_bytes = pd["n"] * (pd["k"] + 1) * pd["pbs_level"] * (pd["k"] + 1) * pd["N"] * 8
+    ksk_bytes = pd["k"] * pd["N"] * pd["ks_level"] * (pd["n"] + 1) * 8
+    # ciphertexts in + out: small LWEs at P-GATE (PBS -> KS), big LWEs at P-FHEVM (KS -> PBS)
+    io_bytes = 16 * ((pd["n"] + 1) if pd["order"] == 0 else (pd["k"] * pd["N"] + 1))
     result = None
     if rank == 0:
         result = {
@@ -293,12 +306,16 @@ def main() -> int:
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None if fhevm else pmc_traffic(B, br_kernel),
+                "traffic": pmc_traffic(B, br_kernel),
                 "bytes_per_launch": B * br_bytes,
                 "kernel_ms": round(br_avg, 3),
                 "launches": br_n,
+                # the reuse the kernel implements and the true minimum traffic
+                "bsk_reuse": (f"each BSK level-step chunk is streamed once per workgroup into LDS and shared by its "
+                              f"{8 if not (fhevm and fft) else 4} ciphertexts; resident workgroups share it through L2"),
+                "min_traffic_bytes_per_pbs": round((bsk_bytes + ksk_bytes) / B + io_bytes),
             },
-            "valu_roofline": None if fhevm else valu_profile(B, br_avg, br_kernel),
+            "valu_roofline": valu_profile(B, br_avg, br_kernel),
             "keyswitch_ms": round(ks_ms / max(ks_n, 1), 3),
             "ms_noise_reduction_ms": round(msr_ms / msr_n, 3) if msr_n else None,
             "key_broadcast_ms": round(bcast_ms, 3),
@@ -308,13 +325,16 @@ def main() -> int:
             threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
             # ~10-20 s of CPU work: the oracle does ~3.5 PBS/s per thread on the NTT at P-GATE, ~23 on
             # FFT64, ~1.3 at P-FHEVM
-            sample = args.cpu_sample or (max(96 * threads, 32) if fhevm and fft else max(16 * threads, 32) if fhevm
-                                         else max(240 * threads, 64) if fft
+            # FFT64: the whole 4096 batch at 16 threads (~11 s at P-GATE, ~15 s at P-FHEVM), so every output is
+            # compared and the two SHA-256 digests cover the batch
+            sample = args.cpu_sample or (max(256 * threads, 32) if fhevm and fft else max(16 * threads, 32) if fhevm
+                                         else max(256 * threads, 64) if fft
                                          else max(40 * threads, 64))
-            cb, exact = cpu_baseline(cts, out, min(sample, B), threads, preset_id,
-                                     lut_host if fhevm else None)
+            cb, exact, digest = cpu_baseline(cts, out, min(sample, B), threads, preset_id,
+                                             lut_host if fhevm else None)
             result["cpu_baseline"] = cb
             result["sample_bitexact"] = exact
+            result["bitexact_check"] = digest
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
