@@ -1,0 +1,36 @@
+"""bench.py keeps the driver's contract: one JSON line with the metric, the whole-job value, the
+roofline and cpu_baseline objects, and a bit-exact oracle comparison of the sampled outputs
+(run here at a reduced batch so it takes seconds; the round-end bench runs the full 4096)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("preset", ["gate_fft", "fhevm_fft"])
+def test_bench_json_contract(preset):
+    r = subprocess.run([sys.executable, "bench.py", "--preset", preset, "--steps", "2", "--warmup", "1",
+                        "--batch", "512", "--cpu-sample", "32"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
+    assert d["dtype"] == "f64" and d["config"]["batch_per_gpu"] == 512
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3 and rf["kernel_ms"] > 0
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0
+    assert d["decrypt_ok"] is True and d["sample_bitexact"] is True
+    bx = d["bitexact_check"]
+    assert bx["bitexact_pbs"] == 32 and bx["gpu_sha256"] == bx["oracle_sha256"]
