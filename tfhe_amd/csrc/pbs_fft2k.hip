@@ -153,6 +153,11 @@ __global__ __launch_bounds__(128) void inv2k_kernel(const double2* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------------
+// F2_MACORDER = 1: transform both components, then one MAC per output column (see the loop)
+#ifndef F2_MACORDER
+#define F2_MACORDER 1
+#endif
+
 // the whole table first (every twiddle read: a per-lane base plus a 16-bit DS immediate offset), then
 // the transpose scratch, then two BSK polynomials (K_{c,0}, K_{c,1} of the component in flight)
 struct F2Shared {
@@ -206,6 +211,38 @@ __device__ __forceinline__ lds_c64* kbase(F2Shared& sh, int h, int lane) {
   return (lds_c64*)(uintptr_t)a;
 }
 
+// output column j of BSK_i (K_{0,j}, K_{1,j}: two 16 KB polynomials) into K[0], K[1]: waves 0-3 load the
+// first, waves 4-7 the second, 4 x 1 KB each
+__device__ __forceinline__ void load_column(const double2* __restrict__ bsk, int i, int j, F2Shared& sh, int wave_s,
+                                            int lane) {
+  constexpr int PER_WAVE = 2 * CHUNK_GLDS / F2_WAVES;
+  const int c = wave_s >> 2, part = wave_s & 3;
+  const char* src = (const char*)(bsk + ((size_t)i * 4 + 2 * c + j) * M2) + part * (PER_WAVE * 1024);
+  char* dst = (char*)sh.K[c] + part * (PER_WAVE * 1024);
+#pragma unroll
+  for (int q = 0; q < PER_WAVE; q++)
+    __builtin_amdgcn_global_load_lds((const void*)(src + q * 1024 + lane * 16),
+                                     (__attribute__((address_space(3))) void*)(dst + q * 1024), 16, 0, 0);
+}
+
+// O = D_0 (.) K[0] + D_1 (.) K[1], the oracle's fma chain from (0, 0) (c = 0 first)
+__device__ __forceinline__ void mac_column(lds_c64* kp, const double (&ar)[8], const double (&ai)[8],
+                                           const double (&br)[8], const double (&bi)[8], double (&or_)[8],
+                                           double (&oi)[8]) {
+#pragma unroll
+  for (int s = 0; s < 8; s++) {
+    const f64x2 u = kp[64 * s], v = kp[M2 + 64 * s];
+    or_[s] = __builtin_fma(ar[s], u.x, 0.0);
+    or_[s] = __builtin_fma(-ai[s], u.y, or_[s]);
+    oi[s] = __builtin_fma(ar[s], u.y, 0.0);
+    oi[s] = __builtin_fma(ai[s], u.x, oi[s]);
+    or_[s] = __builtin_fma(br[s], v.x, or_[s]);
+    or_[s] = __builtin_fma(-bi[s], v.y, or_[s]);
+    oi[s] = __builtin_fma(br[s], v.y, oi[s]);
+    oi[s] = __builtin_fma(bi[s], v.x, oi[s]);
+  }
+}
+
 template <bool WRITE_ACC, bool WRITE_BIG>
 __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
@@ -227,7 +264,11 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
 
   for (int q = threadIdx.x; q < G_C64; q += F2_THREADS) sh.tw[q] = tg[q];
   const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+#if F2_MACORDER
+  load_column(bsk, 0, 0, sh, wave_s, lane);
+#else
   load_pair(bsk, 0, 0, sh, wave_s, lane);
+#endif
 
   u64 accA[16], accB[16];
   {
@@ -247,6 +288,55 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     }
   }
 
+#if F2_MACORDER
+  // both components are transformed first (D_0 held in registers, not the 64 registers of O), then
+  // O_0 = D_0 K_{0,0} + D_1 K_{1,0} and O_1 = D_0 K_{0,1} + D_1 K_{1,1}: the key buffer holds one
+  // output column (K_{0,j}, K_{1,j}) at a time, so the j = 1 column loads between the two MACs
+  for (int i = 0; i < n; i++) {
+    const int a = ms4096(ct[i]);
+    int dg[16];
+    double d0r[8], d0i[8], xr[8], xi[8], o0r[8], o0i[8], o1r[8], o1i[8];
+    __syncthreads();  // the previous CMUX's inverse transforms are done with T
+    rotate_decompose(accA, a, h, lane, R, dg);
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      d0r[e] = (double)dg[e];
+      d0i[e] = (double)dg[e + 8];
+    }
+    fwd_half(d0r, d0i, h, lane, tb, T0, T1, twp, tt);
+    rotate_decompose(accB, a, h, lane, R, dg);
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      xr[e] = (double)dg[e];
+      xi[e] = (double)dg[e + 8];
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's share of column 0; fwd_half's barriers publish it
+    fwd_half(xr, xi, h, lane, tb, T0, T1, twp, tt);
+    mac_column(kbase(sh, h, lane), d0r, d0i, xr, xi, o0r, o0i);
+    __syncthreads();  // every wave is done with column 0
+    load_column(bsk, i, 1, sh, wave_s, lane);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();  // column 1 visible
+    mac_column(kbase(sh, h, lane), d0r, d0i, xr, xi, o1r, o1i);
+    __syncthreads();  // every wave is done with column 1 and with the pair exchanges
+    if (i + 1 < n) load_column(bsk, i + 1, 0, sh, wave_s, lane);
+    inv_exchange(o0r, o0i, h, lane, T0, T1, tt);
+    inv_half(o0r, o0i, h, lane, tb, Tm, twp, tt);
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      accA[e] += f64_to_torus_wide(o0r[e]);
+      accA[e + 8] += f64_to_torus_wide(o0i[e]);
+    }
+    __syncthreads();  // the partner's inverse transposes are done with its region
+    inv_exchange(o1r, o1i, h, lane, T0, T1, tt);
+    inv_half(o1r, o1i, h, lane, tb, Tm, twp, tt);
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      accB[e] += f64_to_torus_wide(o1r[e]);
+      accB[e + 8] += f64_to_torus_wide(o1i[e]);
+    }
+  }
+#else
   for (int i = 0; i < n; i++) {
     const int a = ms4096(ct[i]);
     int dg[16];
@@ -321,6 +411,8 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
       accB[e + 8] += f64_to_torus_wide(o1i[e]);
     }
   }
+
+#endif
 
   if (!live) return;
   if (WRITE_ACC) {
