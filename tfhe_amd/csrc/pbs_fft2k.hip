@@ -205,20 +205,22 @@ __device__ __forceinline__ void rotate_decompose(const u64 (&acc)[16], int a, in
 
 // LDS address of this wave's slot 0 in K, laundered: with K's absolute offset folded in, the MAC's
 // reads would exceed the 16-bit DS immediate and each take a VGPR of its own
-__device__ __forceinline__ lds_c64* kbase(F2Shared& sh, int h, int lane) {
-  u32 a = (u32)(uintptr_t)(lds_f64*)&sh.K[0][h * 512 + lane];
+__device__ __forceinline__ lds_c64* kbase(const double2* kbuf, int h, int lane) {
+  u32 a = (u32)(uintptr_t)(lds_f64*)&kbuf[h * 512 + lane];
   asm volatile("" : "+v"(a));
   return (lds_c64*)(uintptr_t)a;
 }
 
 // output column j of BSK_i (K_{0,j}, K_{1,j}: two 16 KB polynomials) into K[0], K[1]: waves 0-3 load the
 // first, waves 4-7 the second, 4 x 1 KB each
-__device__ __forceinline__ void load_column(const double2* __restrict__ bsk, int i, int j, F2Shared& sh, int wave_s,
-                                            int lane) {
+// (dst: the key buffer K, or for column 1 the transpose area, free between the forward transforms'
+// last exchange and the inverse transforms' first)
+__device__ __forceinline__ void load_column(const double2* __restrict__ bsk, int i, int j, double2* kbuf,
+                                            int wave_s, int lane) {
   constexpr int PER_WAVE = 2 * CHUNK_GLDS / F2_WAVES;
   const int c = wave_s >> 2, part = wave_s & 3;
   const char* src = (const char*)(bsk + ((size_t)i * 4 + 2 * c + j) * M2) + part * (PER_WAVE * 1024);
-  char* dst = (char*)sh.K[c] + part * (PER_WAVE * 1024);
+  char* dst = (char*)(kbuf + c * M2) + part * (PER_WAVE * 1024);
 #pragma unroll
   for (int q = 0; q < PER_WAVE; q++)
     __builtin_amdgcn_global_load_lds((const void*)(src + q * 1024 + lane * 16),
@@ -265,7 +267,7 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
   for (int q = threadIdx.x; q < G_C64; q += F2_THREADS) sh.tw[q] = tg[q];
   const int wave_s = __builtin_amdgcn_readfirstlane(wave);
 #if F2_MACORDER
-  load_column(bsk, 0, 0, sh, wave_s, lane);
+  load_column(bsk, 0, 0, &sh.K[0][0], wave_s, lane);
 #else
   load_pair(bsk, 0, 0, sh, wave_s, lane);
 #endif
@@ -290,8 +292,8 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
 
 #if F2_MACORDER
   // both components are transformed first (D_0 held in registers, not the 64 registers of O), then
-  // O_0 = D_0 K_{0,0} + D_1 K_{1,0} and O_1 = D_0 K_{0,1} + D_1 K_{1,1}: the key buffer holds one
-  // output column (K_{0,j}, K_{1,j}) at a time, so the j = 1 column loads between the two MACs
+  // O_0 = D_0 K_{0,0} + D_1 K_{1,0} and O_1 = D_0 K_{0,1} + D_1 K_{1,1}: the key buffer holds output
+  // column 0 (K_{0,0}, K_{1,0}); column 1 streams into the transpose area while MAC 0 runs
   for (int i = 0; i < n; i++) {
     const int a = ms4096(ct[i]);
     int dg[16];
@@ -312,14 +314,14 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's share of column 0; fwd_half's barriers publish it
     fwd_half(xr, xi, h, lane, tb, T0, T1, twp, tt);
-    mac_column(kbase(sh, h, lane), d0r, d0i, xr, xi, o0r, o0i);
-    __syncthreads();  // every wave is done with column 0
-    load_column(bsk, i, 1, sh, wave_s, lane);
+    double2* const kt = &sh.T[0][0];
+    load_column(bsk, i, 1, kt, wave_s, lane);  // column 1 into the (now idle) transpose area, under MAC 0
+    mac_column(kbase(&sh.K[0][0], h, lane), d0r, d0i, xr, xi, o0r, o0i);
     __builtin_amdgcn_s_waitcnt(0x0F70);
-    __syncthreads();  // column 1 visible
-    mac_column(kbase(sh, h, lane), d0r, d0i, xr, xi, o1r, o1i);
-    __syncthreads();  // every wave is done with column 1 and with the pair exchanges
-    if (i + 1 < n) load_column(bsk, i + 1, 0, sh, wave_s, lane);
+    __syncthreads();  // column 1 visible; every wave is done with column 0
+    if (i + 1 < n) load_column(bsk, i + 1, 0, &sh.K[0][0], wave_s, lane);
+    mac_column(kbase(kt, h, lane), d0r, d0i, xr, xi, o1r, o1i);
+    __syncthreads();  // every wave is done with column 1: the transpose area is free again
     inv_exchange(o0r, o0i, h, lane, T0, T1, tt);
     inv_half(o0r, o0i, h, lane, tb, Tm, twp, tt);
 #pragma unroll
@@ -351,7 +353,7 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's share of K_{0,*}; fwd_half's barriers publish it
     fwd_half(xr, xi, h, lane, tb, T0, T1, twp, tt);
     {  // MAC, c = 0 (oracle order: from (0, 0)); slot s of this wave = BSK index h * 512 + 64 s + L
-      lds_c64* kp = kbase(sh, h, lane);
+      lds_c64* kp = kbase(&sh.K[0][0], h, lane);
 #pragma unroll
       for (int s = 0; s < 8; s++) {
         const f64x2 k0 = kp[64 * s], k1 = kp[M2 + 64 * s];  // whole complexes: two separate b64 reads 16 B apart conflict 2-way
@@ -378,7 +380,7 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     fwd_half(xr, xi, h, lane, tb, T0, T1, twp, tt);
 
     {  // MAC, c = 1
-      lds_c64* kp = kbase(sh, h, lane);
+      lds_c64* kp = kbase(&sh.K[0][0], h, lane);
 #pragma unroll
       for (int s = 0; s < 8; s++) {
         const f64x2 k0 = kp[64 * s], k1 = kp[M2 + 64 * s];  // whole complexes: two separate b64 reads 16 B apart conflict 2-way
