@@ -375,7 +375,10 @@ int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out) {
     return cleanup(fail(TFHE_HIP_EDEVICE, "create: hipStreamCreate failed"));
   using namespace tfhe;
   if (is_fft(*p)) {  // FFT64: twist / pass tables (pbs_fft.hip: make_fft_tables); latency kernel at N = 1024
-    c->lat_max = 1024;  // measured crossover, both N (tools/latency_sweep_fft.sh, tools/debug/lat_anomaly.py)
+    // measured crossovers (tools/latency_sweep_fft.sh): N = 1024 at 1024; N = 2048 at 512 since the
+    // column-order batch kernel (15.3 ms per launch at B = 512 vs 2 rounds of latency kernels, 11.3 ms;
+    // 17.5 vs 18.0 ms at 640)
+    c->lat_max = p->N == 2048 ? 512 : 1024;
     std::vector<double> tw(p->N == 2048 ? fft2k_tables_len() : fft_tables_len());
     if (p->N == 2048) make_fft2k_tables(tw.data());
     else make_fft_tables(tw.data());
