@@ -118,7 +118,7 @@ def test_latency_and_batch_kernels_agree_2k(f2_engine, f2_keys, oracle_mod, f2_p
         acc_l = f2_engine.blind_rotate(small, lut)
         out_l = f2_engine.pbs(cts, lut)
     finally:
-        f2_engine.set_latency_batch(1024)
+        f2_engine.set_latency_batch(512)  # the N = 2048 FFT64 default
     assert np.array_equal(acc_l, acc_b)
     assert np.array_equal(out_l, out_b)
     i = B // 2
