@@ -290,6 +290,9 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     }
   }
 
+#if F2_PRIO
+  if (wave_s >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
 #if F2_MACORDER
   // both components are transformed first (D_0 held in registers, not the 64 registers of O), then
   // O_0 = D_0 K_{0,0} + D_1 K_{1,0} and O_1 = D_0 K_{0,1} + D_1 K_{1,1}: the key buffer holds output
