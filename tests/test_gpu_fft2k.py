@@ -124,3 +124,22 @@ def test_latency_and_batch_kernels_agree_2k(f2_engine, f2_keys, oracle_mod, f2_p
     i = B // 2
     assert np.array_equal(acc_l[i], oracle_mod.blind_rotate_fft(f2_prm, f2_okeys, small[i], lut))
     assert np.array_equal(ck.decrypt(out_l, MM), (7 * msgs + 2) % MM)
+
+
+def test_pbs2k_batch_kernel_ragged_multi_lut_1027(f2_engine, f2_keys, oracle_mod, f2_prm, f2_okeys):
+    """Above the latency crossover (512) with a ragged last workgroup (1027 = 4 * 256 + 3) and three
+    LUTs: every output decrypts to its LUT's value, a sample across the padding edge is bit-exact."""
+    ck, _ = f2_keys
+    B = 1027
+    rng = np.random.default_rng(1027)
+    msgs = rng.integers(0, MM, B).astype(np.uint64)
+    cts = ck.encrypt(msgs, MM, seed=0xC0FFEEB0)
+    luts = np.stack([oracle_mod.lut_from_table(N, MM, [(m * (s + 2) + 1) % MM for m in range(MM)], DELTA)
+                     for s in range(3)])
+    idx = rng.integers(0, 3, B).astype(np.uint32)
+    out = f2_engine.pbs(cts, luts, idx)
+    want = (msgs * (idx.astype(np.uint64) + 2) + 1) % MM
+    assert np.array_equal(ck.decrypt(out, MM), want)
+    sample = np.r_[0:4, 1020:1027]
+    ref = oracle_mod.pbs_batch_fft(f2_prm, f2_okeys, cts[sample], luts, idx[sample])
+    assert np.array_equal(out[sample], ref)
