@@ -168,10 +168,10 @@ int tfhe_hip_nand(tfhe_ctx* ctx, const uint64_t* c1, const uint64_t* c2, size_t 
  * circuits, single /evaluate requests, packages/luxfhejs/src/index.ts:56-141 call patterns); larger
  * batches the throughput kernel.  Defaults = the measured crossovers on MI355X (tools/latency_sweep.py,
  * tools/latency_sweep_fft.sh): NTT engine 1024 for N=1024 (55 vs 61 ms at B=1024, 69 vs 62 at 1280),
- * 512 for N=2048 (42 vs 53 ms at 512, 63 vs 53 at 768); FFT64 engine 1024 for N=1024 and 512 for
- * N=2048 (PBS per round of 256 ciphertexts on the latency kernel: 3.7 ms at N=1024, 5.7 ms at N=2048;
- * batch kernel 14.6 ms up to 2048 ciphertexts at N=1024, 15.3 ms at 512 and 16.0 ms at 1024 at
- * N=2048); 0 disables the latency kernel. */
+ * 512 for N=2048 (42 vs 53 ms at 512, 63 vs 53 at 768); FFT64 engine 512 for both N (PBS with the
+ * latency kernel: 3.9 / 7.9 ms at N=1024 for up to 256 / 512 ciphertexts, 5.7 / 11.3 ms at N=2048;
+ * batch kernel 14.5-15.5 ms up to 2048 ciphertexts at N=1024, 15.3-16.0 ms up to 1024 at N=2048);
+ * 0 disables the latency kernel. */
 int tfhe_hip_set_latency_batch(tfhe_ctx* ctx, size_t max_batch);
 /* Wait for all work on the ctx stream. */
 int tfhe_hip_sync(tfhe_ctx* ctx);

@@ -375,10 +375,11 @@ int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out) {
     return cleanup(fail(TFHE_HIP_EDEVICE, "create: hipStreamCreate failed"));
   using namespace tfhe;
   if (is_fft(*p)) {  // FFT64: twist / pass tables (pbs_fft.hip: make_fft_tables); latency kernel at N = 1024
-    // measured crossovers (tools/latency_sweep_fft.sh): N = 1024 at 1024; N = 2048 at 512 since the
-    // column-order batch kernel (15.3 ms per launch at B = 512 vs 2 rounds of latency kernels, 11.3 ms;
-    // 17.5 vs 18.0 ms at 640)
-    c->lat_max = p->N == 2048 ? 512 : 1024;
+    // measured crossovers (tools/latency_sweep_fft.sh), 512 for both N: N = 1024 7.9 ms (latency, two
+    // rounds) vs 14.8 (batch) at B = 512, 20.9 vs 14.9 at 768 (from the third round on, workgroups that
+    // start staggered stream the BSK from L2 at different CMUX indices and fall out of L2); N = 2048
+    // 11.3 vs 15.3 ms at 512, 18.0 vs 17.5 at 640
+    c->lat_max = 512;
     std::vector<double> tw(p->N == 2048 ? fft2k_tables_len() : fft_tables_len());
     if (p->N == 2048) make_fft2k_tables(tw.data());
     else make_fft_tables(tw.data());
