@@ -15,10 +15,15 @@ BSK/KSK once over RCCL (torch.distributed "nccl" backend = RCCL over xGMI); ever
 bootstraps its own 4096-ciphertext batch with no data-path collective.  value = all ranks' PBS
 divided by the MAX over ranks of the timed region.
 
-The roofline figure is for the dominant kernel (blind rotation + fused sample extract): HIP
-events recorded by libtfhe_hip.so on the launch stream around every launch in the timed region;
-algorithmic bytes per PBS = 61,952,960 (BSK 61,931,520 + LWE in 5,048 + LUT 8,192 + extracted
-LWE 8,200: SURVEY §8d), peak 8.0 TB/s (MI355X HBM3E, MI355X_MICROARCH.md).
+--global-batch G: strong scaling instead (one batch of G PBS, contiguous slices of ~G/N per
+rank; C4 = 65,536 -> 8,192 per GPU at N = 8); value = G x steps / max-over-ranks time.
+
+The roofline figure is for the dominant kernel (blind rotation + fused sample extract), timed by HIP
+events recorded by libtfhe_hip.so on the launch stream around every launch in the timed region.  Its
+bound is VALU issue (see roofline()): achieved = SQ_INSTS_VALU per launch from the counter profile of
+THIS build (profiles/*_roofline.json with a matching tfhe_amd.source_id()) over the live kernel time;
+without one, the FFT64 kernels report algorithmic f64 FLOP/s against the 78.6 TFLOP/s FP64 peak.  The
+SURVEY §8d key-streaming byte model (61,952,960 B per PBS at r = 1) is reported as a labelled model only.
 
 --preset fhevm runs the same protocol on the production fhEVM parameter set (P-FHEVM: n=918, k=1,
 N=2048, PBS 2^23 x 1, KS 2^4 x 4, KS -> PBS; shortint messages m < 16, identity LUT) as a secondary
@@ -60,50 +65,97 @@ def log(msg: str) -> None:
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def pmc_traffic(B: int, kernel: str = "blind_rotate_kernel"):
-    """HBM bytes per blind-rotate launch from the committed rocprofv3 PMC passes
-    (profiles/*_pmc_blind_rotate.json, produced by tools/pmc_summary.py for this same command), or None."""
+# Algorithmic f64 work of the FFT64 blind rotation per PBS, counted from the operation sequence the kernel and
+# oracle/fft_oracle.c share (fma = 2 FLOP; complex multiply 6, complex add 2, radix-8 butterfly 56):
+#   512-point DFT: forward 3 x 64 radix-8 + 2 x 64 x 7 twiddle cmul = 16,128; inverse (8 cmul in pass 2) 16,512;
+#   N = 1024 forward = twist 512 cmul + DFT = 19,200, inverse = DFT + untwist = 19,584;
+#   N = 2048 forward = twist 1024 cmul + 2 DFT + 512 radix-2 combines (10) = 43,520, inverse 44,288;
+#   MAC = (k+1)l x (k+1) x N/2 complex fma (8).
+#   P-GATE  (n=630, (k+1)l = 6): 6 x 19,200 + 2 x 19,584 + 6 x 2 x 512 x 8 = 203,520 FLOP per CMUX
+#   P-FHEVM (n=918, (k+1)l = 2): 2 x 43,520 + 2 x 44,288 + 2 x 2 x 1024 x 8 = 208,384 FLOP per CMUX
+FLOP_PER_PBS = {"gate_fft": 630 * 203_520, "fhevm_fft": 918 * 208_384}
+F64_PEAK_TFLOPS = 78.6    # spec FP64 vector: 256 CUs x 4 SIMDs x 16 f64 lanes x 2 FLOP x 2.4 GHz
+VALU_PEAK_GINST = 1024 * 2.4 / 4  # wave64 f64-rate VALU instructions / ns: 1024 SIMDs, 4 cycles each, 2.4 GHz
+
+
+def profile_for(kernel: str, B: int):
+    """Counter figures for `kernel` from the newest profiles/*_roofline.json whose source_id equals this
+    tree's (tools/profile_round.sh -> tools/roofline_summary.py on the GPU box), measured at batch B.
+    None when no profile of THIS build exists: a different build's counters are never reported."""
     import glob
-    if B != 4096:
-        return None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_blind_rotate.json")), reverse=True):
-        for k, v in json.load(open(f)).items():  # the newest pass that profiled this kernel
+    sid = tfhe_amd.source_id()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_roofline.json")), reverse=True):
+        d = json.load(open(f))
+        if d.get("source_id") != sid or d.get("batch", 4096) != B:
+            continue
+        for k, v in d["kernels"].items():
             if k.split("<")[0].endswith("::" + kernel):
-                return round(v["hbm_bytes_per_launch"])
+                return dict(v, source=os.path.relpath(f, ROOT), source_id=sid)
     return None
 
 
-def valu_profile(B: int, kernel_ms: float, kernel: str = "blind_rotate_kernel"):
-    """VALU roofline of the blind-rotate kernel from the committed SQ counter pass
-    (profiles/*_pmc_sq.csv: rocprofv3 --pmc SQ_INSTS_VALU ... of this bench at B = 4096): wave64 VALU
-    instructions per launch (scaled per PBS to B) x 4 cycles on a 16-lane SIMD, over the SIMD-cycles of
-    the measured launch (1024 SIMDs at 2.4 GHz, MI355X_MICROARCH.md)."""
-    import csv
-    import glob
-    vals, src = [], None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_sq.csv")), reverse=True):
-        vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(f)) if r["Counter_Name"] == "SQ_INSTS_VALU"
-                and r["Kernel_Name"].split("(")[0].split("<")[0].endswith("::" + kernel)]
-        if vals:  # the newest pass that profiled this kernel
-            src = f
-            break
-    if not vals:
-        return None
-    insts = sum(vals) / len(vals) / 4096 * B
-    frac = insts * 4 / (1024 * 2.4e9 * kernel_ms * 1e-3)
-    out = {"bound": "valu", "insts_per_launch": round(insts), "insts_per_pbs": round(insts / B),
-           "issue_frac": round(frac, 3), "model": "4 cycles per wave64 VALU instruction per SIMD, 1024 SIMDs, 2.4 GHz",
-           "source": os.path.relpath(src, ROOT)}
-    # the same instructions priced at the f64 rate measured on this hardware (independent v_fma_f64 /
-    # v_add_f64 chains, 2 waves per SIMD: tools/microbench/f64_rates.hip -> profiles/r01_f64_rates.txt)
-    rates = os.path.join(ROOT, "profiles", "r01_f64_rates.txt")
-    if "fft" in kernel and os.path.exists(rates):
-        cyc = [float(l.split()[3]) for l in open(rates) if l.split() and l.split()[0] in ("v_fma_f64", "v_add_f64")]
-        if cyc:
-            c = sum(cyc) / len(cyc)
-            out["measured_rate_frac"] = round(insts * c / (1024 * 2.4e9 * kernel_ms * 1e-3), 3)
-            out["measured_rate_model"] = f"{c:.2f} nominal cycles per f64 wave64 instruction (microbenchmark)"
+def roofline(preset: str, kernel: str, B: int, kernel_ms: float, br_bytes: int) -> dict:
+    """The dominant kernel's roofline.  The blind rotation is bound by VALU issue, not HBM: each BSK chunk
+    is streamed once per workgroup into LDS and shared by its ciphertexts (and by resident workgroups
+    through L2), so the measured HBM traffic is ~1 GB per 4096-PBS launch, not the 254 GB a key-streaming
+    model (r = 1) would charge.  Primary figure: VALU issue = SQ_INSTS_VALU per launch (same-build counter
+    profile) x 4 cycles over 1024 SIMDs x 2.4 GHz x the live kernel time.  Without a same-build profile
+    the FFT64 kernels fall back to the f64 FLOP figure (algorithmic FLOP / live kernel time vs the
+    78.6 TFLOP/s FP64 vector peak); `traffic` is then null."""
+    prof = profile_for(kernel, B)
+    s = kernel_ms * 1e-3
+    out = {"kernel": kernel + " (+fused sample extract)", "kernel_ms": round(kernel_ms, 3)}
+    flops = FLOP_PER_PBS.get(preset)
+    f64 = None
+    if flops:
+        tf = B * flops / s / 1e12
+        f64 = {"flop_per_pbs": flops, "achieved": round(tf, 2), "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s",
+               "frac": round(tf / F64_PEAK_TFLOPS, 4),
+               "model": "algorithmic f64 FLOP of the transforms + MAC (bench.py FLOP_PER_PBS), fma = 2"}
+    traffic = None
+    if prof and prof.get("hbm_bytes"):
+        traffic = int(prof["hbm_bytes"])
+    if prof and prof.get("SQ_INSTS_VALU"):
+        ginst = prof["SQ_INSTS_VALU"] / s / 1e9
+        out.update({"bound": "valu", "achieved": round(ginst, 1), "peak": VALU_PEAK_GINST,
+                    "unit": "G wave64-VALU-instr/s", "frac": round(ginst / VALU_PEAK_GINST, 4),
+                    "valu_insts_per_launch": int(prof["SQ_INSTS_VALU"])})
+    elif f64:
+        out.update({"bound": "valu", "achieved": f64["achieved"], "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": f64["frac"]})
+    else:
+        out.update({"bound": "valu", "achieved": None, "peak": VALU_PEAK_GINST, "unit": "G wave64-VALU-instr/s",
+                    "frac": None})
+    out["traffic"] = traffic
+    if traffic:
+        gbs = traffic / s / 1e9
+        out["hbm"] = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                      "traffic_per_pbs": round(traffic / B)}
+    out["f64"] = f64
+    out["counters"] = ({"source": prof["source"], "source_id": prof["source_id"],
+                        **{k: prof[k] for k in ("avg_ms", "SQ_WAIT_ANY_per_wave_cycle", "SQ_WAIT_INST_LDS_per_wave_cycle")
+                           if k in prof}} if prof else
+                       {"source": None, "note": f"no profiles/*_roofline.json for source_id {tfhe_amd.source_id()}"})
+    # SURVEY 8(d)'s key-streaming model (r = 1: every PBS charged the whole BSK) -- a model, not a measurement
+    out["hbm_model_r1"] = {"bytes_per_launch": B * br_bytes, "GBps_if_streamed": round(B * br_bytes / s / 1e9, 1),
+                           "note": "model only: the BSK is shared through LDS/L2, see traffic"}
     return out
+
+
+def host_cores() -> tuple:
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU quota when one is set
+    (a GPU box shows the whole machine's CPUs but grants a share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    how = "sched_getaffinity"
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            lim = max(1, int(-(-int(q) // int(per))))
+            if lim < n:
+                n, how = lim, "cgroup cpu.max quota"
+    except (OSError, ValueError):
+        pass
+    return n, how
 
 
 def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int, preset: int = 0,
@@ -149,7 +201,10 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--batch", type=int, default=4096, help="PBS per GPU (weak scaling, the metric's mode)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: this many PBS in total, contiguous slices of ~G/N per rank (SURVEY 8e: "
+                         "C4 = 65,536 -> 8,192 per GPU on 8 GPUs)")
     ap.add_argument("--cpu-sample", type=int, default=0, help="PBS in the CPU baseline sample (0 = auto)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on GPUs; gloo only for rehearsals")
@@ -185,7 +240,12 @@ def main() -> int:
     br_kernel = {"gate": "blind_rotate_kernel", "gate_fft": "blind_rotate_fft_kernel",
                  "fhevm": "blind_rotate2048_kernel", "fhevm_fft": "blind_rotate_fft2k_kernel"}[args.preset]
     br_bytes = BR_BYTES_PER_PBS_FHEVM if fhevm else BR_BYTES_PER_PBS
-    B = args.batch
+    strong = args.global_batch > 0
+    if strong:  # contiguous slice [lo, hi) of one global batch (SURVEY 8e partition)
+        lo, hi = args.global_batch * rank // world, args.global_batch * (rank + 1) // world
+        B = hi - lo
+    else:
+        lo, B = rank * args.batch, args.batch
 
     # ---- key set: generated on rank 0, broadcast once over RCCL ---------------------------------
     t = time.time()
@@ -211,14 +271,19 @@ def main() -> int:
         eng.load_ms_key(tfhe_amd.ms_zeros_keygen(params, KEY_SEED, ck.lwe_key))
 
     # ---- inputs: this rank's batch, encrypted on the host, resident in HBM ----------------------
-    rng = np.random.default_rng(rank_batch_seed(INPUT_SEED, rank))
+    if strong:  # every rank draws the same global message vector and keeps its slice
+        rng = np.random.default_rng(INPUT_SEED)
+        gm = rng.integers(0, FHEVM_MM if fhevm else 2, args.global_batch)[lo:lo + B]
+        rng = None
+    else:
+        rng = np.random.default_rng(rank_batch_seed(INPUT_SEED, rank))
     if fhevm:
-        msgs = rng.integers(0, FHEVM_MM, B).astype(np.uint64)
-        cts = ck.encrypt(msgs, FHEVM_MM, seed=INPUT_SEED + 1, stream0=rank * B)
+        msgs = (gm if strong else rng.integers(0, FHEVM_MM, B)).astype(np.uint64)
+        cts = ck.encrypt(msgs, FHEVM_MM, seed=INPUT_SEED + 1, stream0=lo)
         lut_host = eng.generate_accumulator(lambda m: m, FHEVM_MM)
     else:
-        bits = rng.integers(0, 2, B).astype(bool)
-        cts = ck.encrypt_bool(bits, seed=INPUT_SEED + 1, stream0=rank * B)
+        bits = (gm if strong else rng.integers(0, 2, B)).astype(bool)
+        cts = ck.encrypt_bool(bits, seed=INPUT_SEED + 1, stream0=lo)
         lut_host = eng.gate_lut()
     d_in = torch.from_numpy(cts.view(np.int64)).to(dev)
     d_lut = torch.from_numpy(lut_host.view(np.int64)).to(dev)
@@ -261,9 +326,9 @@ def main() -> int:
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
 
     ms_per_step = elapsed_max * 1e3 / args.steps
-    value = world * B * args.steps / elapsed_max
+    total_pbs = args.global_batch if strong else world * B
+    value = total_pbs * args.steps / elapsed_max
     br_avg = br_ms / max(br_n, 1)
-    achieved = B * br_bytes / (br_avg * 1e-3) / 1e9
 
     pd = params.as_dict()
     bsk_bytes = pd["n"] * (pd["k"] + 1) * pd["pbs_level"] * (pd["k"] + 1) * pd["N"] * 8
@@ -281,7 +346,7 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64" if fft else "u64",
             "data": ("synthetic: ChaCha20-seeded LWE encryptions of uniform bits (key seed 0x7F4E0001), gate LUT"
@@ -296,33 +361,25 @@ def main() -> int:
                              f"PBS 2^23x1, KS 2^4x4, batch {B} per GPU"
                              + (", FFT64 transform (f64 FFT over the 2^64 torus)" if fft else ", NTT transform (Z_p)")),
                 "batch_per_gpu": B,
+                "global_batch": total_pbs,
                 "params": params.as_dict(),
                 "parallelism": f"batch-sharded x{world}, BSK/KSK RCCL broadcast once",
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": br_kernel + " (+fused sample extract)",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(B, br_kernel),
-                "bytes_per_launch": B * br_bytes,
-                "kernel_ms": round(br_avg, 3),
-                "launches": br_n,
-                # the reuse the kernel implements and the true minimum traffic
-                "bsk_reuse": (f"each BSK level-step chunk is streamed once per workgroup into LDS and shared by its "
-                              f"{8 if not (fhevm and fft) else 4} ciphertexts; resident workgroups share it through L2"),
-                "min_traffic_bytes_per_pbs": round((bsk_bytes + ksk_bytes) / B + io_bytes),
-            },
-            "valu_roofline": valu_profile(B, br_avg, br_kernel),
+            "roofline": dict(roofline(args.preset, br_kernel, B, br_avg, br_bytes),
+                             # the reuse the kernel implements and the true minimum traffic
+                             bsk_reuse=(f"each BSK level-step chunk is streamed once per workgroup into LDS and shared "
+                                        f"by its {8 if not (fhevm and fft) else 4} ciphertexts; resident workgroups "
+                                        f"share it through L2"),
+                             min_traffic_bytes_per_pbs=round((bsk_bytes + ksk_bytes) / B + io_bytes),
+                             launches=br_n),
             "keyswitch_ms": round(ks_ms / max(ks_n, 1), 3),
             "ms_noise_reduction_ms": round(msr_ms / msr_n, 3) if msr_n else None,
             "key_broadcast_ms": round(bcast_ms, 3),
             "decrypt_ok": bool(ok.item()),
         }
         if world == 1 and not args.no_cpu:
-            threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+            threads, how = host_cores()
+            log(f"cpu baseline on {threads} host cores ({how})")
             # ~10-20 s of CPU work: the oracle does ~3.5 PBS/s per thread on the NTT at P-GATE, ~23 on
             # FFT64, ~1.3 at P-FHEVM
             # FFT64: the whole 4096 batch at 16 threads (~11 s at P-GATE, ~15 s at P-FHEVM), so every output is

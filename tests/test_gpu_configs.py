@@ -54,3 +54,23 @@ def test_c5_auction_max_tree_256(request, transform):
     assert int(idx.decrypt(ck)[0]) == 77
     assert c.pbs_count > 255 * 100                   # really ran the comparator circuits
     print(f"C5 {transform}: {time.time() - t0:.2f} s, {c.pbs_count} PBS in {c.launches} launches")
+
+
+@pytest.mark.parametrize("transform", ["ntt", "fft64"])
+def test_c2_batch_1024(request, transform, oracle_mod):
+    """C2: batch = 1024 independent P-GATE PBS on one GPU (the exact config size: the FFT64 engine runs
+    its batch kernel here, the NTT engine its latency kernel), every output decrypted, a sample of 16
+    bit-exact against the oracle."""
+    engine = request.getfixturevalue("engine" if transform == "ntt" else "gate_fft_engine")
+    ck, _ = request.getfixturevalue("product_keys" if transform == "ntt" else "gate_fft_keys")
+    B = 1024
+    bits = np.random.default_rng(0xC2).integers(0, 2, B).astype(bool)
+    cts = ck.encrypt_bool(bits, seed=0xC0FFEE02)
+    lut = engine.gate_lut()
+    out = engine.pbs(cts, lut)
+    assert np.array_equal(ck.decrypt_bool(out), bits)
+    preset = tfhe_amd.PRESET_GATE if transform == "ntt" else tfhe_amd.PRESET_GATE_FFT
+    prm = oracle_mod.params(preset)
+    keys = request.getfixturevalue("oracle_keys") if transform == "ntt" else oracle_mod.Keys(prm, 0x7F4E0001)
+    sel = np.linspace(0, B - 1, 16).astype(int)
+    assert np.array_equal(out[sel], oracle_mod.pbs_batch(prm, keys, cts[sel], lut[None]))

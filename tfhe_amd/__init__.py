@@ -165,6 +165,23 @@ def lib():
     return _LIB
 
 
+def source_id() -> str:
+    """Content hash of everything that goes into libtfhe_hip.so (kernel + host sources, build flags,
+    the ABI header).  Profiles under profiles/ carry the source_id of the tree they were measured on;
+    bench.py only uses counter figures whose source_id equals the running tree's (a stale profile of
+    another build is never reported as this build's)."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(_HERE, "csrc")
+    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc))
+    files += [os.path.join(_HERE, "Makefile"), os.path.join(os.path.dirname(_HERE), "include", "tfhe_hip.h")]
+    for f in files:
+        h.update(os.path.relpath(f, os.path.dirname(_HERE)).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 NULL_STREAM = ctypes.c_void_p(-1).value  # TFHE_HIP_NULL_STREAM: the device's legacy null stream
 
 
