@@ -71,29 +71,46 @@ uint32_t tfhe_hip_io_dim(const tfhe_params* p);
 
 /* ---- client-side key material (host) ------------------------------------------------------
  * Replaces TfheClientKey.generate / ServerKey generation (sdk/relayer/src/tfhe.ts:20-28,
- * generateKeys.js:20-31) for the deterministic seeded keys this engine consumes.
- * Streams: LWE key 1, GLWE key 2, BSK_i 0x1000+i, KSK_j 0x100000+j (ChaCha20). */
+ * generateKeys.js:20-31).  All randomness is ChaCha20 keyed by a 192-bit rng key plus a stream index
+ * (LWE key 1, GLWE key 2, BSK_i 0x1000+i, KSK_j 0x100000+j, MS zero z 0x200000+z, ciphertext q stream0+q).
+ *   - tfhe_hip_rng_key_entropy: 192 bits from the OS (getrandom) -- production keys and encryptions;
+ *   - tfhe_hip_rng_key_from_seed: (seed, a public tag) -- REPRODUCIBLE streams for tests, golden vectors
+ *     and the oracle.  A seeded key set is public knowledge: never use one for real data.
+ * The uint64_t-seed entry points below are the seeded (test) forms of the *_k functions. */
+typedef struct tfhe_rng_key {
+  uint32_t w[6];
+} tfhe_rng_key;
+int tfhe_hip_rng_key_entropy(tfhe_rng_key* out);
+int tfhe_hip_rng_key_from_seed(uint64_t seed, tfhe_rng_key* out);
+int tfhe_hip_keygen_k(const tfhe_params* p, const tfhe_rng_key* rk, uint64_t* lwe_key, uint64_t* glwe_key,
+                      uint64_t* bsk /* nullable */, uint64_t* ksk /* nullable */);
 int tfhe_hip_keygen(const tfhe_params* p, uint64_t seed, uint64_t* lwe_key, uint64_t* glwe_key,
                     uint64_t* bsk /* nullable */, uint64_t* ksk /* nullable */);
 /* BSK / KSK (standard domain) for GIVEN binary secret keys — the server-key half of keygen, for key
  * material ingested from tfhe-rs (the packages/kms loader role, SURVEY §8f f3: the ClientKey of
- * sdk/relayer/src/test/keys/privateKey.bin; tfhe_amd/keyio.py parses it).  Same ChaCha streams as
- * tfhe_hip_keygen.  EINVAL if a key word is not 0/1. */
+ * sdk/relayer/src/test/keys/privateKey.bin; tfhe_amd/keyio.py parses it).  EINVAL if a key word is not 0/1. */
+int tfhe_hip_server_keygen_k(const tfhe_params* p, const tfhe_rng_key* rk, const uint64_t* lwe_key,
+                             const uint64_t* glwe_key, uint64_t* bsk /* nullable */, uint64_t* ksk /* nullable */);
 int tfhe_hip_server_keygen(const tfhe_params* p, uint64_t seed, const uint64_t* lwe_key, const uint64_t* glwe_key,
                            uint64_t* bsk /* nullable */, uint64_t* ksk /* nullable */);
 /* Modulus-switch noise reduction key of the P-FHEVM server key (the
  * reference's parameter block carries modulus_switch_zeros_count 1449, ms_bound 2^58,
  * ms_r_sigma_factor 13.179852282053789, ms_input_variance 2.63039184094559e-07 —
  * sdk/relayer/src/test/keys/privateKey.bin @0x5e04..0x5e30).  count LWE encryptions of 0 under
- * the small key, count x (n+1) u64; zero z on ChaCha stream 0x200000 + z. */
+ * the small key, count x (n+1) u64. */
 #define TFHE_HIP_MS_FHEVM_ZEROS 1449u
 #define TFHE_HIP_MS_FHEVM_BOUND 0x1p58
 #define TFHE_HIP_MS_FHEVM_R_SIGMA 13.179852282053789
 #define TFHE_HIP_MS_FHEVM_INPUT_VARIANCE 2.63039184094559e-07
+int tfhe_hip_ms_zeros_keygen_k(const tfhe_params* p, const tfhe_rng_key* rk, const uint64_t* lwe_key, uint32_t count,
+                               uint64_t* zeros);
 int tfhe_hip_ms_zeros_keygen(const tfhe_params* p, uint64_t seed, const uint64_t* lwe_key, uint32_t count,
                              uint64_t* zeros);
-/* Encrypt count torus messages; ciphertext q uses ChaCha stream (stream0 + q).
+/* Encrypt count torus messages; ciphertext q uses ChaCha stream (stream0 + q) of the rng key (a fresh
+ * entropy key per call, or one key with non-overlapping stream ranges).
  * Replaces the encrypt path of packages/luxfhejs/src/index.ts:127-141 (server-side /encrypt). */
+int tfhe_hip_lwe_encrypt_k(uint32_t dim, const uint64_t* key, int32_t noise_log2, const tfhe_rng_key* rk,
+                           uint64_t stream0, const uint64_t* msgs, size_t count, uint64_t* out);
 int tfhe_hip_lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, uint64_t seed,
                          uint64_t stream0, const uint64_t* msgs, size_t count, uint64_t* out);
 /* phase = b - <a, s> (decryption before decoding); replaces /decrypt
@@ -104,16 +121,32 @@ int tfhe_hip_lut_constant(uint32_t N, uint64_t torus_value, uint64_t* lut);
 int tfhe_hip_lut_from_table(uint32_t N, uint32_t msg_modulus, const uint64_t* table, uint64_t delta_out,
                             uint64_t* lut);
 
-/* ---- device engine ------------------------------------------------------------------------ */
-int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out);
+/* ---- device engine ------------------------------------------------------------------------
+ * One engine spans ndev device "shards" (SURVEY §8b/§8e).  Each shard owns a HIP stream, a copy of the
+ * keys and its workspaces.  Host-buffer calls (tfhe_hip_pbs, tfhe_hip_nand) split a batch into
+ * contiguous slices, one per shard, run concurrently (one host thread per shard) and return when all
+ * are done; the outputs are in input order.  Keys are uploaded once to shard 0 (pinned staging) and
+ * broadcast to the others: RCCL (ncclCommInitAll + ncclBroadcast over xGMI, librccl loaded on first use)
+ * when the ordinals are distinct, device copies when an ordinal repeats (a one-GPU box can run
+ * devices = {0, 0} to exercise the split).  TFHE_HIP_BCAST=rccl|copy overrides the choice.
+ * Stage-level entry points (blind_rotate, sample_extract, keyswitch, ms_reduce, ntt_*, fft_*) run on
+ * shard 0.  Replaces the CPU worker pool of the reference's FHE service
+ * (coprocessor-docker-compose.yml:97 --coprocessor-fhe-threads=8). */
+int tfhe_hip_create(const tfhe_params* p, const int* devices, int ndev, tfhe_ctx** out);
 void tfhe_hip_destroy(tfhe_ctx* ctx);
 const char* tfhe_hip_last_error(void);
-int tfhe_hip_device(const tfhe_ctx* ctx);
+int tfhe_hip_device(const tfhe_ctx* ctx);          /* device of shard 0 */
+int tfhe_hip_ndev(const tfhe_ctx* ctx);            /* number of shards */
+int tfhe_hip_device_at(const tfhe_ctx* ctx, int i); /* device of shard i, -1 if out of range */
+/* How the last key load reached shards 1..ndev-1: 0 = single shard, 1 = device copies, 2 = RCCL. */
+int tfhe_hip_key_bcast_mode(const tfhe_ctx* ctx);
 
-/* Upload standard-domain BSK and KSK (host memory) and convert the BSK to the device NTT layout.
- * Replaces the packages/kms key-loader role (pinned-HBM key residency). */
+/* Upload standard-domain BSK and KSK from host memory through a pinned staging ring to shard 0,
+ * broadcast them to every other shard, and convert them on each device (BSK to the transform domain,
+ * KSK to the matrix-core byte planes).  Replaces the packages/kms key-loader role (pinned-HBM key
+ * residency). */
 int tfhe_hip_load_keys(tfhe_ctx* ctx, const uint64_t* bsk, size_t bsk_len, const uint64_t* ksk, size_t ksk_len);
-/* Same, from DEVICE buffers on this ctx's device (e.g. after an RCCL broadcast of the keys). */
+/* Same, from DEVICE buffers on shard 0's device (e.g. after a torch.distributed broadcast of the keys). */
 int tfhe_hip_load_keys_device(tfhe_ctx* ctx, const uint64_t* d_bsk, size_t bsk_len, const uint64_t* d_ksk,
                               size_t ksk_len);
 
@@ -134,8 +167,10 @@ int tfhe_hip_ms_reduce(tfhe_ctx* ctx, const uint64_t* lwe_small, size_t B, uint6
  * the compute behind POST /evaluate (e2e/test/fhe.test.ts:141-157).  Host buffers, synchronous. */
 int tfhe_hip_pbs(tfhe_ctx* ctx, const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
                  const uint32_t* lut_index, uint64_t* lwe_out);
-/* Device buffers, enqueued on `stream` (hipStream_t; NULL = the ctx stream, TFHE_HIP_NULL_STREAM = the
- * device's legacy null stream, e.g. torch's default stream).  Inputs resident in HBM. */
+/* Device buffers, enqueued on `stream` (hipStream_t; NULL = the shard's stream, TFHE_HIP_NULL_STREAM = the
+ * device's legacy null stream, e.g. torch's default stream).  Inputs resident in HBM, on the device of the
+ * shard that runs the batch: the first shard whose device holds d_lwe_in.  Calls on different streams
+ * are ordered on the shard's workspaces by an event (a later call waits for the previous one's kernels). */
 #define TFHE_HIP_NULL_STREAM ((void*)(intptr_t)-1)
 int tfhe_hip_pbs_async(tfhe_ctx* ctx, const uint64_t* d_lwe_in, size_t B, const uint64_t* d_luts, size_t n_lut,
                        const uint32_t* d_lut_index, uint64_t* d_lwe_out, void* stream);

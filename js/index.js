@@ -32,33 +32,36 @@ function paramsPreset(which = PRESET_GATE) {
 }
 
 class ClientKey {
+  /** seed: the test seed the keys came from, or null for keys drawn from OS entropy */
   constructor(params, seed, lweKey, glweKey) {
     this.params = params;
-    this.seed = BigInt(seed);
+    this.seed = seed === undefined || seed === null ? null : BigInt(seed);
     this.lweKey = lweKey;
     this.glweKey = glweKey;
   }
-  static generate(params = paramsPreset(), seed = 0x7F4E0001n) {
-    const k = native.keygen(params, BigInt(seed), false);
+  /** seed undefined (default): 192-bit OS entropy; a seed: the reproducible TEST key (public knowledge) */
+  static generate(params = paramsPreset(), seed = undefined) {
+    const k = native.keygen(params, rngArg(seed), false);
     return new ClientKey(k.params, seed, k.lweKey, k.glweKey);
   }
   get ioKey() { return this.params.order === 0 ? this.lweKey : this.glweKey; }
   get ioNoise() { return this.params.order === 0 ? this.params.lwe_noise_log2 : this.params.glwe_noise_log2; }
   get ctLen() { return this.ioKey.length + 1; }
 
-  encryptTorus(msgs, seed = 1n, stream0 = 0n) {
+  /** seed undefined (default): masks and noise from a fresh OS-entropy ChaCha key for this call */
+  encryptTorus(msgs, seed = undefined, stream0 = 0n) {
     const m = msgs instanceof BigUint64Array ? msgs : BigUint64Array.from(msgs, (v) => mod64(BigInt(v)));
-    return native.encrypt(this.ioKey, this.ioNoise, BigInt(seed), BigInt(stream0), m);
+    return native.encrypt(this.ioKey, this.ioNoise, rngArg(seed), BigInt(stream0), m);
   }
   phase(cts) { return native.phase(this.ioKey, cts); }
 
-  encryptBool(bits, seed = 1n, stream0 = 0n) {
+  encryptBool(bits, seed = undefined, stream0 = 0n) {
     return this.encryptTorus(Array.from(bits, (b) => (b ? MU : TORUS - MU)), seed, stream0);
   }
   decryptBool(cts) { return Array.from(this.phase(cts), (p) => p < (1n << 63n)); }
 
   /** shortint encoding with one padding bit (encryption.rs:5-22) */
-  encrypt(values, msgModulus, seed = 1n, stream0 = 0n) {
+  encrypt(values, msgModulus, seed = undefined, stream0 = 0n) {
     const delta = (1n << 63n) / BigInt(msgModulus);
     return this.encryptTorus(Array.from(values, (v) => (BigInt(v) % BigInt(msgModulus)) * delta), seed, stream0);
   }
@@ -73,17 +76,24 @@ class ServerKey {
   constructor(params, bsk, ksk, msZeros = null) { this.params = params; this.bsk = bsk; this.ksk = ksk; this.msZeros = msZeros; }
 }
 
-/** tfhe-rs gen_keys analogue: deterministic ChaCha20-seeded key set -> [ClientKey, ServerKey] */
-function genKeys(params = paramsPreset(), seed = 0x7F4E0001n) {
-  const k = native.keygen(params, BigInt(seed), true);
+/** undefined -> OS entropy (native side); a seed -> the reproducible test stream */
+const rngArg = (seed) => (seed === undefined || seed === null ? undefined : BigInt(seed));
+
+/** tfhe-rs gen_keys analogue -> [ClientKey, ServerKey].  seed undefined (default): every key from 192 bits
+ *  of OS entropy; a seed gives the reproducible TEST key set (anyone knowing it can decrypt). */
+function genKeys(params = paramsPreset(), seed = undefined) {
+  const k = native.keygen(params, rngArg(seed), true);
   return [new ClientKey(k.params, seed, k.lweKey, k.glweKey), new ServerKey(k.params, k.bsk, k.ksk, k.msZeros || null)];
 }
 
+/** devices: one GPU ordinal or an array (one shard each; batches split across them, keys broadcast once
+ *  over RCCL -- include/tfhe_hip.h tfhe_hip_create) */
 class Engine {
-  constructor(params = paramsPreset(), device = 0) {
+  constructor(params = paramsPreset(), devices = 0) {
     this.params = params;
-    this.handle = native.createEngine(params, device);
+    this.handle = native.createEngine(params, devices);
   }
+  info() { return native.engineInfo(this.handle); }
   loadKeys(serverKey) { native.loadKeys(this.handle, serverKey.bsk, serverKey.ksk, serverKey.msZeros || null); return this; }
   destroy() { if (this.handle) { native.destroyEngine(this.handle); this.handle = null; } }
   gateLut() { return native.lutConstant(this.params.N, MU); }
@@ -101,6 +111,10 @@ class Engine {
   /** batched PBS (blind rotate + sample extract + keyswitch) on the GPU; resolves to ciphertexts */
   pbs(cts, luts, lutIndex = null) { return native.pbs(this.handle, cts, luts, lutIndex); }
   keyswitchProgrammableBootstrap(ct, acc) { return this.pbs(ct, acc); }
+  /** LWE keyswitch B x (kN+1) -> B x (n+1) (the KS stage alone); resolves to ciphertexts */
+  keyswitch(bigLwes) { return native.keyswitch(this.handle, bigLwes); }
+  /** blind rotation of small-key LWEs B x (n+1) -> B x (k+1) x N accumulators (stage-level) */
+  blindRotate(cts, luts, lutIndex = null) { return native.blindRotate(this.handle, cts, luts, lutIndex); }
   nand(c1, c2) { return native.nand(this.handle, c1, c2); }
 }
 
@@ -118,7 +132,7 @@ function gateLin(c1, c2, k1, k2, c, ctLen) {
 
 class FheBool {
   constructor(engine, ct) { this.engine = engine; this.ct = ct; this.ctLen = engine.params.n + 1; }
-  static encrypt(values, clientKey, engine, seed = 1n, stream0 = 0n) {
+  static encrypt(values, clientKey, engine, seed = undefined, stream0 = 0n) {
     const arr = Array.isArray(values) ? values : [values];
     return new FheBool(engine, clientKey.encryptBool(arr, seed, stream0));
   }
@@ -175,7 +189,7 @@ function makeUint(bits) {
       this.count = count === null ? ct.length / (bits * (engine.params.n + 1)) : count;
     }
     static get bitWidth() { return bits; }
-    static encrypt(values, clientKey, engine, seed = 1n, stream0 = 0n) {
+    static encrypt(values, clientKey, engine, seed = undefined, stream0 = 0n) {
       const vs = Array.isArray(values) ? values : [values];
       const flat = [];
       for (const v of vs) for (let j = 0; j < bits; j++) flat.push(((BigInt(v) >> BigInt(j)) & 1n) === 1n);
@@ -229,19 +243,26 @@ const FheUint64 = UINT_CLASSES[64];
  * encrypt_* return serialized ciphertext bytes (Uint8Array) like the HTTP client; evaluate() takes
  * the POST /evaluate shape (e2e/test/fhe.test.ts:105-175) and runs every fhEVM operator on the GPU.
  * Requests submitted concurrently are evaluated in lockstep (one PBS launch per circuit level).
- * config.params: a params object, or 'gate' (default: boolean gates, js/integer.js) or 'fhevm'
- * (P-FHEVM radix blocks, js/radix.js — fhEVM's own representation); 'gate_fft' / 'fhevm_fft' select
- * the same parameter sets on the FFT64 transform.
+ * config.params: a params object, or 'gate_fft' (default: boolean gates on the FFT64 transform -- the
+ * engine the bench measures -- js/integer.js), 'fhevm_fft' (P-FHEVM radix blocks, js/radix.js, fhEVM's
+ * own representation), or 'gate' / 'fhevm' for the same parameter sets on the Goldilocks NTT transform.
+ * config.devices: a GPU ordinal or an array of ordinals (batches split across them, keys broadcast once).
+ * Keys and every encryption draw fresh OS entropy.  config.seed (a reproducible, PUBLIC key set: anyone
+ * who knows it decrypts everything) is refused unless config.dev is true.
  */
 class LuxFHELocalClient {
   constructor(config = {}) {
     const pr = config.params;
     const named = { gate: PRESET_GATE, fhevm: PRESET_FHEVM, gate_fft: PRESET_GATE_FFT, fhevm_fft: PRESET_FHEVM_FFT };
-    this.params = !pr ? paramsPreset(PRESET_GATE) : typeof pr === 'string' ? paramsPreset(named[pr]) : pr;
+    if (typeof pr === 'string' && !(pr in named)) throw new Error(`unknown params preset '${pr}'`);
+    this.params = !pr ? paramsPreset(PRESET_GATE_FFT) : typeof pr === 'string' ? paramsPreset(named[pr]) : pr;
     this.radix = this.params.order === 1;
     this.dim = this.radix ? this.params.k * this.params.N : this.params.n;
-    this.seed = BigInt(config.seed || 0x7F4E0001n);
-    this.device = config.device || 0;
+    if (config.seed !== undefined && config.seed !== null && !config.dev)
+      throw new Error('LuxFHELocalClient: a fixed seed makes every key and ciphertext reproducible by anyone who '
+                      + 'knows it; pass {dev: true} to use one (tests / demos only)');
+    this.seed = config.seed === undefined || config.seed === null ? null : BigInt(config.seed);
+    this.devices = config.devices !== undefined ? config.devices : (config.device || 0);
     this.engine = config.engine || null;
     this.clientKey = null;
     this.serverKey = null;
@@ -251,8 +272,8 @@ class LuxFHELocalClient {
     this.launches = 0;
   }
   async initialize() {
-    [this.clientKey, this.serverKey] = genKeys(this.params, this.seed);
-    if (!this.engine) this.engine = new Engine(this.params, this.device).loadKeys(this.serverKey);
+    [this.clientKey, this.serverKey] = genKeys(this.params, this.seed === null ? undefined : this.seed);
+    if (!this.engine) this.engine = new Engine(this.params, this.devices).loadKeys(this.serverKey);
   }
   /** key descriptor: params + SHA-256 of the evaluation keys (this scheme has no public encryption key) */
   async getPublicKey() {
@@ -266,6 +287,9 @@ class LuxFHELocalClient {
     out.set(h.digest(), head.byteLength);
     return out;
   }
+  /** dev seed: the reproducible stream seed+1 (stream counter advances); otherwise undefined = fresh
+   *  OS entropy for every encryption, so no two ciphertexts share masks or noise, across restarts too */
+  _encSeed() { return this.seed === null ? undefined : this.seed + 1n; }
   encryptValue(value, bitWidth) {
     const w = Number(bitWidth);
     if (!(w >= 1 && w <= 256)) throw new Error(`Encryption failed: bitWidth ${bitWidth} not supported`);
@@ -274,13 +298,13 @@ class LuxFHELocalClient {
       if (w > 1 && w % 2) throw new Error(`Encryption failed: radix bitWidth ${w} must be even`);
       const nb = w === 1 ? 1 : w / 2;
       const digits = Array.from({ length: nb }, (_, j) => (v >> BigInt(2 * j)) & 3n);
-      const ct = this.clientKey.encrypt(digits, radix.SPACE, this.seed + 1n, this.stream);
+      const ct = this.clientKey.encrypt(digits, radix.SPACE, this._encSeed(), this.stream);
       this.stream += BigInt(nb);
       return serializeCiphertext(w === 1 ? KIND.RADIX_BOOL : KIND.RADIX_UINT, w, this.dim, 1, ct);
     }
     const flat = [];
     for (let j = 0; j < w; j++) flat.push(((v >> BigInt(j)) & 1n) === 1n);
-    const ct = this.clientKey.encryptBool(flat, this.seed + 1n, this.stream);
+    const ct = this.clientKey.encryptBool(flat, this._encSeed(), this.stream);
     this.stream += BigInt(w);
     return serializeCiphertext(w === 1 ? 0 : 1, w, this.params.n, 1, ct);
   }

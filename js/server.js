@@ -15,10 +15,15 @@
  * for all of them).  Single-party: this process holds the client key (like the reference's local
  * dev server); /verify checks ciphertext framing only — there is no ZK proof system on this path.
  *
- * --params fhevm serves fhEVM's own representation instead (P-FHEVM radix blocks, js/radix.js:
- * KS -> PBS at N = 2048, every fhEVM operator).
+ * --params fhevm_fft serves fhEVM's own representation instead (P-FHEVM radix blocks, js/radix.js:
+ * KS -> PBS at N = 2048, every fhEVM operator); the default is gate_fft (boolean gates on the FFT64
+ * engine, the one bench.py measures); gate / fhevm run the Goldilocks NTT engine.
+ * --devices 0,1,...,7 spreads every batch over those GPUs (one engine shard each, keys broadcast once
+ * over RCCL).  Keys and encryptions draw OS entropy; --seed (a public, reproducible key set) is only
+ * accepted together with --dev.
  *
- *   node js/server.js [--port 8448] [--host 127.0.0.1] [--device 0] [--seed 0x7F4E0001] [--params gate|fhevm|gate_fft|fhevm_fft]
+ *   node js/server.js [--port 8448] [--host 127.0.0.1] [--devices 0[,1,...]] [--params gate_fft|fhevm_fft|gate|fhevm]
+ *                     [--dev --seed 0x7F4E0001]
  */
 const http = require('http');
 
@@ -119,12 +124,22 @@ if (require.main === module) {
   const args = process.argv.slice(2);
   const opt = (name, dflt) => { const i = args.indexOf(`--${name}`); return i >= 0 ? args[i + 1] : dflt; };
   const { LuxFHELocalClient } = require('./index.js');
-  const params = opt('params', 'gate');
-  const client = new LuxFHELocalClient({ device: Number(opt('device', 0)), seed: BigInt(opt('seed', '0x7F4E0001')), params });
+  const params = opt('params', 'gate_fft');
+  const devices = String(opt('devices', opt('device', '0'))).split(',').map(Number);
+  const dev = args.includes('--dev');
+  const seed = opt('seed', undefined);
+  if (seed !== undefined && !dev) {
+    console.error('--seed makes every key and ciphertext reproducible by anyone who knows it: add --dev to accept that');
+    process.exit(2);
+  }
+  let client;
+  try {
+    client = new LuxFHELocalClient({ devices, seed: seed === undefined ? undefined : BigInt(seed), dev, params });
+  } catch (e) { console.error(e.message); process.exit(2); }
   client.initialize().then(() => {
     const port = Number(opt('port', 8448)), host = opt('host', '127.0.0.1');
-    createServer(client, { device: Number(opt('device', 0)), params }).listen(port, host, () => {
-      console.log(`tfhe_amd FHE server (${params}) on http://${host}:${port}`);
+    createServer(client, { device: devices[0], devices, params }).listen(port, host, () => {
+      console.log(`tfhe_amd FHE server (${params}, devices ${devices.join(',')}) on http://${host}:${port}`);
     });
   }).catch((e) => { console.error(e); process.exit(1); });
 }

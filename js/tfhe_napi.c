@@ -6,8 +6,9 @@
  * compute behind packages/luxfhejs' server calls (packages/luxfhejs/src/index.ts:127-141).
  *
  * Buffers cross as BigUint64Array / Uint32Array (zero-copy views of their backing stores).
- * Device work (pbs, nand) runs in napi_create_async_work and resolves a Promise, so the event
- * loop never blocks; argument buffers are referenced until the work completes.  A failing
+ * Device work (pbs, nand, keyswitch, blindRotate) runs in napi_create_async_work and resolves a
+ * Promise, so the event loop never blocks; argument buffers and the engine handle are referenced until
+ * the work completes (destroyEngine during a job defers the ctx teardown to the last completion).  A failing
  * C-ABI call becomes a JS Error whose `code` is the TFHE_HIP_E* status.
  */
 #include <node_api.h>
@@ -77,6 +78,25 @@ static int get_u64(napi_env env, napi_value v, uint64_t* out) {
   return 0;
 }
 
+/* rng argument: undefined / null -> 192 bits of OS entropy (production); BigInt / number -> the seeded
+ * REPRODUCIBLE stream (tests, golden vectors; public knowledge); Uint8Array of 24 bytes -> raw key. */
+static int get_rng(napi_env env, napi_value v, tfhe_rng_key* rk) {
+  napi_valuetype t = napi_undefined;
+  if (v && napi_typeof(env, v, &t) != napi_ok) return 0;
+  if (t == napi_undefined || t == napi_null) return tfhe_hip_rng_key_entropy(rk) == 0;
+  if (t == napi_bigint || t == napi_number) {
+    uint64_t seed;
+    return get_u64(env, v, &seed) && tfhe_hip_rng_key_from_seed(seed, rk) == 0;
+  }
+  uint8_t* d;
+  size_t n;
+  if (get_typed(env, v, napi_uint8_array, (void**)&d, &n) && n == sizeof(rk->w)) {
+    memcpy(rk->w, d, sizeof(rk->w));
+    return 1;
+  }
+  return 0;
+}
+
 static int get_params(napi_env env, napi_value v, tfhe_params* p) {
   napi_valuetype t;
   napi_typeof(env, v, &t);
@@ -136,15 +156,15 @@ static napi_value js_params_preset(napi_env env, napi_callback_info info) {
   return params_to_js(env, &p);
 }
 
-/* keygen(params, seed[, withServerKey=true]) -> {lweKey, glweKey, bsk, ksk} */
+/* keygen(params, rng[, withServerKey=true]) -> {lweKey, glweKey, bsk, ksk[, msZeros]}; rng as get_rng */
 static napi_value js_keygen(napi_env env, napi_callback_info info) {
   size_t argc = 3;
   napi_value argv[3];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   tfhe_params p = {0};
-  uint64_t seed = 0;
-  if (argc < 2 || !get_params(env, argv[0], &p) || !get_u64(env, argv[1], &seed)) {
-    napi_throw_type_error(env, "EINVAL", "keygen(params, seed[, withServerKey])");
+  tfhe_rng_key rk;
+  if (argc < 1 || !get_params(env, argv[0], &p) || !get_rng(env, argc > 1 ? argv[1] : NULL, &rk)) {
+    napi_throw_type_error(env, "EINVAL", "keygen(params[, seed | 24-byte key | undefined = OS entropy[, withServerKey]])");
     return NULL;
   }
   bool with_sk = true;
@@ -159,12 +179,12 @@ static napi_value js_keygen(napi_env env, napi_callback_info info) {
     a_ksk = new_u64_array(env, tfhe_hip_ksk_len(&p), &ksk);
     if (!a_bsk || !a_ksk) return throw_tfhe(env, TFHE_HIP_ENOMEM);
   }
-  int rc = tfhe_hip_keygen(&p, seed, lwe, glwe, bsk, ksk);
+  int rc = tfhe_hip_keygen_k(&p, &rk, lwe, glwe, bsk, ksk);
   if (rc) return throw_tfhe(env, rc);
   if (with_sk && p.order == 1) { /* KS -> PBS server keys carry the modulus-switch zeros */
     a_zeros = new_u64_array(env, (size_t)TFHE_HIP_MS_FHEVM_ZEROS * (p.n + 1), &zeros);
     if (!a_zeros) return throw_tfhe(env, TFHE_HIP_ENOMEM);
-    rc = tfhe_hip_ms_zeros_keygen(&p, seed, lwe, TFHE_HIP_MS_FHEVM_ZEROS, zeros);
+    rc = tfhe_hip_ms_zeros_keygen_k(&p, &rk, lwe, TFHE_HIP_MS_FHEVM_ZEROS, zeros);
     if (rc) return throw_tfhe(env, rc);
   }
   napi_create_object(env, &o);
@@ -179,23 +199,25 @@ static napi_value js_keygen(napi_env env, napi_callback_info info) {
   return o;
 }
 
-/* encrypt(key: BigUint64Array, noiseLog2, seed, stream0, msgs: BigUint64Array) -> BigUint64Array */
+/* encrypt(key: BigUint64Array, noiseLog2, rng, stream0, msgs: BigUint64Array) -> BigUint64Array;
+ * rng as get_rng (undefined = fresh OS entropy for this call) */
 static napi_value js_encrypt(napi_env env, napi_callback_info info) {
   size_t argc = 5;
   napi_value argv[5];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  uint64_t *key, *msgs, seed, stream0, *out;
+  uint64_t *key, *msgs, stream0, *out;
+  tfhe_rng_key rk;
   size_t dim, count;
   int32_t noise;
   if (argc < 5 || !get_typed(env, argv[0], napi_biguint64_array, (void**)&key, &dim) ||
-      napi_get_value_int32(env, argv[1], &noise) != napi_ok || !get_u64(env, argv[2], &seed) ||
+      napi_get_value_int32(env, argv[1], &noise) != napi_ok || !get_rng(env, argv[2], &rk) ||
       !get_u64(env, argv[3], &stream0) || !get_typed(env, argv[4], napi_biguint64_array, (void**)&msgs, &count)) {
-    napi_throw_type_error(env, "EINVAL", "encrypt(key, noiseLog2, seed, stream0, msgs)");
+    napi_throw_type_error(env, "EINVAL", "encrypt(key, noiseLog2, rng, stream0, msgs)");
     return NULL;
   }
   napi_value res = new_u64_array(env, count * (dim + 1), &out);
   if (!res) return throw_tfhe(env, TFHE_HIP_ENOMEM);
-  int rc = tfhe_hip_lwe_encrypt((uint32_t)dim, key, noise, seed, stream0, msgs, count, out);
+  int rc = tfhe_hip_lwe_encrypt_k((uint32_t)dim, key, noise, &rk, stream0, msgs, count, out);
   if (rc) return throw_tfhe(env, rc);
   return res;
 }
@@ -260,15 +282,20 @@ static void finalize_ctx(napi_env env, void* data, void* hint) {
   if (data) tfhe_hip_destroy((tfhe_ctx*)data);
 }
 
+/* An engine handle.  Every queued job holds a reference to the handle's JS external (so GC cannot
+ * finalize it while the job runs) and counts in `pending`; destroyEngine with jobs in flight only marks
+ * the box, and the last job's completion (main thread, like destroyEngine) destroys the ctx. */
 typedef struct {
   tfhe_ctx* ctx;
   tfhe_params p;
+  int pending;
+  int destroy_requested;
 } ctx_box;
 
 static void finalize_box(napi_env env, void* data, void* hint) {
   ctx_box* b = (ctx_box*)data;
   if (b) {
-    finalize_ctx(env, b->ctx, hint);
+    finalize_ctx(env, b->ctx, hint);  /* unreachable with jobs pending: they reference the external */
     free(b);
   }
 }
@@ -279,20 +306,50 @@ static ctx_box* get_box(napi_env env, napi_value v) {
   return (ctx_box*)d;
 }
 
-/* createEngine(params, device) -> external handle (destroyed by GC or destroyEngine) */
+/* createEngine(params[, devices = 0]) -> external handle (destroyed by GC or destroyEngine).
+ * devices: one ordinal or an array of ordinals (one shard each: include/tfhe_hip.h). */
 static napi_value js_create(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   tfhe_params p = {0};
-  int32_t dev = 0;
+  int devs[64] = {0};
+  int ndev = 1;
   if (argc < 1 || !get_params(env, argv[0], &p)) {
-    napi_throw_type_error(env, "EINVAL", "createEngine(params[, device])");
+    napi_throw_type_error(env, "EINVAL", "createEngine(params[, devices])");
     return NULL;
   }
-  if (argc > 1) napi_get_value_int32(env, argv[1], &dev);
+  if (argc > 1) {
+    bool is_arr = false;
+    napi_is_array(env, argv[1], &is_arr);
+    if (is_arr) {
+      uint32_t len = 0;
+      napi_get_array_length(env, argv[1], &len);
+      if (len < 1 || len > 64) {
+        napi_throw_range_error(env, "EINVAL", "createEngine: 1..64 devices");
+        return NULL;
+      }
+      for (uint32_t i = 0; i < len; i++) {
+        napi_value e;
+        napi_get_element(env, argv[1], i, &e);
+        if (napi_get_value_int32(env, e, &devs[i]) != napi_ok) {
+          napi_throw_type_error(env, "EINVAL", "createEngine: device ordinals must be numbers");
+          return NULL;
+        }
+      }
+      ndev = (int)len;
+    } else {
+      napi_valuetype t;
+      napi_typeof(env, argv[1], &t);
+      if (t == napi_number) napi_get_value_int32(env, argv[1], &devs[0]);
+      else if (t != napi_undefined && t != napi_null) {
+        napi_throw_type_error(env, "EINVAL", "createEngine: devices must be a number or an array of numbers");
+        return NULL;
+      }
+    }
+  }
   tfhe_ctx* c = NULL;
-  int rc = tfhe_hip_create(&p, dev, &c);
+  int rc = tfhe_hip_create(&p, devs, ndev, &c);
   if (rc) return throw_tfhe(env, rc);
   ctx_box* b = (ctx_box*)calloc(1, sizeof(ctx_box));
   b->ctx = c;
@@ -308,10 +365,41 @@ static napi_value js_destroy(napi_env env, napi_callback_info info) {
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   ctx_box* b = argc ? get_box(env, argv[0]) : NULL;
   if (b && b->ctx) {
-    tfhe_hip_destroy(b->ctx);
-    b->ctx = NULL;
+    if (b->pending) {
+      b->destroy_requested = 1;  /* the last pending job's completion destroys the ctx */
+    } else {
+      tfhe_hip_destroy(b->ctx);
+      b->ctx = NULL;
+    }
   }
   return NULL;
+}
+
+/* engineInfo(engine) -> {devices: [..], keyBroadcast: 'single' | 'copy' | 'rccl', pending} */
+static napi_value js_engine_info(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  ctx_box* b = argc ? get_box(env, argv[0]) : NULL;
+  if (!b || !b->ctx || b->destroy_requested) {
+    napi_throw_type_error(env, "EINVAL", "engineInfo(engine): engine destroyed");
+    return NULL;
+  }
+  napi_value o, arr, x;
+  napi_create_object(env, &o);
+  const int nd = tfhe_hip_ndev(b->ctx);
+  napi_create_array_with_length(env, (size_t)nd, &arr);
+  for (int i = 0; i < nd; i++) {
+    napi_create_int32(env, tfhe_hip_device_at(b->ctx, i), &x);
+    napi_set_element(env, arr, (uint32_t)i, x);
+  }
+  napi_set_named_property(env, o, "devices", arr);
+  const int m = tfhe_hip_key_bcast_mode(b->ctx);
+  napi_create_string_utf8(env, m == 2 ? "rccl" : m == 1 ? "copy" : "single", NAPI_AUTO_LENGTH, &x);
+  napi_set_named_property(env, o, "keyBroadcast", x);
+  napi_create_int32(env, b->pending, &x);
+  napi_set_named_property(env, o, "pending", x);
+  return o;
 }
 
 /* loadKeys(handle, bsk, ksk) */
@@ -323,9 +411,10 @@ static napi_value js_load_keys(napi_env env, napi_callback_info info) {
   ctx_box* b = argc ? get_box(env, argv[0]) : NULL;
   uint64_t *bsk, *ksk;
   size_t bl, kl;
-  if (!b || !b->ctx || argc < 3 || !get_typed(env, argv[1], napi_biguint64_array, (void**)&bsk, &bl) ||
+  if (!b || !b->ctx || b->destroy_requested || b->pending || argc < 3 ||
+      !get_typed(env, argv[1], napi_biguint64_array, (void**)&bsk, &bl) ||
       !get_typed(env, argv[2], napi_biguint64_array, (void**)&ksk, &kl)) {
-    napi_throw_type_error(env, "EINVAL", "loadKeys(engine, bsk, ksk[, msZeros])");
+    napi_throw_type_error(env, "EINVAL", "loadKeys(engine, bsk, ksk[, msZeros]) on an idle live engine");
     return NULL;
   }
   uint64_t* zeros = NULL;
@@ -348,14 +437,16 @@ static napi_value js_load_keys(napi_env env, napi_callback_info info) {
   return NULL;
 }
 
-/* ---- async work: pbs / nand ------------------------------------------------------------ */
+/* ---- async work: pbs / nand / keyswitch / blindRotate ------------------------------------ */
+enum { JOB_PBS = 0, JOB_NAND = 1, JOB_KEYSWITCH = 2, JOB_BLIND_ROTATE = 3 };
 typedef struct {
   napi_async_work work;
   napi_deferred deferred;
-  napi_ref refs[4];
+  napi_ref refs[5];
   int nrefs;
+  ctx_box* box;
   tfhe_ctx* ctx;
-  int kind; /* 0 = pbs, 1 = nand */
+  int kind;
   const uint64_t *in, *in2, *luts;
   const uint32_t* lut_index;
   size_t B, n_lut;
@@ -368,8 +459,10 @@ typedef struct {
 static void job_execute(napi_env env, void* data) {
   (void)env;
   job_t* j = (job_t*)data;
-  if (j->kind == 0) j->rc = tfhe_hip_pbs(j->ctx, j->in, j->B, j->luts, j->n_lut, j->lut_index, j->out);
-  else j->rc = tfhe_hip_nand(j->ctx, j->in, j->in2, j->B, j->out);
+  if (j->kind == JOB_PBS) j->rc = tfhe_hip_pbs(j->ctx, j->in, j->B, j->luts, j->n_lut, j->lut_index, j->out);
+  else if (j->kind == JOB_NAND) j->rc = tfhe_hip_nand(j->ctx, j->in, j->in2, j->B, j->out);
+  else if (j->kind == JOB_KEYSWITCH) j->rc = tfhe_hip_keyswitch(j->ctx, j->in, j->B, j->out);
+  else j->rc = tfhe_hip_blind_rotate(j->ctx, j->in, j->B, j->luts, j->n_lut, j->lut_index, j->out);
   if (j->rc) snprintf(j->err, sizeof(j->err), "%s", tfhe_hip_last_error());
 }
 
@@ -393,10 +486,17 @@ static void job_complete(napi_env env, napi_status status, void* data) {
   for (int i = 0; i < j->nrefs; i++) napi_delete_reference(env, j->refs[i]);
   napi_delete_reference(env, j->out_ref);
   napi_delete_async_work(env, j->work);
+  ctx_box* b = j->box;
+  if (--b->pending == 0 && b->destroy_requested && b->ctx) {
+    tfhe_hip_destroy(b->ctx);
+    b->ctx = NULL;
+  }
   free(j);
 }
 
-static napi_value queue_job(napi_env env, job_t* j, napi_value* keep, int nkeep, size_t out_len) {
+/* engine: the handle (argv[0]) -- referenced by the job, so the box outlives it */
+static napi_value queue_job(napi_env env, ctx_box* b, napi_value engine, job_t* j, napi_value* keep, int nkeep,
+                            size_t out_len) {
   napi_value promise, out, name;
   uint64_t* outp;
   out = new_u64_array(env, out_len, &outp);
@@ -404,9 +504,13 @@ static napi_value queue_job(napi_env env, job_t* j, napi_value* keep, int nkeep,
     free(j);
     return throw_tfhe(env, TFHE_HIP_ENOMEM);
   }
+  j->box = b;
+  j->ctx = b->ctx;
   j->out = outp;
   napi_create_reference(env, out, 1, &j->out_ref);
+  napi_create_reference(env, engine, 1, &j->refs[j->nrefs++]);
   for (int i = 0; i < nkeep; i++) napi_create_reference(env, keep[i], 1, &j->refs[j->nrefs++]);
+  b->pending++;
   NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
   napi_create_string_utf8(env, "tfhe_hip", NAPI_AUTO_LENGTH, &name);
   NAPI_CALL(env, napi_create_async_work(env, NULL, name, job_execute, job_complete, j, &j->work));
@@ -414,54 +518,100 @@ static napi_value queue_job(napi_env env, job_t* j, napi_value* keep, int nkeep,
   return promise;
 }
 
-/* pbs(handle, cts, luts[, lutIndex]) -> Promise<BigUint64Array> */
-static napi_value js_pbs(napi_env env, napi_callback_info info) {
+static ctx_box* live_box(napi_env env, size_t argc, napi_value* argv) {
+  ctx_box* b = argc ? get_box(env, argv[0]) : NULL;
+  return b && b->ctx && !b->destroy_requested ? b : NULL;
+}
+
+/* optional Uint32Array lutIndex at argv[i]: 1 = ok (idx may stay NULL), 0 = wrong type */
+static int get_lut_index(napi_env env, size_t argc, napi_value* argv, size_t i, uint32_t** idx, size_t* n) {
+  napi_valuetype t = napi_undefined;
+  if (argc > i) napi_typeof(env, argv[i], &t);
+  if (t == napi_undefined || t == napi_null) return 1;
+  return get_typed(env, argv[i], napi_uint32_array, (void**)idx, n);
+}
+
+/* pbs(engine, cts, luts[, lutIndex]) -> Promise<BigUint64Array>: full PBS (both orders incl. keyswitch) */
+/* blindRotate(engine, cts, luts[, lutIndex]) -> Promise<BigUint64Array> of B x (k+1) x N accumulators */
+static napi_value pbs_like(napi_env env, napi_callback_info info, int kind) {
   size_t argc = 4;
   napi_value argv[4];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  ctx_box* b = argc ? get_box(env, argv[0]) : NULL;
+  ctx_box* b = live_box(env, argc, argv);
   uint64_t *in, *luts;
   uint32_t* idx = NULL;
   size_t n_in, n_l, n_idx = 0;
-  if (!b || !b->ctx || argc < 3 || !get_typed(env, argv[1], napi_biguint64_array, (void**)&in, &n_in) ||
+  const char* usage = kind == JOB_PBS ? "pbs(engine, cts, luts[, lutIndex])" : "blindRotate(engine, cts, luts[, lutIndex])";
+  if (!b || argc < 3 || !get_typed(env, argv[1], napi_biguint64_array, (void**)&in, &n_in) ||
       !get_typed(env, argv[2], napi_biguint64_array, (void**)&luts, &n_l)) {
-    napi_throw_type_error(env, "EINVAL", "pbs(engine, cts, luts[, lutIndex])");
+    napi_throw_type_error(env, "EINVAL", usage);
     return NULL;
   }
-  napi_valuetype t = napi_undefined;
-  if (argc > 3) napi_typeof(env, argv[3], &t);
-  if (t != napi_undefined && t != napi_null && !get_typed(env, argv[3], napi_uint32_array, (void**)&idx, &n_idx)) {
+  if (!get_lut_index(env, argc, argv, 3, &idx, &n_idx)) {
     napi_throw_type_error(env, "EINVAL", "lutIndex must be a Uint32Array");
     return NULL;
   }
+  const tfhe_params p = b->p;
+  /* blind rotation inputs are small-key LWEs (n + 1), PBS inputs are io_dim + 1 */
+  const size_t dim = kind == JOB_PBS ? (size_t)tfhe_hip_io_dim(&p) + 1 : (size_t)p.n + 1;
+  if (n_in % dim || n_l % p.N || !n_l || (idx && n_idx != n_in / dim)) {
+    napi_throw_range_error(env, "EINVAL", "buffer sizes do not match the parameter set");
+    return NULL;
+  }
   job_t* j = (job_t*)calloc(1, sizeof(job_t));
-  j->ctx = b->ctx;
-  j->kind = 0;
+  if (!j) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  j->kind = kind;
   j->in = in;
   j->luts = luts;
   j->lut_index = idx;
-  const tfhe_params p = b->p;
-  const size_t dim = (size_t)tfhe_hip_io_dim(&p) + 1;
-  if (n_in % dim || n_l % p.N || (idx && n_idx != n_in / dim)) {
-    free(j);
-    napi_throw_range_error(env, "EINVAL", "pbs: buffer sizes do not match the parameter set");
-    return NULL;
-  }
   j->B = n_in / dim;
   j->n_lut = n_l / p.N;
   napi_value keep[3] = {argv[1], argv[2], idx ? argv[3] : argv[1]};
-  return queue_job(env, j, keep, 3, n_in);
+  const size_t out_len = kind == JOB_PBS ? n_in : j->B * (size_t)(p.k + 1) * p.N;
+  return queue_job(env, b, argv[0], j, keep, 3, out_len);
 }
 
-/* nand(handle, c1, c2) -> Promise<BigUint64Array> */
+static napi_value js_pbs(napi_env env, napi_callback_info info) { return pbs_like(env, info, JOB_PBS); }
+static napi_value js_blind_rotate(napi_env env, napi_callback_info info) {
+  return pbs_like(env, info, JOB_BLIND_ROTATE);
+}
+
+/* keyswitch(engine, bigLwes: B x (kN+1)) -> Promise<BigUint64Array> of B x (n+1) (LWE keyswitch, the KS half
+ * of ServerKey::keyswitch_programmable_bootstrap, ml/biometrics/notebooks/main.rs:71) */
+static napi_value js_keyswitch(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  ctx_box* b = live_box(env, argc, argv);
+  uint64_t* in;
+  size_t n_in;
+  if (!b || argc < 2 || !get_typed(env, argv[1], napi_biguint64_array, (void**)&in, &n_in)) {
+    napi_throw_type_error(env, "EINVAL", "keyswitch(engine, bigLwes)");
+    return NULL;
+  }
+  const size_t big = (size_t)b->p.k * b->p.N + 1, small = (size_t)b->p.n + 1;
+  if (n_in % big) {
+    napi_throw_range_error(env, "EINVAL", "keyswitch: length is not a multiple of k*N + 1");
+    return NULL;
+  }
+  job_t* j = (job_t*)calloc(1, sizeof(job_t));
+  if (!j) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  j->kind = JOB_KEYSWITCH;
+  j->in = in;
+  j->B = n_in / big;
+  napi_value keep[1] = {argv[1]};
+  return queue_job(env, b, argv[0], j, keep, 1, j->B * small);
+}
+
+/* nand(engine, c1, c2) -> Promise<BigUint64Array> */
 static napi_value js_nand(napi_env env, napi_callback_info info) {
   size_t argc = 3;
   napi_value argv[3];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  ctx_box* b = argc ? get_box(env, argv[0]) : NULL;
+  ctx_box* b = live_box(env, argc, argv);
   uint64_t *c1, *c2;
   size_t n1, n2;
-  if (!b || !b->ctx || argc < 3 || !get_typed(env, argv[1], napi_biguint64_array, (void**)&c1, &n1) ||
+  if (!b || argc < 3 || !get_typed(env, argv[1], napi_biguint64_array, (void**)&c1, &n1) ||
       !get_typed(env, argv[2], napi_biguint64_array, (void**)&c2, &n2) || n1 != n2) {
     napi_throw_type_error(env, "EINVAL", "nand(engine, c1, c2) with equal-length BigUint64Arrays");
     return NULL;
@@ -472,13 +622,13 @@ static napi_value js_nand(napi_env env, napi_callback_info info) {
     return NULL;
   }
   job_t* j = (job_t*)calloc(1, sizeof(job_t));
-  j->ctx = b->ctx;
-  j->kind = 1;
+  if (!j) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  j->kind = JOB_NAND;
   j->in = c1;
   j->in2 = c2;
   j->B = n1 / dim;
   napi_value keep[2] = {argv[1], argv[2]};
-  return queue_job(env, j, keep, 2, n1);
+  return queue_job(env, b, argv[0], j, keep, 2, n1);
 }
 
 static napi_value js_last_error(napi_env env, napi_callback_info info) {
@@ -501,6 +651,9 @@ static napi_value init(napi_env env, napi_value exports) {
       {"loadKeys", 0, js_load_keys, 0, 0, 0, napi_enumerable, 0},
       {"pbs", 0, js_pbs, 0, 0, 0, napi_enumerable, 0},
       {"nand", 0, js_nand, 0, 0, 0, napi_enumerable, 0},
+      {"keyswitch", 0, js_keyswitch, 0, 0, 0, napi_enumerable, 0},
+      {"blindRotate", 0, js_blind_rotate, 0, 0, 0, napi_enumerable, 0},
+      {"engineInfo", 0, js_engine_info, 0, 0, 0, napi_enumerable, 0},
       {"lastError", 0, js_last_error, 0, 0, 0, napi_enumerable, 0},
   };
   napi_define_properties(env, exports, sizeof(d) / sizeof(d[0]), d);

@@ -20,4 +20,12 @@ const m = ck.encrypt([0, 1, 2, 3], 4, 9n);
 assert.deepStrictEqual(ck.decrypt(m, 4), [0, 1, 2, 3]);
 try { t.native.lutFromTable(1024, 3, new BigUint64Array(3), 1n); out.err = 'none'; } catch (e) { out.err = e.code; }
 try { new t.Engine(p, 0); out.engine = 'created'; } catch (e) { out.engine = e.code; }
+// production defaults draw OS entropy: fresh keys and fresh encryption randomness every call
+const [ck1] = t.genKeys(p), [ck2] = t.genKeys(p);
+out.entropy_keys_differ = h(ck1.lweKey) !== h(ck2.lweKey);
+const e1 = ck1.encryptBool([true]), e2 = ck1.encryptBool([true]);
+out.entropy_cts_differ = h(e1) !== h(e2) && ck1.decryptBool(e1)[0] && ck1.decryptBool(e2)[0];
+try { new t.LuxFHELocalClient({ seed: 1n }); out.seed_refused = false; } catch (e) { out.seed_refused = /dev: true/.test(e.message); }
+out.seed_dev_ok = new t.LuxFHELocalClient({ seed: 1n, dev: true }).seed === 1n;
+out.default_params = new t.LuxFHELocalClient().params.transform;
 console.log(JSON.stringify(out));

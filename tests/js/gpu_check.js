@@ -26,9 +26,35 @@ const t = require('../../js');
   // several PBS in flight from the event loop
   const many = await Promise.all([0, 1, 2].map(() => eng.pbs(ct, acc)));
   for (const r of many) assert.deepStrictEqual(ck.decrypt(r, 8), msgs.map((m) => f(m) % 8));
+  // stage-level calls: blind rotation alone, keyswitch alone (P-GATE: PBS = KS(SE(BR)))
+  const br = await eng.blindRotate(ct, acc);
+  assert.strictEqual(br.length, msgs.length * 2 * p.N);
+  const big = new BigUint64Array(msgs.length * (p.N + 1));  // sample extract on the host: a_j = -A[N-j]
+  for (let q = 0; q < msgs.length; q++) {
+    const A = br.subarray(q * 2 * p.N, q * 2 * p.N + p.N), Bp = br.subarray(q * 2 * p.N + p.N, (q + 1) * 2 * p.N);
+    const o = big.subarray(q * (p.N + 1), (q + 1) * (p.N + 1));
+    o[0] = A[0];
+    for (let j = 1; j < p.N; j++) o[j] = BigInt.asUintN(64, -A[p.N - j]);
+    o[p.N] = Bp[0];
+  }
+  if (p.transform === 1) {  // FFT64 accumulators are native-torus values: extract + keyswitch == pbs
+    const ks = await eng.keyswitch(big);
+    assert.deepStrictEqual(Array.from(ks), Array.from(res));
+  }
+  // destroy while a job is in flight: the job still completes (the ctx outlives it), then it is gone
+  const inflight = eng.pbs(ct, acc);
   eng.destroy();
+  assert.deepStrictEqual(ck.decrypt(await inflight, 8), msgs.map((m) => f(m) % 8));
+  // two shards of device 0: the batch splits across them, keys reach shard 1 by device copy
+  const eng2 = new t.Engine(p, [0, 0]).loadKeys(sk);
+  const info = eng2.info();
+  assert.deepStrictEqual(info.devices, [0, 0]);
+  assert.strictEqual(info.keyBroadcast, 'copy');
+  const r2 = await eng2.pbs(ct, acc);
+  assert.deepStrictEqual(Array.from(r2), Array.from(res));
+  eng2.destroy();
   // luxfhejs-style client
-  const cl = new t.LuxFHELocalClient({ params: p });
+  const cl = new t.LuxFHELocalClient({ params: p, devices: [0, 0] });
   await cl.initialize();
   const l = await cl.encrypt_uint8(0b10110011), r = await cl.encrypt_uint8(0b01100110);
   const x = await cl.evaluate({ op: 'xor', left: l, right: r, bitWidth: 8 });

@@ -58,7 +58,9 @@ function request(port, method, url, body, headers = {}) {
       return out;
     },
   };
-  const cfg = fhevm ? { params: 'fhevm' } : {};
+  // GPU: the server defaults (FFT64 engines), spread over two shards of device 0 (the --devices split)
+  const cfg = fhevm ? { params: useGpu ? 'fhevm_fft' : 'fhevm' } : {};
+  if (useGpu) cfg.devices = [0, 0];
   if (!useGpu) cfg.engine = fhevm ? rdbl : dbl;
   client = new tfhe.LuxFHELocalClient(cfg);
   const ctBytes = (w) => 16 + 8 * (fhevm ? (w / 2) * 2049 : w * 631);

@@ -161,3 +161,31 @@ def test_ms_noise_reduction_rule_oracle(oracle_mod):
     assert (picks[:-2] >= 0).mean() > 0.5 and (picks[-2:] >= 0).all()
     d = (ok.phase(red[:-2], ok.lwe_key, prm.n) - ok.phase(small[:-2], ok.lwe_key, prm.n)).view(np.int64)
     assert np.abs(d).max() < 2 ** 50
+
+
+def test_entropy_keygen_and_encryption_are_fresh():
+    """no public default seed.  gen_keys / server_keygen / encrypt without a seed draw
+    192 bits of OS entropy: two key sets, two server keys for one client key and two encryptions of
+    one message all differ (and still decrypt); an explicit seed stays reproducible (tests, oracle)."""
+    import tfhe_amd
+    p = tfhe_amd.Params.preset(tfhe_amd.PRESET_GATE_FFT)
+    a, _ = tfhe_amd.gen_keys(p, with_server_key=False)
+    b, _ = tfhe_amd.gen_keys(p, with_server_key=False)
+    assert a.seed is None and not np.array_equal(a.lwe_key, b.lwe_key)
+    s1, s2 = tfhe_amd.gen_keys(p, 99, with_server_key=False)[0], tfhe_amd.gen_keys(p, 99, with_server_key=False)[0]
+    assert np.array_equal(s1.lwe_key, s2.lwe_key)
+    c1, c2 = a.encrypt_bool([True, False]), a.encrypt_bool([True, False])
+    assert not np.array_equal(c1, c2)
+    assert list(a.decrypt_bool(c1)) == [True, False] and list(a.decrypt_bool(c2)) == [True, False]
+    assert np.array_equal(a.encrypt_bool([True], seed=5), a.encrypt_bool([True], seed=5))
+    k1, k2 = tfhe_amd.rng_key(), tfhe_amd.rng_key()
+    assert list(k1.w) != list(k2.w)
+    fh = tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM)
+    ck, _ = tfhe_amd.gen_keys(fh, 7, with_server_key=False)
+    sk1, sk2 = tfhe_amd.server_keygen(ck), tfhe_amd.server_keygen(ck)
+    assert not np.array_equal(sk1.ksk[:4096], sk2.ksk[:4096])
+    assert not np.array_equal(sk1.ms_zeros[:4], sk2.ms_zeros[:4])
+    # the KSK rows still encrypt the right key bits: phase of row (j=0, level 0) is s'_0 * 2^60 + small noise
+    ph = ck.phase(sk1.ksk[: fh.n + 1], key=ck.lwe_key)
+    want = int(ck.glwe_key[0]) << 60
+    assert abs(((int(ph[0]) - want + (1 << 63)) % (1 << 64)) - (1 << 63)) < (1 << 50)

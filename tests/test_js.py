@@ -33,7 +33,8 @@ def _run(script, timeout, *args):
 def test_js_addon_cpu(product_keys):
     out = _run("cpu_check.js", 300)
     assert out["exports"] == sorted(["paramsPreset", "keygen", "encrypt", "phase", "lutConstant", "lutFromTable",
-                                     "createEngine", "destroyEngine", "loadKeys", "pbs", "nand", "lastError"])
+                                     "createEngine", "destroyEngine", "loadKeys", "pbs", "nand", "lastError",
+                                     "keyswitch", "blindRotate", "engineInfo"])
     ck, sk = product_keys
     sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
     assert out["lwe_key_sha"] == sha(ck.lwe_key)
@@ -42,6 +43,10 @@ def test_js_addon_cpu(product_keys):
     cts = ck.encrypt_bool(np.array([True, False, True]), seed=0xC0FFEE02, stream0=5)
     assert out["ct_sha"] == sha(cts)
     assert out["err"] == "-1"
+    # no public default seed -- keys and encryptions from OS entropy, fixed seeds only with dev
+    assert out["entropy_keys_differ"] and out["entropy_cts_differ"]
+    assert out["seed_refused"] and out["seed_dev_ok"]
+    assert out["default_params"] == 1  # LuxFHELocalClient defaults to the FFT64 engine
     if out["engine"] != "created":  # no GPU here: a clean error, not an abort
         assert out["engine"] in ("-1", "-3")
 

@@ -76,6 +76,22 @@ class Params(ctypes.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+class RngKey(ctypes.Structure):
+    """192-bit ChaCha20 key material (tfhe_rng_key)."""
+    _fields_ = [("w", ctypes.c_uint32 * 6)]
+
+
+def rng_key(seed: Optional[int] = None) -> RngKey:
+    """seed None: 192 bits of OS entropy (production keys and encryptions); an int: the REPRODUCIBLE
+    seeded stream that tests, golden vectors and the oracle use (public knowledge -- test data only)."""
+    k = RngKey()
+    if seed is None:
+        _check(lib().tfhe_hip_rng_key_entropy(ctypes.byref(k)))
+    else:
+        _check(lib().tfhe_hip_rng_key_from_seed(ctypes.c_uint64(seed), ctypes.byref(k)))
+    return k
+
+
 _LIB = None
 
 # Every symbol declared in include/tfhe_hip.h (tests check the .so exports all of them).
@@ -93,7 +109,9 @@ ABI_SYMBOLS = (
     "tfhe_hip_glwe_phase", "tfhe_hip_sns_params_preset", "tfhe_hip_sns_bsk_len", "tfhe_hip_sns_keygen",
     "tfhe_hip_sns_create", "tfhe_hip_sns_destroy", "tfhe_hip_sns_load_key", "tfhe_hip_sns_squash",
     "tfhe_hip_sns_squash_async", "tfhe_hip_sns_blind_rotate", "tfhe_hip_sns_phase", "tfhe_hip_fft_fwd",
-    "tfhe_hip_fft_inv",
+    "tfhe_hip_fft_inv", "tfhe_hip_rng_key_entropy", "tfhe_hip_rng_key_from_seed", "tfhe_hip_keygen_k",
+    "tfhe_hip_server_keygen_k", "tfhe_hip_ms_zeros_keygen_k", "tfhe_hip_lwe_encrypt_k", "tfhe_hip_ndev",
+    "tfhe_hip_device_at", "tfhe_hip_key_bcast_mode",
 )
 
 # P-FHEVM modulus-switch noise reduction key (include/tfhe_hip.h TFHE_HIP_MS_FHEVM_*)
@@ -138,7 +156,19 @@ def lib():
         L.tfhe_hip_lwe_phase.argtypes = [ctypes.c_uint32, _U64P, _U64P, ctypes.c_size_t, _U64P]
         L.tfhe_hip_lut_constant.argtypes = [ctypes.c_uint32, ctypes.c_uint64, _U64P]
         L.tfhe_hip_lut_from_table.argtypes = [ctypes.c_uint32, ctypes.c_uint32, _U64P, ctypes.c_uint64, _U64P]
-        L.tfhe_hip_create.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.tfhe_hip_create.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_void_p)]
+        L.tfhe_hip_ndev.argtypes = [ctypes.c_void_p]
+        L.tfhe_hip_device_at.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.tfhe_hip_key_bcast_mode.argtypes = [ctypes.c_void_p]
+        _RKP = ctypes.POINTER(RngKey)
+        L.tfhe_hip_rng_key_entropy.argtypes = [_RKP]
+        L.tfhe_hip_rng_key_from_seed.argtypes = [ctypes.c_uint64, _RKP]
+        L.tfhe_hip_keygen_k.argtypes = [ctypes.c_void_p, _RKP, _U64P, _U64P, _U64P, _U64P]
+        L.tfhe_hip_server_keygen_k.argtypes = [ctypes.c_void_p, _RKP, _U64P, _U64P, _U64P, _U64P]
+        L.tfhe_hip_ms_zeros_keygen_k.argtypes = [ctypes.c_void_p, _RKP, _U64P, ctypes.c_uint32, _U64P]
+        L.tfhe_hip_lwe_encrypt_k.argtypes = [ctypes.c_uint32, _U64P, ctypes.c_int32, _RKP, ctypes.c_uint64, _U64P,
+                                             ctypes.c_size_t, _U64P]
         L.tfhe_hip_destroy.argtypes = [ctypes.c_void_p]
         L.tfhe_hip_load_keys.argtypes = [ctypes.c_void_p, _U64P, ctypes.c_size_t, _U64P, ctypes.c_size_t]
         L.tfhe_hip_load_keys_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
@@ -220,9 +250,10 @@ def decode_bool(phase) -> np.ndarray:
 
 # --------------------------------------------------------------------------------------- keys
 class ClientKey:
-    """Secret key material: LWE key s (dim n) and GLWE key S (k*N), from a ChaCha20 seed."""
+    """Secret key material: LWE key s (dim n) and GLWE key S (k*N).  ``seed`` is the test seed the keys
+    were derived from, or None for keys drawn from OS entropy."""
 
-    def __init__(self, params: Params, seed: int, lwe_key: np.ndarray, glwe_key: np.ndarray):
+    def __init__(self, params: Params, seed: Optional[int], lwe_key: np.ndarray, glwe_key: np.ndarray):
         self.params, self.seed, self.lwe_key, self.glwe_key = params, seed, lwe_key, glwe_key
 
     # keys of the PBS input/output ciphertexts
@@ -234,13 +265,16 @@ class ClientKey:
     def io_noise_log2(self) -> int:
         return self.params.lwe_noise_log2 if self.params.order == 0 else self.params.glwe_noise_log2
 
-    def encrypt_torus(self, msgs, seed: int = 1, stream0: int = 0) -> np.ndarray:
+    def encrypt_torus(self, msgs, seed: Optional[int] = None, stream0: int = 0) -> np.ndarray:
+        """seed None (default): masks and noise from a fresh 192-bit OS-entropy ChaCha key per call;
+        an int seed: the reproducible test stream (ciphertext q on stream stream0 + q)."""
         m = _c_u64(msgs).reshape(-1)
         dim = self.params.io_dim
         out = np.zeros((m.shape[0], dim + 1), dtype=np.uint64)
         key = _c_u64(self.io_key)
-        _check(lib().tfhe_hip_lwe_encrypt(dim, _u64(key), self.io_noise_log2, seed, stream0, _u64(m), m.shape[0],
-                                          _u64(out)))
+        rk = rng_key(seed)
+        _check(lib().tfhe_hip_lwe_encrypt_k(dim, _u64(key), self.io_noise_log2, ctypes.byref(rk), stream0, _u64(m),
+                                            m.shape[0], _u64(out)))
         return out
 
     def phase(self, cts: np.ndarray, key: Optional[np.ndarray] = None) -> np.ndarray:
@@ -251,13 +285,13 @@ class ClientKey:
         _check(lib().tfhe_hip_lwe_phase(dim, _u64(key), _u64(cts), cts.shape[0], _u64(out)))
         return out
 
-    def encrypt_bool(self, bits, seed: int = 1, stream0: int = 0) -> np.ndarray:
+    def encrypt_bool(self, bits, seed: Optional[int] = None, stream0: int = 0) -> np.ndarray:
         return self.encrypt_torus(encode_bool(bits), seed, stream0)
 
     def decrypt_bool(self, cts) -> np.ndarray:
         return decode_bool(self.phase(cts))
 
-    def encrypt(self, msgs, msg_modulus: int, seed: int = 1, stream0: int = 0) -> np.ndarray:
+    def encrypt(self, msgs, msg_modulus: int, seed: Optional[int] = None, stream0: int = 0) -> np.ndarray:
         """Shortint-style encoding with one padding bit: m * 2^63 / msg_modulus (encryption.rs:5-22)."""
         delta = (1 << 63) // msg_modulus
         m = (np.asarray(msgs, dtype=np.uint64) % np.uint64(msg_modulus)) * np.uint64(delta)
@@ -278,16 +312,23 @@ class ServerKey:
         self.params, self.bsk, self.ksk, self.ms_zeros = params, bsk, ksk, ms_zeros
 
 
-def ms_zeros_keygen(params: Params, seed: int, lwe_key: np.ndarray, count: int = MS_FHEVM["count"]) -> np.ndarray:
-    """Encryptions of zero under the small key for the modulus-switch noise reduction."""
+def ms_zeros_keygen(params: Params, seed: Optional[int], lwe_key: np.ndarray,
+                    count: int = MS_FHEVM["count"]) -> np.ndarray:
+    """Encryptions of zero under the small key for the modulus-switch noise reduction (seed None:
+    OS entropy)."""
     z = np.zeros((count, params.n + 1), dtype=np.uint64)
     lwe = _c_u64(lwe_key)
-    _check(lib().tfhe_hip_ms_zeros_keygen(ctypes.byref(params), seed, _u64(lwe), count, _u64(z)))
+    rk = rng_key(seed)
+    _check(lib().tfhe_hip_ms_zeros_keygen_k(ctypes.byref(params), ctypes.byref(rk), _u64(lwe), count, _u64(z)))
     return z
 
 
-def gen_keys(params: Optional[Params] = None, seed: int = 0x7F4E0001, with_server_key: bool = True):
-    """Deterministic key generation (tfhe-rs ``gen_keys`` analogue).  Returns (ClientKey, ServerKey)."""
+def gen_keys(params: Optional[Params] = None, seed: Optional[int] = None, with_server_key: bool = True):
+    """Key generation (tfhe-rs ``gen_keys`` analogue).  Returns (ClientKey, ServerKey).
+
+    seed None (default): every key and the server-key randomness come from a fresh 192-bit OS-entropy
+    ChaCha20 key.  An int seed gives the REPRODUCIBLE test key set (same streams as the oracle) --
+    anyone who knows the seed knows the secret key, so seeded keys are for tests and benchmarks only."""
     params = params or Params.preset(PRESET_GATE)
     L = lib()
     lwe = np.zeros(params.n, dtype=np.uint64)
@@ -296,24 +337,36 @@ def gen_keys(params: Optional[Params] = None, seed: int = 0x7F4E0001, with_serve
     if with_server_key:
         bsk = np.zeros(L.tfhe_hip_bsk_len(ctypes.byref(params)), dtype=np.uint64)
         ksk = np.zeros(L.tfhe_hip_ksk_len(ctypes.byref(params)), dtype=np.uint64)
-    _check(L.tfhe_hip_keygen(ctypes.byref(params), seed, _u64(lwe), _u64(glwe),
-                             _u64(bsk) if bsk is not None else None, _u64(ksk) if ksk is not None else None))
+    rk = rng_key(seed)
+    _check(L.tfhe_hip_keygen_k(ctypes.byref(params), ctypes.byref(rk), _u64(lwe), _u64(glwe),
+                               _u64(bsk) if bsk is not None else None, _u64(ksk) if ksk is not None else None))
     ck = ClientKey(params, seed, lwe, glwe)
     if not with_server_key:
         return ck, None
-    zeros = ms_zeros_keygen(params, seed, lwe) if params.order == 1 else None
+    zeros = None
+    if params.order == 1:
+        zeros = np.zeros((MS_FHEVM["count"], params.n + 1), dtype=np.uint64)
+        _check(L.tfhe_hip_ms_zeros_keygen_k(ctypes.byref(params), ctypes.byref(rk), _u64(lwe), zeros.shape[0],
+                                            _u64(zeros)))
     return ck, ServerKey(params, bsk, ksk, zeros)
 
 
-def server_keygen(ck: "ClientKey", seed: int = 0x7F4E0001) -> ServerKey:
-    """BSK / KSK for the secret keys of ``ck`` (e.g. a tfhe-rs ClientKey ingested by tfhe_amd.keyio)."""
+def server_keygen(ck: "ClientKey", seed: Optional[int] = None) -> ServerKey:
+    """BSK / KSK (+ MS zeros) for the secret keys of ``ck`` (e.g. a tfhe-rs ClientKey ingested by
+    tfhe_amd.keyio).  seed None (default): fresh 192-bit OS entropy, so the published evaluation keys
+    reveal nothing reproducible; an int seed only for tests."""
     p = ck.params
     L = lib()
     bsk = np.zeros(L.tfhe_hip_bsk_len(ctypes.byref(p)), dtype=np.uint64)
     ksk = np.zeros(L.tfhe_hip_ksk_len(ctypes.byref(p)), dtype=np.uint64)
     lwe, glwe = _c_u64(ck.lwe_key), _c_u64(ck.glwe_key)
-    _check(L.tfhe_hip_server_keygen(ctypes.byref(p), seed, _u64(lwe), _u64(glwe), _u64(bsk), _u64(ksk)))
-    return ServerKey(p, bsk, ksk, ms_zeros_keygen(p, seed, lwe) if p.order == 1 else None)
+    rk = rng_key(seed)
+    _check(L.tfhe_hip_server_keygen_k(ctypes.byref(p), ctypes.byref(rk), _u64(lwe), _u64(glwe), _u64(bsk), _u64(ksk)))
+    zeros = None
+    if p.order == 1:
+        zeros = np.zeros((MS_FHEVM["count"], p.n + 1), dtype=np.uint64)
+        _check(L.tfhe_hip_ms_zeros_keygen_k(ctypes.byref(p), ctypes.byref(rk), _u64(lwe), zeros.shape[0], _u64(zeros)))
+    return ServerKey(p, bsk, ksk, zeros)
 
 
 def lut_constant(N: int, torus_value: int) -> np.ndarray:
@@ -331,14 +384,24 @@ def lut_from_table(N: int, msg_modulus: int, table: Sequence[int], delta_out: in
 
 # ------------------------------------------------------------------------------------- engine
 class Engine:
-    """One device context (one GPU).  Mirrors the server-side operator surface of the path."""
+    """A device engine over one or more GPUs (``device``: an ordinal or a sequence of ordinals, one
+    shard each; include/tfhe_hip.h).  Host-array batches split into per-device slices that run
+    concurrently; keys are uploaded once and broadcast to every shard (RCCL for distinct ordinals).
+    Mirrors the server-side operator surface of the path."""
 
-    def __init__(self, params: Optional[Params] = None, device: int = 0):
+    def __init__(self, params: Optional[Params] = None, device=0):
         self.params = params or Params.preset(PRESET_GATE)
+        devs = [int(device)] if isinstance(device, (int, np.integer)) else [int(d) for d in device]
+        arr = (ctypes.c_int * len(devs))(*devs)
         h = ctypes.c_void_p()
-        _check(lib().tfhe_hip_create(ctypes.byref(self.params), device, ctypes.byref(h)))
+        _check(lib().tfhe_hip_create(ctypes.byref(self.params), arr, len(devs), ctypes.byref(h)))
         self._h = h
-        self.device = device
+        self.devices = devs
+        self.device = devs[0]
+
+    @property
+    def key_bcast_mode(self) -> str:
+        return {0: "single", 1: "copy", 2: "rccl"}.get(lib().tfhe_hip_key_bcast_mode(self._h), "?")
 
     def close(self) -> None:
         if getattr(self, "_h", None) and self._h.value:
@@ -526,7 +589,7 @@ class FheBool:
         self.engine, self.ct = engine, _c_u64(ct).reshape(-1, engine.params.n + 1)
 
     @classmethod
-    def encrypt(cls, values, ck: ClientKey, engine: Engine, seed: int = 1, stream0: int = 0) -> "FheBool":
+    def encrypt(cls, values, ck: ClientKey, engine: Engine, seed: Optional[int] = None, stream0: int = 0) -> "FheBool":
         return cls(engine, ck.encrypt_bool(np.atleast_1d(values), seed, stream0))
 
     def decrypt(self, ck: ClientKey) -> np.ndarray:
@@ -560,7 +623,7 @@ class FheUint8:
         self.bits = _c_u64(bits).reshape(-1, 8, engine.params.n + 1)
 
     @classmethod
-    def encrypt(cls, values, ck: ClientKey, engine: Engine, seed: int = 1, stream0: int = 0) -> "FheUint8":
+    def encrypt(cls, values, ck: ClientKey, engine: Engine, seed: Optional[int] = None, stream0: int = 0) -> "FheUint8":
         v = np.atleast_1d(np.asarray(values, dtype=np.uint64))
         bits = ((v[:, None] >> np.arange(8, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
         return cls(engine, ck.encrypt_bool(bits.reshape(-1), seed, stream0))

@@ -1,13 +1,23 @@
-// api.cpp — the C ABI of libtfhe_hip.so (include/tfhe_hip.h): device context, key residency,
-// launch sequencing, error reporting.  Host code; kernels live in pbs_kernels.hip.
+// api.cpp — the C ABI of libtfhe_hip.so (include/tfhe_hip.h): device shards, key residency and
+// broadcast, launch sequencing, error reporting.  Host code; kernels live in the .hip files.
+//
+// An engine (tfhe_ctx) spans ndev device shards.  A shard = one device ordinal + its own stream,
+// key copy, twiddle tables and workspaces.  Keys reach shard 0 through a pinned staging ring and the
+// other shards by RCCL broadcast (distinct ordinals) or device copies (a repeated ordinal); host-buffer
+// PBS batches split into contiguous slices that the shards run concurrently.
+#include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
 #include <stdarg.h>
-#include <stdlib.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/tfhe_hip.h"
@@ -15,8 +25,8 @@
 #include "gl64.h"
 #include "pbs_kernels.h"
 
-using tfhe::u64;
 using tfhe::u32;
+using tfhe::u64;
 
 namespace {
 
@@ -38,6 +48,12 @@ int fail(int code, const char* fmt, ...) {
     if (_e != hipSuccess)                                                                      \
       return fail(_e == hipErrorOutOfMemory ? TFHE_HIP_ENOMEM : TFHE_HIP_EDEVICE, "%s: %s (%s:%d)", #expr, \
                   hipGetErrorString(_e), __FILE__, __LINE__);                                  \
+  } while (0)
+
+#define RC_TRY(expr)      \
+  do {                    \
+    int _rc = (expr);     \
+    if (_rc) return _rc;  \
   } while (0)
 
 bool params_valid(const tfhe_params* p) {
@@ -72,39 +88,41 @@ u64 canonical_psi(uint32_t N) {
   return gl_pow(w, m);
 }
 
-}  // namespace
-
-struct tfhe_ctx {
-  tfhe_params p{};
-  int device = 0;
-  hipStream_t stream = nullptr;
-  u64* d_bsk = nullptr;  // NTT layout, x N^-1
-  u64* d_ksk = nullptr;
-  void* d_ks_planes = nullptr;  // KSK recoded into 8 signed byte planes (ks_mfma.hip)
-  bool ks_valu = false;         // TFHE_HIP_KS_VALU=1: the VALU keyswitch kernel instead (A/B runs)
-  u64* d_tw = nullptr;  // 4 x 1024 twiddle tables of the device NTT layout
-  u64 ninv = 0;
-  bool keys = false;
-  size_t lat_max = 1024;  // batches up to this size use the latency blind-rotate kernel
-  // modulus-switch noise reduction (order 1): zeros resident in HBM
-  u64* d_ms_zeros = nullptr;
-  uint32_t ms_count = 0;
-  double ms_bound = 0, ms_r_sigma = 0, ms_var128 = 0;
-  // workspaces
-  u64* d_big = nullptr;
-  size_t big_cap = 0;  // u64 elements
-  void* d_stage = nullptr;
-  size_t stage_cap = 0;  // bytes
-  void* d_ks_dig = nullptr;
-  size_t ks_dig_cap = 0;  // bytes
-  std::mutex mu;
-  // timing
-  bool timing = false;
-  std::vector<hipEvent_t> ev[3];  // start/stop pairs, flattened
-  std::vector<hipEvent_t> ev_pool;
+// ---- RCCL, loaded on first use (a process that already holds torch's librccl reuses that copy) -----------
+struct Rccl {
+  bool tried = false, ok = false;
+  std::string why;
+  ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*bcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  const char* (*err)(ncclResult_t) = nullptr;
 };
 
-namespace {
+Rccl& rccl() {
+  static Rccl r;
+  static std::mutex m;
+  std::lock_guard<std::mutex> lk(m);
+  if (r.tried) return r;
+  r.tried = true;
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+  if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    r.why = std::string("dlopen librccl.so.1: ") + dlerror();
+    return r;
+  }
+  r.comm_init_all = (decltype(r.comm_init_all))dlsym(h, "ncclCommInitAll");
+  r.bcast = (decltype(r.bcast))dlsym(h, "ncclBroadcast");
+  r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+  r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+  r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+  r.err = (decltype(r.err))dlsym(h, "ncclGetErrorString");
+  r.ok = r.comm_init_all && r.bcast && r.group_start && r.group_end && r.comm_destroy && r.err;
+  if (!r.ok) r.why = "librccl.so.1 lacks ncclCommInitAll / ncclBroadcast / ncclGroupStart / ncclGroupEnd";
+  return r;
+}
 
 struct DeviceGuard {
   int prev = -1;
@@ -118,8 +136,54 @@ struct DeviceGuard {
   }
 };
 
-int grow(void** ptr, size_t* cap, size_t bytes) {
+}  // namespace
+
+// One device's slice of an engine.
+struct tfhe_shard {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  u64* d_bsk = nullptr;         // transform domain (NTT layout x N^-1, or Fourier)
+  u64* d_ksk = nullptr;         // standard KSK (VALU keyswitch; RCCL broadcast source / target)
+  void* d_ks_planes = nullptr;  // KSK recoded into 8 signed byte planes (ks_mfma.hip)
+  u64* d_tw = nullptr;          // twiddle tables of the device transform
+  u64* d_ms_zeros = nullptr;    // modulus-switch noise reduction zeros (order 1)
+  // workspaces: every user waits for `ws_free` (the previous user's completion) on its own stream
+  u64* d_big = nullptr;
+  size_t big_cap = 0;  // bytes
+  void* d_stage = nullptr;
+  size_t stage_cap = 0;  // bytes
+  void* d_ks_dig = nullptr;
+  size_t ks_dig_cap = 0;  // bytes
+  hipEvent_t ws_free = nullptr;
+  hipStream_t ws_last = nullptr;
+  bool ws_used = false;
+  // timing: start/stop event pairs per slot (0 = blind rotate, 1 = keyswitch, 2 = MS noise reduction)
+  std::vector<hipEvent_t> ev[3];
+  std::vector<hipEvent_t> ev_pool;
+};
+
+struct tfhe_ctx {
+  tfhe_params p{};
+  std::vector<tfhe_shard> sh;
+  bool keys = false;
+  bool ks_valu = false;  // TFHE_HIP_KS_VALU=1: the VALU keyswitch kernel instead (A/B runs)
+  size_t lat_max = 1024; // batches up to this size (per shard) use the latency blind-rotate kernel
+  u64 ninv = 0;
+  uint32_t ms_count = 0;
+  double ms_bound = 0, ms_r_sigma = 0, ms_var128 = 0;
+  int bcast_mode = 0;  // tfhe_hip_key_bcast_mode
+  std::vector<ncclComm_t> comms;
+  std::mutex mu;
+  bool timing = false;
+};
+
+namespace {
+
+using shard = tfhe_shard;
+
+int grow(shard& s, void** ptr, size_t* cap, size_t bytes) {
   if (*cap >= bytes) return 0;
+  if (s.ws_used) HIP_TRY(hipEventSynchronize(s.ws_free));  // no launch may still read the old buffer
   if (*ptr) (void)hipFree(*ptr);
   *ptr = nullptr;
   *cap = 0;
@@ -128,10 +192,23 @@ int grow(void** ptr, size_t* cap, size_t bytes) {
   return 0;
 }
 
-hipEvent_t take_event(tfhe_ctx* c) {
-  if (!c->ev_pool.empty()) {
-    hipEvent_t e = c->ev_pool.back();
-    c->ev_pool.pop_back();
+// Workspace ordering across streams (tfhe_hip_pbs_async may be called on any stream): the stream that
+// uses the shard's workspaces next waits for the event recorded after the previous use.
+int ws_begin(shard& s, hipStream_t st) {
+  if (s.ws_used && s.ws_last != st) HIP_TRY(hipStreamWaitEvent(st, s.ws_free, 0));
+  return 0;
+}
+int ws_end(shard& s, hipStream_t st) {
+  HIP_TRY(hipEventRecord(s.ws_free, st));
+  s.ws_last = st;
+  s.ws_used = true;
+  return 0;
+}
+
+hipEvent_t take_event(shard& s) {
+  if (!s.ev_pool.empty()) {
+    hipEvent_t e = s.ev_pool.back();
+    s.ev_pool.pop_back();
     return e;
   }
   hipEvent_t e = nullptr;
@@ -139,41 +216,41 @@ hipEvent_t take_event(tfhe_ctx* c) {
   return e;
 }
 
-void timed_begin(tfhe_ctx* c, int which, hipStream_t s) {
+void timed_begin(tfhe_ctx* c, shard& s, int which, hipStream_t st) {
   if (!c->timing) return;
-  hipEvent_t e = take_event(c);
+  hipEvent_t e = take_event(s);
   if (e) {
-    (void)hipEventRecord(e, s);
-    c->ev[which].push_back(e);
+    (void)hipEventRecord(e, st);
+    s.ev[which].push_back(e);
   }
 }
-void timed_end(tfhe_ctx* c, int which, hipStream_t s) {
+void timed_end(tfhe_ctx* c, shard& s, int which, hipStream_t st) {
   if (!c->timing) return;
-  if (c->ev[which].size() % 2 == 0) return;  // begin failed
-  hipEvent_t e = take_event(c);
+  if (s.ev[which].size() % 2 == 0) return;  // begin failed
+  hipEvent_t e = take_event(s);
   if (e) {
-    (void)hipEventRecord(e, s);
-    c->ev[which].push_back(e);
+    (void)hipEventRecord(e, st);
+    s.ev[which].push_back(e);
   } else {
-    c->ev_pool.push_back(c->ev[which].back());
-    c->ev[which].pop_back();
+    s.ev_pool.push_back(s.ev[which].back());
+    s.ev[which].pop_back();
   }
 }
 
 uint32_t io_dim(const tfhe_params& p) { return p.order == 0 ? p.n : p.k * p.N; }
 
-hipError_t launch_br(tfhe_ctx* c, const u64* in, size_t B, const u64* luts, const u32* idx, size_t n_lut, u64* out_big,
-                     u64* out_acc, hipStream_t s) {
+hipError_t launch_br(tfhe_ctx* c, shard& s, const u64* in, size_t B, const u64* luts, const u32* idx, size_t n_lut,
+                     u64* out_big, u64* out_acc, hipStream_t st) {
   if (is_fft(c->p) && c->p.N == 2048)
-    return tfhe::launch_blind_rotate_fft2k(in, B, (int)c->p.n, luts, idx, (int)n_lut, (const double*)c->d_bsk,
-                                           (const double*)c->d_tw, out_big, out_acc, s, c->lat_max);
+    return tfhe::launch_blind_rotate_fft2k(in, B, (int)c->p.n, luts, idx, (int)n_lut, (const double*)s.d_bsk,
+                                           (const double*)s.d_tw, out_big, out_acc, st, c->lat_max);
   if (is_fft(c->p))
-    return tfhe::launch_blind_rotate_fft(in, B, (int)c->p.n, luts, idx, (int)n_lut, (const double*)c->d_bsk,
-                                         (const double*)c->d_tw, out_big, out_acc, s, c->lat_max);
+    return tfhe::launch_blind_rotate_fft(in, B, (int)c->p.n, luts, idx, (int)n_lut, (const double*)s.d_bsk,
+                                         (const double*)s.d_tw, out_big, out_acc, st, c->lat_max);
   if (c->p.N == 2048)
-    return tfhe::launch_blind_rotate_2048(in, B, (int)c->p.n, luts, idx, (int)n_lut, c->d_bsk, c->d_tw, out_big, out_acc,
-                                          s, c->lat_max);
-  return tfhe::launch_blind_rotate(in, B, (int)c->p.n, luts, idx, (int)n_lut, c->d_bsk, c->d_tw, out_big, out_acc, s,
+    return tfhe::launch_blind_rotate_2048(in, B, (int)c->p.n, luts, idx, (int)n_lut, s.d_bsk, s.d_tw, out_big, out_acc,
+                                          st, c->lat_max);
+  return tfhe::launch_blind_rotate(in, B, (int)c->p.n, luts, idx, (int)n_lut, s.d_bsk, s.d_tw, out_big, out_acc, st,
                                    c->lat_max);
 }
 
@@ -183,55 +260,57 @@ uint32_t log2u(uint32_t x) {
   return l;
 }
 
-hipError_t launch_ms(tfhe_ctx* c, u64* small, size_t B, int* picks, hipStream_t s) {
-  return tfhe::launch_ms_reduce(small, B, (int)c->p.n, c->d_ms_zeros, (int)c->ms_count, (int)log2u(2 * c->p.N),
-                                c->ms_bound, c->ms_r_sigma, c->ms_var128, picks, s);
+hipError_t launch_ms(tfhe_ctx* c, shard& s, u64* small, size_t B, int* picks, hipStream_t st) {
+  return tfhe::launch_ms_reduce(small, B, (int)c->p.n, s.d_ms_zeros, (int)c->ms_count, (int)log2u(2 * c->p.N),
+                                c->ms_bound, c->ms_r_sigma, c->ms_var128, picks, st);
 }
 
-hipError_t launch_ks(tfhe_ctx* c, const u64* in_big, size_t B, u64* out, hipStream_t s) {
+int launch_ks(tfhe_ctx* c, shard& s, const u64* in_big, size_t B, u64* out, hipStream_t st) {
   const int big_dim = (int)(c->p.k * c->p.N);
-  if (c->ks_valu || !c->d_ks_planes)
-    return tfhe::launch_keyswitch(in_big, B, big_dim, c->d_ksk, (int)c->p.n, (int)c->p.ks_base_log,
-                                  (int)c->p.ks_level, out, s);
-  if (grow(&c->d_ks_dig, &c->ks_dig_cap, tfhe::ks_digits_bytes(B, big_dim, (int)c->p.ks_level)))
-    return hipErrorOutOfMemory;
-  return tfhe::launch_keyswitch_mfma(in_big, B, big_dim, c->d_ks_planes, (int)c->p.n, (int)c->p.ks_base_log,
-                                     (int)c->p.ks_level, c->d_ks_dig, out, s);
+  if (c->ks_valu || !s.d_ks_planes) {
+    HIP_TRY(tfhe::launch_keyswitch(in_big, B, big_dim, s.d_ksk, (int)c->p.n, (int)c->p.ks_base_log,
+                                   (int)c->p.ks_level, out, st));
+    return 0;
+  }
+  RC_TRY(grow(s, &s.d_ks_dig, &s.ks_dig_cap, tfhe::ks_digits_bytes(B, big_dim, (int)c->p.ks_level)));
+  HIP_TRY(tfhe::launch_keyswitch_mfma(in_big, B, big_dim, s.d_ks_planes, (int)c->p.n, (int)c->p.ks_base_log,
+                                      (int)c->p.ks_level, s.d_ks_dig, out, st));
+  return 0;
 }
 
-// PBS on device buffers (caller holds c->mu, device set).  Order 0 (P-GATE): BR + SE -> KS;
-// order 1 (P-FHEVM): KS -> [MS noise reduction] -> BR + SE.  Timing slots 0 = blind rotate,
-// 1 = keyswitch, 2 = modulus-switch noise reduction.
-int pbs_device(tfhe_ctx* c, const u64* d_in, size_t B, const u64* d_luts, size_t n_lut, const u32* d_idx, u64* d_out,
-               hipStream_t s) {
+// PBS on device buffers (caller holds c->mu and has set the shard's device; workspaces ordered by the
+// caller's ws_begin / ws_end).  Order 0 (P-GATE): BR + SE -> KS; order 1 (P-FHEVM): KS -> [MS noise
+// reduction] -> BR + SE.
+int pbs_device(tfhe_ctx* c, shard& s, const u64* d_in, size_t B, const u64* d_luts, size_t n_lut, const u32* d_idx,
+               u64* d_out, hipStream_t st) {
   const size_t big = (size_t)c->p.k * c->p.N + 1, small = (size_t)c->p.n + 1;
-  int rc = grow((void**)&c->d_big, &c->big_cap, B * (c->p.order == 0 ? big : small) * sizeof(u64));
-  if (rc) return rc;
+  RC_TRY(grow(s, (void**)&s.d_big, &s.big_cap, B * (c->p.order == 0 ? big : small) * sizeof(u64)));
   if (c->p.order == 0) {
-    timed_begin(c, 0, s);
-    HIP_TRY(launch_br(c, d_in, B, d_luts, d_idx, n_lut, c->d_big, nullptr, s));
-    timed_end(c, 0, s);
-    timed_begin(c, 1, s);
-    HIP_TRY(launch_ks(c, c->d_big, B, d_out, s));
-    timed_end(c, 1, s);
+    timed_begin(c, s, 0, st);
+    HIP_TRY(launch_br(c, s, d_in, B, d_luts, d_idx, n_lut, s.d_big, nullptr, st));
+    timed_end(c, s, 0, st);
+    timed_begin(c, s, 1, st);
+    RC_TRY(launch_ks(c, s, s.d_big, B, d_out, st));
+    timed_end(c, s, 1, st);
   } else {
-    timed_begin(c, 1, s);
-    HIP_TRY(launch_ks(c, d_in, B, c->d_big, s));
-    timed_end(c, 1, s);
+    timed_begin(c, s, 1, st);
+    RC_TRY(launch_ks(c, s, d_in, B, s.d_big, st));
+    timed_end(c, s, 1, st);
     if (c->ms_count) {
-      timed_begin(c, 2, s);
-      HIP_TRY(launch_ms(c, c->d_big, B, nullptr, s));
-      timed_end(c, 2, s);
+      timed_begin(c, s, 2, st);
+      HIP_TRY(launch_ms(c, s, s.d_big, B, nullptr, st));
+      timed_end(c, s, 2, st);
     }
-    timed_begin(c, 0, s);
-    HIP_TRY(launch_br(c, c->d_big, B, d_luts, d_idx, n_lut, d_out, nullptr, s));
-    timed_end(c, 0, s);
+    timed_begin(c, s, 0, st);
+    HIP_TRY(launch_br(c, s, s.d_big, B, d_luts, d_idx, n_lut, d_out, nullptr, st));
+    timed_end(c, s, 0, st);
   }
   return 0;
 }
 
-// Stage host buffers into one device allocation. Returns device pointers in order.
-int stage(tfhe_ctx* c, std::initializer_list<std::pair<const void*, size_t>> in, std::vector<void*>& dptr,
+// Stage host buffers into the shard's staging allocation (on the shard stream).  Returns device pointers
+// in order, plus one for `extra_out_bytes` of output.
+int stage(shard& s, std::initializer_list<std::pair<const void*, size_t>> in, std::vector<void*>& dptr,
           size_t extra_out_bytes) {
   size_t total = 0;
   std::vector<size_t> off;
@@ -241,22 +320,207 @@ int stage(tfhe_ctx* c, std::initializer_list<std::pair<const void*, size_t>> in,
   }
   const size_t out_off = total;
   total += (extra_out_bytes + 255) & ~(size_t)255;
-  int rc = grow(&c->d_stage, &c->stage_cap, total ? total : 256);
-  if (rc) return rc;
+  RC_TRY(grow(s, &s.d_stage, &s.stage_cap, total ? total : 256));
   size_t i = 0;
   dptr.clear();
   for (auto& x : in) {
-    void* d = (char*)c->d_stage + off[i++];
-    if (x.first && x.second) HIP_TRY(hipMemcpyAsync(d, x.first, x.second, hipMemcpyHostToDevice, c->stream));
+    void* d = (char*)s.d_stage + off[i++];
+    if (x.first && x.second) HIP_TRY(hipMemcpyAsync(d, x.first, x.second, hipMemcpyHostToDevice, s.stream));
     dptr.push_back(x.first ? d : nullptr);
   }
-  dptr.push_back((char*)c->d_stage + out_off);
+  dptr.push_back((char*)s.d_stage + out_off);
+  return 0;
+}
+
+// Host -> device copy through a pinned staging ring (2 x 16 MB): the CPU fills one slot while the DMA
+// engine drains the other.  Pageable sources would otherwise go through the runtime's own bounce buffer
+// one synchronous piece at a time.
+int upload_pinned(shard& s, void* dst, const void* src, size_t bytes) {
+  const size_t slot = 16u << 20;
+  void* ring[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  int rc = 0;
+  auto cleanup = [&]() {
+    for (int i = 0; i < 2; i++) {
+      if (done[i]) (void)hipEventDestroy(done[i]);
+      if (ring[i]) (void)hipHostFree(ring[i]);
+    }
+  };
+  for (int i = 0; i < 2 && !rc; i++) {
+    if (hipHostMalloc(&ring[i], slot, hipHostMallocDefault) != hipSuccess) rc = fail(TFHE_HIP_ENOMEM, "pinned staging alloc");
+    else if (hipEventCreateWithFlags(&done[i], hipEventDisableTiming) != hipSuccess) rc = fail(TFHE_HIP_EDEVICE, "event");
+  }
+  bool used[2] = {false, false};
+  for (size_t off = 0, k = 0; off < bytes && !rc; off += slot, k ^= 1) {
+    const size_t n = std::min(slot, bytes - off);
+    if (used[k] && hipEventSynchronize(done[k]) != hipSuccess) rc = fail(TFHE_HIP_EDEVICE, "staging sync");
+    if (rc) break;
+    memcpy(ring[k], (const char*)src + off, n);
+    if (hipMemcpyAsync((char*)dst + off, ring[k], n, hipMemcpyHostToDevice, s.stream) != hipSuccess ||
+        hipEventRecord(done[k], s.stream) != hipSuccess)
+      rc = fail(TFHE_HIP_EDEVICE, "staged upload failed");
+    used[k] = true;
+  }
+  if (hipStreamSynchronize(s.stream) != hipSuccess && !rc) rc = fail(TFHE_HIP_EDEVICE, "staged upload sync");
+  cleanup();
+  return rc;
+}
+
+bool devices_distinct(const tfhe_ctx* c) {
+  for (size_t i = 0; i < c->sh.size(); i++)
+    for (size_t j = i + 1; j < c->sh.size(); j++)
+      if (c->sh[i].device == c->sh[j].device) return false;
+  return true;
+}
+
+// Broadcast `count` u64 from src (on shard 0's device) into dst[i] of every shard i >= 1.
+int broadcast(tfhe_ctx* c, const u64* src, const std::vector<u64*>& dst, size_t count) {
+  const int nd = (int)c->sh.size();
+  const char* env = getenv("TFHE_HIP_BCAST");
+  const bool forced = env && strcmp(env, "rccl") == 0;  // also a 1-device communicator: the RCCL plumbing test
+  if (nd < 2 && !forced) return 0;
+  const bool want_rccl = env ? forced : devices_distinct(c);
+  if (want_rccl) {
+    if (!devices_distinct(c)) return fail(TFHE_HIP_EINVAL, "RCCL broadcast needs distinct device ordinals");
+    Rccl& R = rccl();
+    if (!R.ok) return fail(TFHE_HIP_EDEVICE, "RCCL unavailable: %s", R.why.c_str());
+    if (c->comms.empty()) {
+      std::vector<int> devs(nd);
+      for (int i = 0; i < nd; i++) devs[i] = c->sh[i].device;
+      c->comms.assign(nd, nullptr);
+      const ncclResult_t r = R.comm_init_all(c->comms.data(), nd, devs.data());
+      if (r != ncclSuccess) {
+        c->comms.clear();
+        return fail(TFHE_HIP_EDEVICE, "ncclCommInitAll: %s", R.err(r));
+      }
+    }
+    R.group_start();
+    ncclResult_t r = ncclSuccess;
+    for (int i = 0; i < nd && r == ncclSuccess; i++) {
+      DeviceGuard g(c->sh[i].device);
+      r = R.bcast(i == 0 ? (const void*)src : (const void*)dst[i], i == 0 ? (void*)src : (void*)dst[i], count,
+                  ncclUint64, 0, c->comms[i], c->sh[i].stream);
+    }
+    const ncclResult_t r2 = R.group_end();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+      return fail(TFHE_HIP_EDEVICE, "ncclBroadcast: %s", R.err(r != ncclSuccess ? r : r2));
+    for (int i = 0; i < nd; i++) {
+      DeviceGuard g(c->sh[i].device);
+      HIP_TRY(hipStreamSynchronize(c->sh[i].stream));
+    }
+    c->bcast_mode = 2;
+    return 0;
+  }
+  for (int i = 1; i < nd; i++) {
+    shard& s = c->sh[i];
+    DeviceGuard g(s.device);
+    if (s.device == c->sh[0].device)
+      HIP_TRY(hipMemcpyAsync(dst[i], src, count * 8, hipMemcpyDeviceToDevice, s.stream));
+    else
+      HIP_TRY(hipMemcpyPeerAsync(dst[i], s.device, src, c->sh[0].device, count * 8, s.stream));
+    HIP_TRY(hipStreamSynchronize(s.stream));
+  }
+  c->bcast_mode = 1;
+  return 0;
+}
+
+// Convert a standard-domain BSK at `std_bsk` (on the shard's device) to the transform domain and the KSK
+// at s.d_ksk to byte planes.
+int convert_keys(tfhe_ctx* c, shard& s, const u64* std_bsk, size_t bsk_len) {
+  const size_t polys = bsk_len / c->p.N;
+  DeviceGuard g(s.device);
+  if (!c->ks_valu) {
+    const int big_dim = (int)(c->p.k * c->p.N);
+    if (!s.d_ks_planes)
+      HIP_TRY(hipMalloc(&s.d_ks_planes, tfhe::ks_planes_bytes(big_dim, (int)c->p.ks_level, (int)c->p.n)));
+    HIP_TRY(tfhe::launch_ksk_planes(s.d_ksk, big_dim, (int)c->p.ks_level, (int)c->p.n, s.d_ks_planes, s.stream));
+  }
+  if (is_fft(c->p) && c->p.N == 2048)
+    HIP_TRY(tfhe::launch_bsk_to_fourier2k(std_bsk, (double*)s.d_bsk, polys, (const double*)s.d_tw, s.stream));
+  else if (is_fft(c->p))
+    HIP_TRY(tfhe::launch_bsk_to_fourier(std_bsk, (double*)s.d_bsk, polys, (const double*)s.d_tw, s.stream));
+  else if (c->p.N == 2048)
+    HIP_TRY(tfhe::launch_bsk_to_ntt_2048(std_bsk, s.d_bsk, polys, s.d_tw, c->ninv, s.stream));
+  else
+    HIP_TRY(tfhe::launch_bsk_to_ntt(std_bsk, s.d_bsk, (int)(polys / 12), s.d_tw, c->ninv, s.stream));
+  HIP_TRY(hipStreamSynchronize(s.stream));
+  return 0;
+}
+
+int shard_init(tfhe_ctx* c, shard& s) {
+  DeviceGuard g(s.device);
+  HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&s.ws_free, hipEventDisableTiming));
+  const tfhe_params& p = c->p;
+  using namespace tfhe;
+  if (is_fft(p)) {  // FFT64: twist / pass tables (pbs_fft.hip: make_fft_tables)
+    std::vector<double> tw(p.N == 2048 ? fft2k_tables_len() : fft_tables_len());
+    if (p.N == 2048) make_fft2k_tables(tw.data());
+    else make_fft_tables(tw.data());
+    HIP_TRY(hipMalloc(&s.d_tw, tw.size() * 8));
+    HIP_TRY(hipMemcpy(s.d_tw, tw.data(), tw.size() * 8, hipMemcpyHostToDevice));
+    return 0;
+  }
+  // twiddle tables of the device NTT layout (pbs_kernels.hip: make_ntt_tables)
+  std::vector<u64> tw(p.N == 2048 ? ntt2048_tables_len() : 4 * p.N);
+  if (p.N == 2048) make_ntt2048_tables(canonical_psi(p.N), tw.data());
+  else make_ntt_tables(canonical_psi(p.N), tw.data());
+  HIP_TRY(hipMalloc(&s.d_tw, tw.size() * 8));
+  HIP_TRY(hipMemcpy(s.d_tw, tw.data(), tw.size() * 8, hipMemcpyHostToDevice));
+  return 0;
+}
+
+void shard_free(shard& s) {
+  DeviceGuard g(s.device);
+  if (s.stream) (void)hipStreamSynchronize(s.stream);
+  for (int w = 0; w < 3; w++)
+    for (auto e : s.ev[w]) (void)hipEventDestroy(e);
+  for (auto e : s.ev_pool) (void)hipEventDestroy(e);
+  (void)hipFree(s.d_bsk);
+  (void)hipFree(s.d_ksk);
+  (void)hipFree(s.d_ks_planes);
+  (void)hipFree(s.d_ks_dig);
+  (void)hipFree(s.d_tw);
+  (void)hipFree(s.d_ms_zeros);
+  (void)hipFree(s.d_big);
+  (void)hipFree(s.d_stage);
+  if (s.ws_free) (void)hipEventDestroy(s.ws_free);
+  if (s.stream) (void)hipStreamDestroy(s.stream);
+}
+
+// Run fn(shard index, lo, hi) for contiguous slices of [0, B) on every shard concurrently (one host
+// thread per shard beyond the first); the first error (with its message) is returned on this thread.
+template <class F>
+int for_each_slice(tfhe_ctx* c, size_t B, F&& fn) {
+  const size_t nd = c->sh.size();
+  std::vector<int> rc(nd, 0);
+  std::vector<std::string> msg(nd);
+  auto run = [&](size_t i) {
+    const size_t lo = B * i / nd, hi = B * (i + 1) / nd;
+    if (lo == hi) return;
+    DeviceGuard g(c->sh[i].device);
+    rc[i] = fn(i, lo, hi);
+    if (rc[i]) msg[i] = g_err;
+  };
+  if (nd == 1) {
+    run(0);
+    return rc[0];
+  }
+  std::vector<std::thread> th;
+  for (size_t i = 1; i < nd; i++) th.emplace_back(run, i);
+  run(0);
+  for (auto& t : th) t.join();
+  for (size_t i = 0; i < nd; i++)
+    if (rc[i]) {
+      g_err = "shard " + std::to_string(i) + " (device " + std::to_string(c->sh[i].device) + "): " + msg[i];
+      return rc[i];
+    }
   return 0;
 }
 
 }  // namespace
 
-// error slot shared with pks_api.cpp
+// error slot shared with pks_api.cpp / sns_api.cpp
 int tfhe_hip_set_error(int code, const char* msg) {
   g_err = msg;
   return code;
@@ -292,37 +556,78 @@ size_t tfhe_hip_bsk_len(const tfhe_params* p) { return p ? tfhe::client::bsk_len
 size_t tfhe_hip_ksk_len(const tfhe_params* p) { return p ? tfhe::client::ksk_len(*p) : 0; }
 uint32_t tfhe_hip_io_dim(const tfhe_params* p) { return p ? io_dim(*p) : 0; }
 
+int tfhe_hip_rng_key_entropy(tfhe_rng_key* out) {
+  if (!out) return fail(TFHE_HIP_EINVAL, "rng_key_entropy: null out");
+  if (!tfhe::client::rng_key_entropy(out)) return fail(TFHE_HIP_EDEVICE, "rng_key_entropy: getrandom failed");
+  return 0;
+}
+
+int tfhe_hip_rng_key_from_seed(uint64_t seed, tfhe_rng_key* out) {
+  if (!out) return fail(TFHE_HIP_EINVAL, "rng_key_from_seed: null out");
+  *out = tfhe::client::rng_key_from_seed(seed);
+  return 0;
+}
+
+static int check_binary(const uint64_t* key, size_t len, const char* what) {
+  for (size_t i = 0; i < len; i++)
+    if (key[i] > 1) return fail(TFHE_HIP_EINVAL, "%s[%zu] is not binary", what, i);
+  return 0;
+}
+
+int tfhe_hip_keygen_k(const tfhe_params* p, const tfhe_rng_key* rk, uint64_t* lwe_key, uint64_t* glwe_key,
+                      uint64_t* bsk, uint64_t* ksk) {
+  if (!params_valid(p) || !rk || !lwe_key || !glwe_key) return fail(TFHE_HIP_EINVAL, "keygen: bad arguments");
+  tfhe::client::keygen(*p, *rk, lwe_key, glwe_key, bsk, ksk);
+  return 0;
+}
+
 int tfhe_hip_keygen(const tfhe_params* p, uint64_t seed, uint64_t* lwe_key, uint64_t* glwe_key, uint64_t* bsk,
                     uint64_t* ksk) {
-  if (!params_valid(p) || !lwe_key || !glwe_key) return fail(TFHE_HIP_EINVAL, "keygen: bad arguments");
-  tfhe::client::keygen(*p, seed, lwe_key, glwe_key, bsk, ksk);
+  const tfhe_rng_key rk = tfhe::client::rng_key_from_seed(seed);
+  return tfhe_hip_keygen_k(p, &rk, lwe_key, glwe_key, bsk, ksk);
+}
+
+int tfhe_hip_server_keygen_k(const tfhe_params* p, const tfhe_rng_key* rk, const uint64_t* lwe_key,
+                             const uint64_t* glwe_key, uint64_t* bsk, uint64_t* ksk) {
+  if (!params_valid(p) || !rk || !lwe_key || !glwe_key) return fail(TFHE_HIP_EINVAL, "server_keygen: bad arguments");
+  RC_TRY(check_binary(lwe_key, p->n, "server_keygen: lwe_key"));
+  RC_TRY(check_binary(glwe_key, (size_t)p->k * p->N, "server_keygen: glwe_key"));
+  tfhe::client::server_keygen(*p, *rk, lwe_key, glwe_key, bsk, ksk);
   return 0;
 }
 
 int tfhe_hip_server_keygen(const tfhe_params* p, uint64_t seed, const uint64_t* lwe_key, const uint64_t* glwe_key,
                            uint64_t* bsk, uint64_t* ksk) {
-  if (!params_valid(p) || !lwe_key || !glwe_key) return fail(TFHE_HIP_EINVAL, "server_keygen: bad arguments");
-  for (uint32_t i = 0; i < p->n; i++)
-    if (lwe_key[i] > 1) return fail(TFHE_HIP_EINVAL, "server_keygen: lwe_key[%u] is not binary", i);
-  for (uint32_t i = 0; i < p->k * p->N; i++)
-    if (glwe_key[i] > 1) return fail(TFHE_HIP_EINVAL, "server_keygen: glwe_key[%u] is not binary", i);
-  tfhe::client::server_keygen(*p, seed, lwe_key, glwe_key, bsk, ksk);
+  const tfhe_rng_key rk = tfhe::client::rng_key_from_seed(seed);
+  return tfhe_hip_server_keygen_k(p, &rk, lwe_key, glwe_key, bsk, ksk);
+}
+
+int tfhe_hip_ms_zeros_keygen_k(const tfhe_params* p, const tfhe_rng_key* rk, const uint64_t* lwe_key, uint32_t count,
+                               uint64_t* zeros) {
+  if (!params_valid(p) || !rk || !lwe_key || (count && !zeros))
+    return fail(TFHE_HIP_EINVAL, "ms_zeros_keygen: bad arguments");
+  tfhe::client::ms_zeros_keygen(*p, *rk, lwe_key, count, zeros);
   return 0;
 }
 
 int tfhe_hip_ms_zeros_keygen(const tfhe_params* p, uint64_t seed, const uint64_t* lwe_key, uint32_t count,
                              uint64_t* zeros) {
-  if (!params_valid(p) || !lwe_key || (count && !zeros)) return fail(TFHE_HIP_EINVAL, "ms_zeros_keygen: bad arguments");
-  tfhe::client::ms_zeros_keygen(*p, seed, lwe_key, count, zeros);
+  const tfhe_rng_key rk = tfhe::client::rng_key_from_seed(seed);
+  return tfhe_hip_ms_zeros_keygen_k(p, &rk, lwe_key, count, zeros);
+}
+
+int tfhe_hip_lwe_encrypt_k(uint32_t dim, const uint64_t* key, int32_t noise_log2, const tfhe_rng_key* rk,
+                           uint64_t stream0, const uint64_t* msgs, size_t count, uint64_t* out) {
+  if (!dim || !key || !rk || (count && (!msgs || !out))) return fail(TFHE_HIP_EINVAL, "lwe_encrypt: bad arguments");
+  if (noise_log2 >= 0 || noise_log2 < -63) return fail(TFHE_HIP_EINVAL, "lwe_encrypt: noise_log2 out of range");
+  tfhe::client::lwe_encrypt(dim, key, noise_log2, *rk, stream0, msgs, count, out);
   return 0;
 }
 
 int tfhe_hip_lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, uint64_t seed, uint64_t stream0,
                          const uint64_t* msgs, size_t count, uint64_t* out) {
-  if (!dim || !key || (count && (!msgs || !out))) return fail(TFHE_HIP_EINVAL, "lwe_encrypt: bad arguments");
-  if (noise_log2 >= 0 || noise_log2 < -63) return fail(TFHE_HIP_EINVAL, "lwe_encrypt: noise_log2 out of range");
-  tfhe::client::lwe_encrypt(dim, key, noise_log2, seed, stream0, msgs, count, out);
-  return 0;
+  const tfhe_rng_key rk = tfhe::client::rng_key_from_seed(seed);
+  return tfhe_hip_lwe_encrypt_k(dim, key, noise_log2, &rk, stream0, msgs, count, out);
 }
 
 int tfhe_hip_lwe_phase(uint32_t dim, const uint64_t* key, const uint64_t* ct, size_t count, uint64_t* out) {
@@ -345,7 +650,7 @@ int tfhe_hip_lut_from_table(uint32_t N, uint32_t msg_modulus, const uint64_t* ta
   return 0;
 }
 
-int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out) {
+int tfhe_hip_create(const tfhe_params* p, const int* devices, int ndev, tfhe_ctx** out) {
   if (!out) return fail(TFHE_HIP_EINVAL, "create: null out");
   *out = nullptr;
   if (!params_valid(p)) return fail(TFHE_HIP_EINVAL, "create: invalid parameters");
@@ -355,127 +660,106 @@ int tfhe_hip_create(const tfhe_params* p, int device, tfhe_ctx** out) {
                 "FFT64) and P-FHEVM (k=1, N=2048, PBS 23x1, KS 4x4, KS->PBS; NTT or FFT64); got "
                 "k=%u N=%u pbs %ux%u ks %ux%u order %u transform %u",
                 p->k, p->N, p->pbs_base_log, p->pbs_level, p->ks_base_log, p->ks_level, p->order, p->transform);
-  int ndev = 0;
-  HIP_TRY(hipGetDeviceCount(&ndev));
-  if (device < 0 || device >= ndev) return fail(TFHE_HIP_EINVAL, "create: device %d of %d", device, ndev);
-  DeviceGuard g(device);
-  tfhe_ctx* c = new tfhe_ctx();
+  if (!devices || ndev < 1 || ndev > 64) return fail(TFHE_HIP_EINVAL, "create: need 1..64 device ordinals, got %d", ndev);
+  int count = 0;
+  HIP_TRY(hipGetDeviceCount(&count));
+  for (int i = 0; i < ndev; i++)
+    if (devices[i] < 0 || devices[i] >= count)
+      return fail(TFHE_HIP_EINVAL, "create: device %d of %d (devices[%d])", devices[i], count, i);
+  std::unique_ptr<tfhe_ctx> c(new tfhe_ctx());
   c->p = *p;
-  c->device = device;
-  c->lat_max = p->N == 2048 ? 512 : 1024;  // measured crossovers (tools/latency_sweep.py)
+  // measured latency-kernel crossovers (tools/latency_sweep.py, tools/latency_sweep_fft.sh): NTT engine
+  // 1024 (N = 1024) / 512 (N = 2048); FFT64 512 for both N (from the third round of latency workgroups
+  // on, workgroups that start staggered stream the BSK from L2 at different CMUX indices)
+  c->lat_max = is_fft(*p) ? 512 : p->N == 2048 ? 512 : 1024;
   {
     const char* e = getenv("TFHE_HIP_KS_VALU");
     c->ks_valu = e && e[0] == '1';
   }
-  auto cleanup = [&](int rc) {
-    tfhe_hip_destroy(c);
-    return rc;
-  };
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
-    return cleanup(fail(TFHE_HIP_EDEVICE, "create: hipStreamCreate failed"));
-  using namespace tfhe;
-  if (is_fft(*p)) {  // FFT64: twist / pass tables (pbs_fft.hip: make_fft_tables); latency kernel at N = 1024
-    // measured crossovers (tools/latency_sweep_fft.sh), 512 for both N: N = 1024 7.9 ms (latency, two
-    // rounds) vs 14.8 (batch) at B = 512, 20.9 vs 14.9 at 768 (from the third round on, workgroups that
-    // start staggered stream the BSK from L2 at different CMUX indices and fall out of L2); N = 2048
-    // 11.3 vs 15.3 ms at 512, 18.0 vs 17.5 at 640
-    c->lat_max = 512;
-    std::vector<double> tw(p->N == 2048 ? fft2k_tables_len() : fft_tables_len());
-    if (p->N == 2048) make_fft2k_tables(tw.data());
-    else make_fft_tables(tw.data());
-    if (hipMalloc(&c->d_tw, tw.size() * 8) != hipSuccess)
-      return cleanup(fail(TFHE_HIP_ENOMEM, "create: twiddle allocation failed"));
-    if (hipMemcpy(c->d_tw, tw.data(), tw.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
-      return cleanup(fail(TFHE_HIP_EDEVICE, "create: twiddle upload failed"));
-    *out = c;
-    return 0;
+  if (!is_fft(*p)) c->ninv = tfhe::gl_pow(p->N, tfhe::GL_P - 2);
+  c->sh.resize(ndev);
+  for (int i = 0; i < ndev; i++) c->sh[i].device = devices[i];
+  for (int i = 0; i < ndev; i++) {
+    const int rc = shard_init(c.get(), c->sh[i]);
+    if (rc) {
+      std::string m = g_err;
+      tfhe_hip_destroy(c.release());
+      return fail(rc, "create: shard %d (device %d): %s", i, devices[i], m.c_str());
+    }
   }
-  // twiddle tables of the device NTT layout (pbs_kernels.hip: make_ntt_tables)
-  const uint32_t N = p->N;
-  std::vector<u64> tw(N == 2048 ? ntt2048_tables_len() : 4 * N);
-  if (N == 2048) make_ntt2048_tables(canonical_psi(N), tw.data());
-  else make_ntt_tables(canonical_psi(N), tw.data());
-  c->ninv = gl_pow(N, GL_P - 2);
-  if (hipMalloc(&c->d_tw, tw.size() * 8) != hipSuccess)
-    return cleanup(fail(TFHE_HIP_ENOMEM, "create: twiddle allocation failed"));
-  if (hipMemcpy(c->d_tw, tw.data(), tw.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
-    return cleanup(fail(TFHE_HIP_EDEVICE, "create: twiddle upload failed"));
-  *out = c;
+  *out = c.release();
   return 0;
 }
 
 void tfhe_hip_destroy(tfhe_ctx* c) {
   if (!c) return;
-  {
-    DeviceGuard g(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (int w = 0; w < 3; w++)
-      for (auto e : c->ev[w]) (void)hipEventDestroy(e);
-    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
-    (void)hipFree(c->d_bsk);
-    (void)hipFree(c->d_ksk);
-    (void)hipFree(c->d_ks_planes);
-    (void)hipFree(c->d_ks_dig);
-    (void)hipFree(c->d_tw);
-    (void)hipFree(c->d_ms_zeros);
-    (void)hipFree(c->d_big);
-    (void)hipFree(c->d_stage);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
-  }
+  for (auto& s : c->sh) shard_free(s);
+  if (!c->comms.empty() && rccl().ok)
+    for (auto cm : c->comms)
+      if (cm) rccl().comm_destroy(cm);
   delete c;
 }
 
-int tfhe_hip_device(const tfhe_ctx* c) { return c ? c->device : -1; }
+int tfhe_hip_device(const tfhe_ctx* c) { return c && !c->sh.empty() ? c->sh[0].device : -1; }
+int tfhe_hip_ndev(const tfhe_ctx* c) { return c ? (int)c->sh.size() : 0; }
+int tfhe_hip_device_at(const tfhe_ctx* c, int i) {
+  return c && i >= 0 && i < (int)c->sh.size() ? c->sh[(size_t)i].device : -1;
+}
+int tfhe_hip_key_bcast_mode(const tfhe_ctx* c) { return c ? c->bcast_mode : -1; }
 
 static int load_keys_impl(tfhe_ctx* c, const uint64_t* bsk, size_t bsk_len, const uint64_t* ksk, size_t ksk_len,
-                          hipMemcpyKind kind) {
+                          bool from_host) {
   if (!c || !bsk || !ksk) return fail(TFHE_HIP_EINVAL, "load_keys: null argument");
   if (bsk_len != tfhe::client::bsk_len(c->p) || ksk_len != tfhe::client::ksk_len(c->p))
     return fail(TFHE_HIP_EINVAL, "load_keys: sizes %zu/%zu, expected %zu/%zu", bsk_len, ksk_len,
                 tfhe::client::bsk_len(c->p), tfhe::client::ksk_len(c->p));
   std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
   c->keys = false;
-  if (!c->d_bsk) HIP_TRY(hipMalloc(&c->d_bsk, bsk_len * 8));
-  if (!c->d_ksk) HIP_TRY(hipMalloc(&c->d_ksk, ksk_len * 8));
-  HIP_TRY(hipMemcpyAsync(c->d_ksk, ksk, ksk_len * 8, kind, c->stream));
-  if (!c->ks_valu) {  // byte planes of the KSK for the matrix-core keyswitch
-    const int big_dim = (int)(c->p.k * c->p.N);
-    if (!c->d_ks_planes)
-      HIP_TRY(hipMalloc(&c->d_ks_planes, tfhe::ks_planes_bytes(big_dim, (int)c->p.ks_level, (int)c->p.n)));
-    HIP_TRY(tfhe::launch_ksk_planes(c->d_ksk, big_dim, (int)c->p.ks_level, (int)c->p.n, c->d_ks_planes, c->stream));
+  c->bcast_mode = 0;
+  const size_t nd = c->sh.size();
+  // every shard: key buffers + a standard-domain BSK staging area (its d_stage)
+  for (auto& s : c->sh) {
+    DeviceGuard g(s.device);
+    if (s.ws_used) HIP_TRY(hipEventSynchronize(s.ws_free));
+    if (!s.d_bsk) HIP_TRY(hipMalloc(&s.d_bsk, bsk_len * 8));
+    if (!s.d_ksk) HIP_TRY(hipMalloc(&s.d_ksk, ksk_len * 8));
+    RC_TRY(grow(s, &s.d_stage, &s.stage_cap, bsk_len * 8));
   }
-  // standard-domain BSK staged in the workspace, converted in one launch
-  void* tmp = nullptr;
-  if (kind == hipMemcpyHostToDevice) {
-    int rc = grow(&c->d_stage, &c->stage_cap, bsk_len * 8);
-    if (rc) return rc;
-    tmp = c->d_stage;
-    HIP_TRY(hipMemcpyAsync(tmp, bsk, bsk_len * 8, kind, c->stream));
-  } else {
-    tmp = (void*)bsk;
+  shard& s0 = c->sh[0];
+  const u64* bsk0 = (const u64*)bsk;  // standard BSK on shard 0's device
+  {
+    DeviceGuard g(s0.device);
+    if (from_host) {
+      RC_TRY(upload_pinned(s0, s0.d_stage, bsk, bsk_len * 8));
+      RC_TRY(upload_pinned(s0, s0.d_ksk, ksk, ksk_len * 8));
+      bsk0 = (const u64*)s0.d_stage;
+    } else {
+      HIP_TRY(hipMemcpyAsync(s0.d_ksk, ksk, ksk_len * 8, hipMemcpyDeviceToDevice, s0.stream));
+      HIP_TRY(hipStreamSynchronize(s0.stream));
+    }
   }
-  const size_t polys = bsk_len / c->p.N;
-  if (is_fft(c->p) && c->p.N == 2048)
-    HIP_TRY(tfhe::launch_bsk_to_fourier2k((const u64*)tmp, (double*)c->d_bsk, polys, (const double*)c->d_tw, c->stream));
-  else if (is_fft(c->p))
-    HIP_TRY(tfhe::launch_bsk_to_fourier((const u64*)tmp, (double*)c->d_bsk, polys, (const double*)c->d_tw, c->stream));
-  else if (c->p.N == 2048)
-    HIP_TRY(tfhe::launch_bsk_to_ntt_2048((const u64*)tmp, c->d_bsk, polys, c->d_tw, c->ninv, c->stream));
-  else
-    HIP_TRY(tfhe::launch_bsk_to_ntt((const u64*)tmp, c->d_bsk, (int)(polys / 12), c->d_tw, c->ninv, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (nd > 1 || getenv("TFHE_HIP_BCAST")) {  // standard keys from shard 0 to every other shard, once
+    std::vector<u64*> dst_b(nd), dst_k(nd);
+    for (size_t i = 0; i < nd; i++) {
+      dst_b[i] = (u64*)c->sh[i].d_stage;
+      dst_k[i] = c->sh[i].d_ksk;
+    }
+    RC_TRY(broadcast(c, bsk0, dst_b, bsk_len));
+    RC_TRY(broadcast(c, s0.d_ksk, dst_k, ksk_len));
+  }
+  for (size_t i = 0; i < nd; i++)
+    RC_TRY(convert_keys(c, c->sh[i], i == 0 ? bsk0 : (const u64*)c->sh[i].d_stage, bsk_len));
   c->keys = true;
   return 0;
 }
 
 int tfhe_hip_load_keys(tfhe_ctx* c, const uint64_t* bsk, size_t bsk_len, const uint64_t* ksk, size_t ksk_len) {
-  return load_keys_impl(c, bsk, bsk_len, ksk, ksk_len, hipMemcpyHostToDevice);
+  return load_keys_impl(c, bsk, bsk_len, ksk, ksk_len, true);
 }
 
 int tfhe_hip_load_keys_device(tfhe_ctx* c, const uint64_t* d_bsk, size_t bsk_len, const uint64_t* d_ksk,
                               size_t ksk_len) {
-  return load_keys_impl(c, d_bsk, bsk_len, d_ksk, ksk_len, hipMemcpyDeviceToDevice);
+  return load_keys_impl(c, d_bsk, bsk_len, d_ksk, ksk_len, false);
 }
 
 int tfhe_hip_load_ms_key(tfhe_ctx* c, const uint64_t* zeros, uint32_t count, double bound, double r_sigma,
@@ -487,15 +771,18 @@ int tfhe_hip_load_ms_key(tfhe_ctx* c, const uint64_t* zeros, uint32_t count, dou
   if (count > 0x7FFFFFFF || !(bound >= 0) || !(r_sigma >= 0) || !(input_variance >= 0))
     return fail(TFHE_HIP_EINVAL, "load_ms_key: count %u / bound / r_sigma / variance out of range", count);
   std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  (void)hipFree(c->d_ms_zeros);
-  c->d_ms_zeros = nullptr;
   c->ms_count = 0;
-  if (!count) return 0;
   const size_t bytes = (size_t)count * (c->p.n + 1) * 8;
-  HIP_TRY(hipMalloc(&c->d_ms_zeros, bytes));
-  HIP_TRY(hipMemcpy(c->d_ms_zeros, zeros, bytes, hipMemcpyHostToDevice));
+  for (auto& s : c->sh) {
+    DeviceGuard g(s.device);
+    HIP_TRY(hipStreamSynchronize(s.stream));
+    if (s.ws_used) HIP_TRY(hipEventSynchronize(s.ws_free));
+    (void)hipFree(s.d_ms_zeros);
+    s.d_ms_zeros = nullptr;
+    if (!count) continue;
+    HIP_TRY(hipMalloc(&s.d_ms_zeros, bytes));
+    HIP_TRY(hipMemcpy(s.d_ms_zeros, zeros, bytes, hipMemcpyHostToDevice));
+  }
   c->ms_count = count;
   c->ms_bound = bound;
   c->ms_r_sigma = r_sigma;
@@ -509,15 +796,17 @@ int tfhe_hip_ms_reduce(tfhe_ctx* c, const uint64_t* in, size_t B, uint64_t* out,
   if (B == 0) return 0;
   if (B > 0x7FFFFFFF) return fail(TFHE_HIP_EINVAL, "ms_reduce: batch too large");
   std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
+  shard& s = c->sh[0];
+  DeviceGuard g(s.device);
   const size_t small = (size_t)c->p.n + 1;
+  RC_TRY(ws_begin(s, s.stream));
   std::vector<void*> d;
-  int rc = stage(c, {{in, B * small * 8}}, d, B * 4);
-  if (rc) return rc;
-  HIP_TRY(launch_ms(c, (u64*)d[0], B, (int*)d[1], c->stream));
-  HIP_TRY(hipMemcpyAsync(out, d[0], B * small * 8, hipMemcpyDeviceToHost, c->stream));
-  if (picks) HIP_TRY(hipMemcpyAsync(picks, d[1], B * 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  RC_TRY(stage(s, {{in, B * small * 8}}, d, B * 4));
+  HIP_TRY(launch_ms(c, s, (u64*)d[0], B, (int*)d[1], s.stream));
+  HIP_TRY(hipMemcpyAsync(out, d[0], B * small * 8, hipMemcpyDeviceToHost, s.stream));
+  if (picks) HIP_TRY(hipMemcpyAsync(picks, d[1], B * 4, hipMemcpyDeviceToHost, s.stream));
+  RC_TRY(ws_end(s, s.stream));
+  HIP_TRY(hipStreamSynchronize(s.stream));
   return 0;
 }
 
@@ -529,8 +818,21 @@ int tfhe_hip_pbs_async(tfhe_ctx* c, const uint64_t* d_in, size_t B, const uint64
   if (!d_in || !d_luts || !n_lut || !d_out) return fail(TFHE_HIP_EINVAL, "pbs: null buffer or n_lut == 0");
   if (B > 0x7FFFFFFF) return fail(TFHE_HIP_EINVAL, "pbs: batch too large");
   std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
-  return pbs_device(c, d_in, B, d_luts, n_lut, d_idx, d_out, stream == TFHE_HIP_NULL_STREAM ? (hipStream_t)0 : stream ? (hipStream_t)stream : c->stream);
+  size_t si = 0;
+  if (c->sh.size() > 1) {  // the shard whose device holds the input
+    hipPointerAttribute_t a;
+    HIP_TRY(hipPointerGetAttributes(&a, d_in));
+    si = c->sh.size();
+    for (size_t i = 0; i < c->sh.size() && si == c->sh.size(); i++)
+      if (c->sh[i].device == a.device) si = i;
+    if (si == c->sh.size()) return fail(TFHE_HIP_EINVAL, "pbs_async: input on device %d, no shard there", a.device);
+  }
+  shard& s = c->sh[si];
+  DeviceGuard g(s.device);
+  hipStream_t st = stream == TFHE_HIP_NULL_STREAM ? (hipStream_t)0 : stream ? (hipStream_t)stream : s.stream;
+  RC_TRY(ws_begin(s, st));
+  RC_TRY(pbs_device(c, s, d_in, B, d_luts, n_lut, d_idx, d_out, st));
+  return ws_end(s, st);
 }
 
 int tfhe_hip_pbs(tfhe_ctx* c, const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
@@ -539,21 +841,26 @@ int tfhe_hip_pbs(tfhe_ctx* c, const uint64_t* lwe_in, size_t B, const uint64_t* 
   if (!c->keys) return fail(TFHE_HIP_ENOKEYS, "pbs: keys not loaded");
   if (B == 0) return 0;
   if (!lwe_in || !luts || !n_lut || !lwe_out) return fail(TFHE_HIP_EINVAL, "pbs: null buffer or n_lut == 0");
+  if (B > 0x7FFFFFFF) return fail(TFHE_HIP_EINVAL, "pbs: batch too large");
   if (lut_index)
     for (size_t q = 0; q < B; q++)
       if (lut_index[q] >= n_lut) return fail(TFHE_HIP_EINVAL, "pbs: lut_index[%zu] = %u >= n_lut %zu", q, lut_index[q], n_lut);
   std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
   const size_t dim = io_dim(c->p) + 1;
-  std::vector<void*> d;
-  int rc = stage(c, {{lwe_in, B * dim * 8}, {luts, n_lut * c->p.N * 8}, {lut_index, lut_index ? B * 4 : 0}}, d,
-                 B * dim * 8);
-  if (rc) return rc;
-  rc = pbs_device(c, (const u64*)d[0], B, (const u64*)d[1], n_lut, (const u32*)d[2], (u64*)d[3], c->stream);
-  if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(lwe_out, d[3], B * dim * 8, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  return 0;
+  return for_each_slice(c, B, [&](size_t i, size_t lo, size_t hi) -> int {
+    shard& s = c->sh[i];
+    const size_t b = hi - lo;
+    RC_TRY(ws_begin(s, s.stream));
+    std::vector<void*> d;
+    RC_TRY(stage(s, {{lwe_in + lo * dim, b * dim * 8}, {luts, n_lut * c->p.N * 8},
+                     {lut_index ? lut_index + lo : nullptr, lut_index ? b * 4 : 0}},
+                 d, b * dim * 8));
+    RC_TRY(pbs_device(c, s, (const u64*)d[0], b, (const u64*)d[1], n_lut, (const u32*)d[2], (u64*)d[3], s.stream));
+    HIP_TRY(hipMemcpyAsync(lwe_out + lo * dim, d[3], b * dim * 8, hipMemcpyDeviceToHost, s.stream));
+    RC_TRY(ws_end(s, s.stream));
+    HIP_TRY(hipStreamSynchronize(s.stream));
+    return 0;
+  });
 }
 
 int tfhe_hip_blind_rotate(tfhe_ctx* c, const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
@@ -562,16 +869,21 @@ int tfhe_hip_blind_rotate(tfhe_ctx* c, const uint64_t* lwe_in, size_t B, const u
   if (!c->keys) return fail(TFHE_HIP_ENOKEYS, "blind_rotate: keys not loaded");
   if (B == 0) return 0;
   if (!lwe_in || !luts || !n_lut || !acc_out) return fail(TFHE_HIP_EINVAL, "blind_rotate: null buffer");
+  if (lut_index)
+    for (size_t q = 0; q < B; q++)
+      if (lut_index[q] >= n_lut) return fail(TFHE_HIP_EINVAL, "blind_rotate: lut_index[%zu] >= n_lut", q);
   std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
+  shard& s = c->sh[0];
+  DeviceGuard g(s.device);
   const size_t din = (size_t)c->p.n + 1, acc_len = (size_t)(c->p.k + 1) * c->p.N;
+  RC_TRY(ws_begin(s, s.stream));
   std::vector<void*> d;
-  int rc = stage(c, {{lwe_in, B * din * 8}, {luts, n_lut * c->p.N * 8}, {lut_index, lut_index ? B * 4 : 0}}, d,
-                 B * acc_len * 8);
-  if (rc) return rc;
-  HIP_TRY(launch_br(c, (const u64*)d[0], B, (const u64*)d[1], (const u32*)d[2], n_lut, nullptr, (u64*)d[3], c->stream));
-  HIP_TRY(hipMemcpyAsync(acc_out, d[3], B * acc_len * 8, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  RC_TRY(stage(s, {{lwe_in, B * din * 8}, {luts, n_lut * c->p.N * 8}, {lut_index, lut_index ? B * 4 : 0}}, d,
+               B * acc_len * 8));
+  HIP_TRY(launch_br(c, s, (const u64*)d[0], B, (const u64*)d[1], (const u32*)d[2], n_lut, nullptr, (u64*)d[3], s.stream));
+  HIP_TRY(hipMemcpyAsync(acc_out, d[3], B * acc_len * 8, hipMemcpyDeviceToHost, s.stream));
+  RC_TRY(ws_end(s, s.stream));
+  HIP_TRY(hipStreamSynchronize(s.stream));
   return 0;
 }
 
@@ -579,18 +891,20 @@ int tfhe_hip_sample_extract(tfhe_ctx* c, const uint64_t* acc, size_t B, uint64_t
   if (!c || (B && (!acc || !out))) return fail(TFHE_HIP_EINVAL, "sample_extract: bad arguments");
   if (B == 0) return 0;
   std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
+  shard& s = c->sh[0];
+  DeviceGuard g(s.device);
   const size_t acc_len = (size_t)(c->p.k + 1) * c->p.N, big = (size_t)c->p.k * c->p.N + 1;
+  RC_TRY(ws_begin(s, s.stream));
   std::vector<void*> d;
-  int rc = stage(c, {{acc, B * acc_len * 8}}, d, B * big * 8);
-  if (rc) return rc;
+  RC_TRY(stage(s, {{acc, B * acc_len * 8}}, d, B * big * 8));
   if (is_fft(c->p) && c->p.N == 2048)
-    HIP_TRY(tfhe::launch_sample_extract_torus2k((const u64*)d[0], B, (u64*)d[1], c->stream));
-  else if (is_fft(c->p)) HIP_TRY(tfhe::launch_sample_extract_torus((const u64*)d[0], B, (u64*)d[1], c->stream));
-  else if (c->p.N == 2048) HIP_TRY(tfhe::launch_sample_extract_2048((const u64*)d[0], B, (u64*)d[1], c->stream));
-  else HIP_TRY(tfhe::launch_sample_extract((const u64*)d[0], B, (u64*)d[1], c->stream));
-  HIP_TRY(hipMemcpyAsync(out, d[1], B * big * 8, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(tfhe::launch_sample_extract_torus2k((const u64*)d[0], B, (u64*)d[1], s.stream));
+  else if (is_fft(c->p)) HIP_TRY(tfhe::launch_sample_extract_torus((const u64*)d[0], B, (u64*)d[1], s.stream));
+  else if (c->p.N == 2048) HIP_TRY(tfhe::launch_sample_extract_2048((const u64*)d[0], B, (u64*)d[1], s.stream));
+  else HIP_TRY(tfhe::launch_sample_extract((const u64*)d[0], B, (u64*)d[1], s.stream));
+  HIP_TRY(hipMemcpyAsync(out, d[1], B * big * 8, hipMemcpyDeviceToHost, s.stream));
+  RC_TRY(ws_end(s, s.stream));
+  HIP_TRY(hipStreamSynchronize(s.stream));
   return 0;
 }
 
@@ -599,14 +913,16 @@ int tfhe_hip_keyswitch(tfhe_ctx* c, const uint64_t* in, size_t B, uint64_t* out)
   if (!c->keys) return fail(TFHE_HIP_ENOKEYS, "keyswitch: keys not loaded");
   if (B == 0) return 0;
   std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
+  shard& s = c->sh[0];
+  DeviceGuard g(s.device);
   const size_t big = (size_t)c->p.k * c->p.N + 1, small = (size_t)c->p.n + 1;
+  RC_TRY(ws_begin(s, s.stream));
   std::vector<void*> d;
-  int rc = stage(c, {{in, B * big * 8}}, d, B * small * 8);
-  if (rc) return rc;
-  HIP_TRY(launch_ks(c, (const u64*)d[0], B, (u64*)d[1], c->stream));
-  HIP_TRY(hipMemcpyAsync(out, d[1], B * small * 8, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  RC_TRY(stage(s, {{in, B * big * 8}}, d, B * small * 8));
+  RC_TRY(launch_ks(c, s, (const u64*)d[0], B, (u64*)d[1], s.stream));
+  HIP_TRY(hipMemcpyAsync(out, d[1], B * small * 8, hipMemcpyDeviceToHost, s.stream));
+  RC_TRY(ws_end(s, s.stream));
+  HIP_TRY(hipStreamSynchronize(s.stream));
   return 0;
 }
 
@@ -617,61 +933,59 @@ static int ntt_impl(tfhe_ctx* c, uint64_t* polys, size_t count, bool inverse) {
   for (size_t i = 0; i < count * c->p.N; i++)
     if (polys[i] >= tfhe::GL_P) return fail(TFHE_HIP_EINVAL, "ntt: value at %zu not reduced mod p", i);
   std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
+  shard& s = c->sh[0];
+  DeviceGuard g(s.device);
   const size_t bytes = count * c->p.N * 8;
+  RC_TRY(ws_begin(s, s.stream));
   std::vector<void*> d;
-  int rc = stage(c, {{polys, bytes}}, d, 0);
-  if (rc) return rc;
+  RC_TRY(stage(s, {{polys, bytes}}, d, 0));
   if (c->p.N == 2048) {
-    if (inverse) HIP_TRY(tfhe::launch_ntt2048_inv((u64*)d[0], count, c->d_tw, c->ninv, c->stream));
-    else HIP_TRY(tfhe::launch_ntt2048_fwd((u64*)d[0], count, c->d_tw, c->stream));
+    if (inverse) HIP_TRY(tfhe::launch_ntt2048_inv((u64*)d[0], count, s.d_tw, c->ninv, s.stream));
+    else HIP_TRY(tfhe::launch_ntt2048_fwd((u64*)d[0], count, s.d_tw, s.stream));
   } else {
-    if (inverse) HIP_TRY(tfhe::launch_ntt_inv((u64*)d[0], count, c->d_tw, c->ninv, c->stream));
-    else HIP_TRY(tfhe::launch_ntt_fwd((u64*)d[0], count, c->d_tw, c->stream));
+    if (inverse) HIP_TRY(tfhe::launch_ntt_inv((u64*)d[0], count, s.d_tw, c->ninv, s.stream));
+    else HIP_TRY(tfhe::launch_ntt_fwd((u64*)d[0], count, s.d_tw, s.stream));
   }
-  HIP_TRY(hipMemcpyAsync(polys, d[0], bytes, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpyAsync(polys, d[0], bytes, hipMemcpyDeviceToHost, s.stream));
+  RC_TRY(ws_end(s, s.stream));
+  HIP_TRY(hipStreamSynchronize(s.stream));
   return 0;
 }
 
 int tfhe_hip_ntt_fwd(tfhe_ctx* c, uint64_t* polys, size_t count) { return ntt_impl(c, polys, count, false); }
+int tfhe_hip_ntt_inv(tfhe_ctx* c, uint64_t* polys, size_t count) { return ntt_impl(c, polys, count, true); }
+
+static int fft_impl(tfhe_ctx* c, const void* in, size_t count, double* out, bool inverse) {
+  if (!c || (count && (!in || !out))) return fail(TFHE_HIP_EINVAL, "fft: bad arguments");
+  if (!is_fft(c->p)) return fail(TFHE_HIP_EUNSUPPORTED, "fft: ctx transform is not FFT64");
+  if (count == 0) return 0;
+  std::lock_guard<std::mutex> lk(c->mu);
+  shard& s = c->sh[0];
+  DeviceGuard g(s.device);
+  const size_t bytes = count * c->p.N * 8;
+  RC_TRY(ws_begin(s, s.stream));
+  std::vector<void*> d;
+  RC_TRY(stage(s, {{in, bytes}}, d, bytes));
+  const double* tw = (const double*)s.d_tw;
+  if (!inverse) {
+    if (c->p.N == 2048) HIP_TRY(tfhe::launch_fft2k_fwd((const u64*)d[0], count, (double*)d[1], tw, s.stream));
+    else HIP_TRY(tfhe::launch_fft_fwd((const u64*)d[0], count, (double*)d[1], tw, s.stream));
+  } else {
+    if (c->p.N == 2048) HIP_TRY(tfhe::launch_fft2k_inv((const double*)d[0], count, (double*)d[1], tw, s.stream));
+    else HIP_TRY(tfhe::launch_fft_inv((const double*)d[0], count, (double*)d[1], tw, s.stream));
+  }
+  HIP_TRY(hipMemcpyAsync(out, d[1], bytes, hipMemcpyDeviceToHost, s.stream));
+  RC_TRY(ws_end(s, s.stream));
+  HIP_TRY(hipStreamSynchronize(s.stream));
+  return 0;
+}
 
 int tfhe_hip_fft_fwd(tfhe_ctx* c, const uint64_t* polys, size_t count, double* out) {
-  if (!c || (count && (!polys || !out))) return fail(TFHE_HIP_EINVAL, "fft_fwd: bad arguments");
-  if (!is_fft(c->p)) return fail(TFHE_HIP_EUNSUPPORTED, "fft_fwd: ctx transform is not FFT64");
-  if (count == 0) return 0;
-  std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
-  const size_t bytes = count * c->p.N * 8;
-  std::vector<void*> d;
-  int rc = stage(c, {{polys, bytes}}, d, bytes);
-  if (rc) return rc;
-  if (c->p.N == 2048)
-    HIP_TRY(tfhe::launch_fft2k_fwd((const u64*)d[0], count, (double*)d[1], (const double*)c->d_tw, c->stream));
-  else HIP_TRY(tfhe::launch_fft_fwd((const u64*)d[0], count, (double*)d[1], (const double*)c->d_tw, c->stream));
-  HIP_TRY(hipMemcpyAsync(out, d[1], bytes, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  return 0;
+  return fft_impl(c, polys, count, out, false);
 }
-
 int tfhe_hip_fft_inv(tfhe_ctx* c, const double* in, size_t count, double* out) {
-  if (!c || (count && (!in || !out))) return fail(TFHE_HIP_EINVAL, "fft_inv: bad arguments");
-  if (!is_fft(c->p)) return fail(TFHE_HIP_EUNSUPPORTED, "fft_inv: ctx transform is not FFT64");
-  if (count == 0) return 0;
-  std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
-  const size_t bytes = count * c->p.N * 8;
-  std::vector<void*> d;
-  int rc = stage(c, {{in, bytes}}, d, bytes);
-  if (rc) return rc;
-  if (c->p.N == 2048)
-    HIP_TRY(tfhe::launch_fft2k_inv((const double*)d[0], count, (double*)d[1], (const double*)c->d_tw, c->stream));
-  else HIP_TRY(tfhe::launch_fft_inv((const double*)d[0], count, (double*)d[1], (const double*)c->d_tw, c->stream));
-  HIP_TRY(hipMemcpyAsync(out, d[1], bytes, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  return 0;
+  return fft_impl(c, in, count, out, true);
 }
-int tfhe_hip_ntt_inv(tfhe_ctx* c, uint64_t* polys, size_t count) { return ntt_impl(c, polys, count, true); }
 
 int tfhe_hip_nand(tfhe_ctx* c, const uint64_t* c1, const uint64_t* c2, size_t B, uint64_t* out) {
   if (!c || (B && (!c1 || !c2 || !out))) return fail(TFHE_HIP_EINVAL, "nand: bad arguments");
@@ -697,13 +1011,17 @@ int tfhe_hip_set_latency_batch(tfhe_ctx* c, size_t max_batch) {
 
 int tfhe_hip_sync(tfhe_ctx* c) {
   if (!c) return fail(TFHE_HIP_EINVAL, "sync: null ctx");
-  DeviceGuard g(c->device);
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (auto& s : c->sh) {
+    DeviceGuard g(s.device);
+    HIP_TRY(hipStreamSynchronize(s.stream));
+    if (s.ws_used) HIP_TRY(hipEventSynchronize(s.ws_free));
+  }
   return 0;
 }
 
 int tfhe_hip_timing_enable(tfhe_ctx* c, int enable) {
   if (!c) return fail(TFHE_HIP_EINVAL, "timing: null ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
   c->timing = enable != 0;
   return 0;
 }
@@ -711,26 +1029,29 @@ int tfhe_hip_timing_enable(tfhe_ctx* c, int enable) {
 int tfhe_hip_timing_reset(tfhe_ctx* c) {
   if (!c) return fail(TFHE_HIP_EINVAL, "timing: null ctx");
   std::lock_guard<std::mutex> lk(c->mu);
-  for (int w = 0; w < 3; w++) {
-    for (auto e : c->ev[w]) c->ev_pool.push_back(e);
-    c->ev[w].clear();
-  }
+  for (auto& s : c->sh)
+    for (int w = 0; w < 3; w++) {
+      for (auto e : s.ev[w]) s.ev_pool.push_back(e);
+      s.ev[w].clear();
+    }
   return 0;
 }
 
 int tfhe_hip_timing_stats(tfhe_ctx* c, int which, double* total_ms, int* launches) {
   if (!c || which < 0 || which > 2 || !total_ms || !launches) return fail(TFHE_HIP_EINVAL, "timing: bad arguments");
   std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
   double tot = 0;
   int cnt = 0;
-  auto& v = c->ev[which];
-  for (size_t i = 0; i + 1 < v.size(); i += 2) {
-    HIP_TRY(hipEventSynchronize(v[i + 1]));
-    float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, v[i], v[i + 1]));
-    tot += ms;
-    cnt++;
+  for (auto& s : c->sh) {
+    DeviceGuard g(s.device);
+    auto& v = s.ev[which];
+    for (size_t i = 0; i + 1 < v.size(); i += 2) {
+      HIP_TRY(hipEventSynchronize(v[i + 1]));
+      float ms = 0;
+      HIP_TRY(hipEventElapsedTime(&ms, v[i], v[i + 1]));
+      tot += ms;
+      cnt++;
+    }
   }
   *total_ms = tot;
   *launches = cnt;

@@ -7,7 +7,9 @@
 // the Gaussian sampler uses only IEEE + - * / sqrt, so keys are bit-identical on every host.
 #include <math.h>
 #include <stdint.h>
+#include <errno.h>
 #include <string.h>
+#include <sys/random.h>
 
 #include <algorithm>
 #include <thread>
@@ -39,19 +41,45 @@ static void parallel_for(int64_t count, F&& f) {
 }
 
 // ---------------------------------------------------------------- ChaCha20 (RFC 8439) stream
+// A 64-bit seed maps to the rng key (seed, "tfhe-amd chacha!"): the reproducible streams that tests,
+// golden vectors and the oracle use.  Production keys / encryptions take 192 bits of OS entropy
+// instead (rng_key_entropy), so nothing about them follows from public constants.
+tfhe_rng_key rng_key_from_seed(uint64_t seed) {
+  static const uint8_t tag[16] = {'t', 'f', 'h', 'e', '-', 'a', 'm', 'd', ' ', 'c', 'h', 'a', 'c', 'h', 'a', '!'};
+  tfhe_rng_key k;
+  k.w[0] = (uint32_t)seed;
+  k.w[1] = (uint32_t)(seed >> 32);
+  memcpy(&k.w[2], tag, 16);
+  return k;
+}
+
+bool rng_key_entropy(tfhe_rng_key* k) {
+  uint8_t* p = (uint8_t*)k->w;
+  size_t got = 0;
+  while (got < sizeof(k->w)) {
+    const ssize_t r = getrandom(p + got, sizeof(k->w) - got, 0);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    got += (size_t)r;
+  }
+  return true;
+}
+
 struct ChaCha {
   uint32_t key[8];
   uint32_t ctr = 0;
   uint32_t buf[16];
   int pos = 16;
 
-  ChaCha(uint64_t seed, uint64_t stream) {
-    static const uint8_t tag[16] = {'t', 'f', 'h', 'e', '-', 'a', 'm', 'd', ' ', 'c', 'h', 'a', 'c', 'h', 'a', '!'};
-    key[0] = (uint32_t)seed;
-    key[1] = (uint32_t)(seed >> 32);
+  // key words 0, 1, 4..7 = the 192-bit rng key, words 2, 3 = the stream index
+  ChaCha(const tfhe_rng_key& rk, uint64_t stream) {
+    key[0] = rk.w[0];
+    key[1] = rk.w[1];
     key[2] = (uint32_t)stream;
     key[3] = (uint32_t)(stream >> 32);
-    for (int i = 0; i < 4; i++) memcpy(&key[4 + i], tag + 4 * i, 4);
+    for (int i = 0; i < 4; i++) key[4 + i] = rk.w[2 + i];
   }
   static inline uint32_t rl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
   void refill() {
@@ -169,25 +197,25 @@ static void lwe_one(uint32_t dim, const uint64_t* key, int32_t noise_log2, ChaCh
   out[dim] = acc + m;
 }
 
-void keygen(const tfhe_params& p, uint64_t seed, uint64_t* lwe_key, uint64_t* glwe_key, uint64_t* bsk,
+void keygen(const tfhe_params& p, const tfhe_rng_key& rk, uint64_t* lwe_key, uint64_t* glwe_key, uint64_t* bsk,
             uint64_t* ksk) {
   {
-    ChaCha r(seed, 1);
+    ChaCha r(rk, 1);
     for (uint32_t i = 0; i < p.n; i++) lwe_key[i] = r.next() & 1;
   }
   {
-    ChaCha r(seed, 2);
+    ChaCha r(rk, 2);
     for (uint32_t i = 0; i < p.k * p.N; i++) glwe_key[i] = r.next() & 1;
   }
-  server_keygen(p, seed, lwe_key, glwe_key, bsk, ksk);
+  server_keygen(p, rk, lwe_key, glwe_key, bsk, ksk);
 }
 
-void server_keygen(const tfhe_params& p, uint64_t seed, const uint64_t* lwe_key, const uint64_t* glwe_key,
+void server_keygen(const tfhe_params& p, const tfhe_rng_key& rk, const uint64_t* lwe_key, const uint64_t* glwe_key,
                    uint64_t* bsk, uint64_t* ksk) {
   if (bsk) {
     const size_t row = (size_t)(p.k + 1) * p.N, per_i = (size_t)(p.k + 1) * p.pbs_level * row;
     parallel_for((int64_t)p.n, [&](int64_t i) {
-      ChaCha r(seed, 0x1000 + (uint64_t)i);
+      ChaCha r(rk, 0x1000 + (uint64_t)i);
       for (uint32_t c = 0; c <= p.k; c++)
         for (uint32_t l = 0; l < p.pbs_level; l++) {
           uint64_t* out = bsk + per_i * i + row * (c * p.pbs_level + l);
@@ -205,7 +233,7 @@ void server_keygen(const tfhe_params& p, uint64_t seed, const uint64_t* lwe_key,
   if (ksk) {
     const size_t per_j = (size_t)p.ks_level * (p.n + 1);
     parallel_for((int64_t)(p.k * p.N), [&](int64_t j) {
-      ChaCha r(seed, 0x100000 + (uint64_t)j);
+      ChaCha r(rk, 0x100000 + (uint64_t)j);
       for (uint32_t l = 0; l < p.ks_level; l++)
         lwe_one(p.n, lwe_key, p.lwe_noise_log2, r, glwe_key[j] << (64 - p.ks_base_log * (l + 1)),
                 ksk + per_j * j + (size_t)l * (p.n + 1));
@@ -214,17 +242,17 @@ void server_keygen(const tfhe_params& p, uint64_t seed, const uint64_t* lwe_key,
 }
 
 // modulus-switch zeros of the P-FHEVM server key: zero z on ChaCha stream 0x200000 + z
-void ms_zeros_keygen(const tfhe_params& p, uint64_t seed, const uint64_t* lwe_key, uint32_t count, uint64_t* zeros) {
+void ms_zeros_keygen(const tfhe_params& p, const tfhe_rng_key& rk, const uint64_t* lwe_key, uint32_t count, uint64_t* zeros) {
   parallel_for((int64_t)count, [&](int64_t z) {
-    ChaCha r(seed, 0x200000 + (uint64_t)z);
+    ChaCha r(rk, 0x200000 + (uint64_t)z);
     lwe_one(p.n, lwe_key, p.lwe_noise_log2, r, 0, zeros + (size_t)z * (p.n + 1));
   });
 }
 
-void lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, uint64_t seed, uint64_t stream0,
+void lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, const tfhe_rng_key& rk, uint64_t stream0,
                  const uint64_t* msgs, size_t count, uint64_t* out) {
   auto one = [&](int64_t q) {
-    ChaCha r(seed, stream0 + (uint64_t)q);
+    ChaCha r(rk, stream0 + (uint64_t)q);
     lwe_one(dim, key, noise_log2, r, msgs[q], out + (size_t)q * (dim + 1));
   };
   if (count > 256) parallel_for((int64_t)count, one);
@@ -285,16 +313,16 @@ static void glwe_native(uint32_t k, uint32_t N, const uint64_t* key, int32_t noi
 }
 
 // output GLWE key from ChaCha stream 4, PKSK row j from stream 0x300000 + j
-void pks_keygen(const tfhe_pks_params& pp, uint64_t seed, const uint64_t* in_key, uint64_t* out_key, uint64_t* pksk) {
+void pks_keygen(const tfhe_pks_params& pp, const tfhe_rng_key& rk, const uint64_t* in_key, uint64_t* out_key, uint64_t* pksk) {
   const uint32_t k = pp.out_k, N = pp.out_N;
   {
-    ChaCha r(seed, 4);
+    ChaCha r(rk, 4);
     for (uint32_t i = 0; i < k * N; i++) out_key[i] = r.next() & 1;
   }
   if (!pksk) return;
   const size_t row = (size_t)(k + 1) * N;
   parallel_for((int64_t)pp.in_dim, [&](int64_t j) {
-    ChaCha r(seed, 0x300000 + (uint64_t)j);
+    ChaCha r(rk, 0x300000 + (uint64_t)j);
     std::vector<uint64_t> m(N, 0);
     for (uint32_t l = 0; l < pp.level; l++) {
       m[0] = in_key[j] << (64 - pp.base_log * (l + 1));
@@ -412,10 +440,10 @@ static u128 sns_gadget(uint32_t shift) {
 }
 
 // GLWE key from ChaCha stream 5; BSK row i from stream 0x400000 + i; layout [i][c*L+l][j][prime][N]
-void sns_keygen(const tfhe_sns_params& sp, uint64_t seed, const uint64_t* lwe_key, uint64_t* glwe_key, uint64_t* bsk) {
+void sns_keygen(const tfhe_sns_params& sp, const tfhe_rng_key& rk, const uint64_t* lwe_key, uint64_t* glwe_key, uint64_t* bsk) {
   const uint32_t k = sp.k, N = sp.N, L = sp.level;
   {
-    ChaCha r(seed, 5);
+    ChaCha r(rk, 5);
     for (uint32_t i = 0; i < k * N; i++) glwe_key[i] = r.next() & 1;
   }
   if (!bsk) return;
@@ -427,7 +455,7 @@ void sns_keygen(const tfhe_sns_params& sp, uint64_t seed, const uint64_t* lwe_ke
     }
   const size_t row = (size_t)(k + 1) * 2 * N, per_i = (size_t)(k + 1) * L * row;
   parallel_for((int64_t)sp.n, [&](int64_t i) {
-    ChaCha r(seed, 0x400000 + (uint64_t)i);
+    ChaCha r(rk, 0x400000 + (uint64_t)i);
     std::vector<uint64_t> tmp(N), acc(N);
     std::vector<int64_t> e(N);
     for (uint32_t c = 0; c <= k; c++)

@@ -127,7 +127,7 @@ int tfhe_hip_pks_keygen(const tfhe_pks_params* pp, uint64_t seed, const uint64_t
   if (!pks_valid(pp) || !in_key || !out_key) return fail(TFHE_HIP_EINVAL, "pks_keygen: bad arguments");
   for (uint32_t j = 0; j < pp->in_dim; j++)
     if (in_key[j] > 1) return fail(TFHE_HIP_EINVAL, "pks_keygen: in_key[%u] is not binary", j);
-  tfhe::client::pks_keygen(*pp, seed, in_key, out_key, pksk);
+  tfhe::client::pks_keygen(*pp, tfhe::client::rng_key_from_seed(seed), in_key, out_key, pksk);
   return 0;
 }
 

@@ -165,7 +165,7 @@ int tfhe_hip_sns_keygen(const tfhe_sns_params* sp, uint64_t seed, const uint64_t
   if (!sns_valid(sp) || !lwe_key || !glwe_key) return fail(TFHE_HIP_EINVAL, "sns_keygen: bad arguments");
   for (uint32_t i = 0; i < sp->n; i++)
     if (lwe_key[i] > 1) return fail(TFHE_HIP_EINVAL, "sns_keygen: lwe_key[%u] is not binary", i);
-  tfhe::client::sns_keygen(*sp, seed, lwe_key, glwe_key, bsk);
+  tfhe::client::sns_keygen(*sp, tfhe::client::rng_key_from_seed(seed), lwe_key, glwe_key, bsk);
   return 0;
 }
 

@@ -28,7 +28,7 @@ that fill the GPU use the ripple adder (XOR3 + MAJ per bit, fewest PBS).
 """
 from __future__ import annotations
 
-from typing import Generator, List, Sequence, Union
+from typing import Generator, List, Optional, Sequence, Union
 
 import numpy as np
 
@@ -349,7 +349,7 @@ class FheUint:
         return ((v[:, None] >> np.arange(width, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
 
     @classmethod
-    def encrypt(cls, circuit: Circuit, ck: ClientKey, values, width: int, seed: int = 1,
+    def encrypt(cls, circuit: Circuit, ck: ClientKey, values, width: int, seed: Optional[int] = None,
                 stream0: int = 0) -> "FheUint":
         b = cls._bits_of(values, width)
         ct = ck.encrypt_bool(b.reshape(-1), seed, stream0).reshape(b.shape[0], width, -1)

@@ -170,8 +170,12 @@ def compact_public_key_noise(mask: np.ndarray, body: np.ndarray, pke_key: np.nda
     return int(np.abs(e.astype(object)).max())
 
 
-def to_engine_keys(tk: TfhersClientKey, seed: int = 0x7F4E0001, with_server_key: bool = True):
-    """(ClientKey, ServerKey) of this engine over the ingested secret keys (P-FHEVM preset, checked)."""
+def to_engine_keys(tk: TfhersClientKey, seed=None, with_server_key: bool = True):
+    """(ClientKey, ServerKey) of this engine over the ingested secret keys (P-FHEVM preset, checked).
+
+    The server-key randomness (BSK / KSK masks and noise, the modulus-switch zeros) comes from 192 bits of
+    OS entropy unless a test seed is given: with a public seed anyone holding the published evaluation
+    keys could regenerate every mask and noise term and solve the KSK rows for the secret key."""
     import tfhe_amd
     p = tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM)
     P = tk.params

@@ -20,7 +20,7 @@ plaintext right operands, mixed widths zero-extended.
 """
 from __future__ import annotations
 
-from typing import Callable, Dict, List, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -177,7 +177,7 @@ class RadixUint:
         return (v[:, None] >> (2 * np.arange(w // 2, dtype=np.uint64))[None, :]) & np.uint64(3)
 
     @classmethod
-    def encrypt(cls, c: RadixCircuit, ck, values, w: int, seed: int = 1, stream0: int = 0) -> "RadixUint":
+    def encrypt(cls, c: RadixCircuit, ck, values, w: int, seed: Optional[int] = None, stream0: int = 0) -> "RadixUint":
         d = cls._digits(values, w)
         ct = ck.encrypt(d.reshape(-1), SPACE, seed, stream0).reshape(d.shape + (-1,))
         return cls(c, ct)
