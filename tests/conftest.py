@@ -105,3 +105,25 @@ def fhevm_fft_engine(fhevm_fft_keys):
     eng.load_keys(sk)
     yield eng
     eng.close()
+
+
+# ---- fhEVM operator KATs (tests/golden/fhevm_kats.json: clear values stored as decimal strings) ----------
+KATS_PATH = os.path.join(ROOT, "tests", "golden", "fhevm_kats.json")
+
+
+def load_kats(max_width: int = 256):
+    """The reference's 2,394 fhEVM KATs with args / expect as Python ints; max_width drops overloads
+    wider than that (operand or result type)."""
+    import json
+
+    def width(t):
+        return 1 if t == "ebool" else int(t.lstrip("e").replace("uint", ""))
+
+    with open(KATS_PATH) as f:
+        kats = json.load(f)
+    out = []
+    for k in kats:
+        if max(width(t) for t in k["types"] + [k["result_type"]]) > max_width:
+            continue
+        out.append(dict(k, args=[int(a) for a in k["args"]], expect=int(k["expect"])))
+    return out

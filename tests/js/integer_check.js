@@ -9,11 +9,14 @@ const kats = require(path.join(__dirname, '..', 'golden', 'fhevm_kats.json'));
 
 const HALF = 1n << 63n;
 let minMargin = 1n << 62n;
+// trivial ciphertexts: the mask width does not matter, so the double runs at n = 0 (body only) to keep
+// the euint128 multiplier levels (~10^6 gates) in memory
+const D = 1;
 const engine = {
-  params: { n: 630 },
+  params: { n: D - 1 },
   gateLut() { return null; },
   async pbs(cts) {
-    const d = 631;
+    const d = D;
     const out = new BigUint64Array(cts.length);
     for (let i = 0; i < cts.length; i += d) {
       for (let j = 0; j < d - 1; j++) assert.strictEqual(cts[i + j], 0n, 'trivial ciphertexts only');
@@ -27,7 +30,7 @@ const engine = {
     return out;
   },
 };
-const clearKey = { decryptBool(col) { const r = []; for (let i = 630; i < col.length; i += 631) r.push(col[i] !== 0n && col[i] < HALF); return r; } };
+const clearKey = { decryptBool(col) { const r = []; for (let i = D - 1; i < col.length; i += D) r.push(col[i] !== 0n && col[i] < HALF); return r; } };
 const width = (t) => (t === 'ebool' ? 1 : Number(t.replace('euint', '').replace('uint', '')));
 
 (async () => {
@@ -40,9 +43,9 @@ const width = (t) => (t === 'ebool' ? 1 : Number(t.replace('euint', '').replace(
   let bad = 0;
   kats.forEach((k, i) => {
     let got;
-    if (k.result_type === 'ebool') got = clearKey.decryptBool(res[i])[0] ? 1 : 0;
-    else got = Number(res[i].decrypt(clearKey)[0]);
-    const want = k.result_type === 'ebool' ? (k.expect ? 1 : 0) : k.expect;
+    if (k.result_type === 'ebool') got = clearKey.decryptBool(res[i])[0] ? 1n : 0n;
+    else got = res[i].decrypt(clearKey)[0];
+    const want = k.result_type === 'ebool' ? (BigInt(k.expect) ? 1n : 0n) : BigInt(k.expect);
     if (got !== want) { bad++; if (bad < 5) console.error('KAT mismatch', k.source, k.op, k.types, k.args, want, got); }
   });
   assert.strictEqual(bad, 0, `${bad} KATs failed`);

@@ -1,7 +1,7 @@
 """fhEVM operator KATs replayed on the MI355X (message-level parity).
 
-Every KAT of the reference's tests/fhevm-suite/e2e/test/fhevmOperations*.ts for ebool / euint8 /
-euint16 / euint32 overloads (936, fixture tests/golden/fhevm_kats.json) is encrypted under the
+Every KAT of the reference's tests/fhevm-suite/e2e/test/fhevmOperations*.ts -- all 2,394 overloads,
+ebool and euint8 .. euint256 (fixture tests/golden/fhevm_kats.json) -- is encrypted under the
 P-GATE key, evaluated by tfhe_amd.integer through the GPU gate bootstrap (libtfhe_hip.so) — all
 KATs in lockstep, one PBS launch per circuit level — and decrypted.  Expected values are the
 reference's own `expect(res).to.equal(...)` constants.
@@ -27,8 +27,9 @@ def _width(t):
 def test_fhevm_kats_gpu(request, transform):
     engine = request.getfixturevalue("engine" if transform == "ntt" else "gate_fft_engine")
     ck, _ = request.getfixturevalue("product_keys" if transform == "ntt" else "gate_fft_keys")
-    with open(GOLDEN) as f:
-        kats = json.load(f)
+    from conftest import load_kats
+    kats = load_kats()
+    assert len(kats) == 2394
     c = I.Circuit(engine)
     ops, stream = [], 0
     for k in kats:

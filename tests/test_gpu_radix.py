@@ -1,6 +1,6 @@
 """Radix integers (tfhe_amd/radix.py) on the MI355X at the production fhEVM parameters: every
-reference fhEVM operator KAT (all 936, div/rem included), encrypted under the P-FHEVM key, evaluated
-in lockstep (one multi-LUT PBS launch per circuit level) and decrypted."""
+reference fhEVM operator KAT (all 2,394: ebool .. euint256, div/rem included), encrypted under the
+P-FHEVM key, evaluated in lockstep (one multi-LUT PBS launch per circuit level) and decrypted."""
 import json
 import os
 
@@ -8,7 +8,8 @@ import numpy as np
 import pytest
 
 from tfhe_amd import radix as R
-from test_radix import GOLDEN, _w, supported
+from conftest import load_kats
+from test_radix import _w, supported
 
 pytestmark = pytest.mark.gpu
 
@@ -17,8 +18,8 @@ pytestmark = pytest.mark.gpu
 def test_radix_kats_gpu(request, transform):
     fhevm_engine = request.getfixturevalue("fhevm_engine" if transform == "ntt" else "fhevm_fft_engine")
     ck, _ = request.getfixturevalue("fhevm_keys" if transform == "ntt" else "fhevm_fft_keys")
-    with open(GOLDEN) as f:
-        kats = [k for k in json.load(f) if supported(k)]
+    kats = [k for k in load_kats() if supported(k)]
+    assert len(kats) == 2394
     c = R.RadixCircuit(fhevm_engine)
     ops, stream = [], 0
     for k in kats:

@@ -66,8 +66,9 @@ def _run_plain(script, *args, timeout=600):
 
 
 def test_js_integer_kats_cpu():
-    """js/integer.js replays all 936 fhEVM KATs (cleartext test double; same 27 launches as Python)."""
-    assert _run_plain("integer_check.js").startswith("OK 936 KATs, 27 launches")
+    """js/integer.js replays all 2,394 fhEVM KATs (ebool .. euint256; cleartext test double; the same
+    27 launches as Python)."""
+    assert _run_plain("integer_check.js").startswith("OK 2394 KATs, 27 launches")
 
 
 def test_js_radix_kats_cpu():
@@ -75,10 +76,10 @@ def test_js_radix_kats_cpu():
     tfhe_amd/radix.py (tests/test_radix.py) — the two layers build identical circuits."""
     import sys
     sys.path.insert(0, os.path.dirname(__file__))
-    from test_radix import GOLDEN, CleartextRadixCircuit, kat_op, supported
-    with open(GOLDEN) as f:
-        kats = [k for k in json.load(f) if supported(k)]
-    c = CleartextRadixCircuit()
+    from conftest import load_kats
+    from test_radix import CleartextRadixCircuit, kat_op, supported
+    kats = [k for k in load_kats() if supported(k)]
+    c = CleartextRadixCircuit(N=16)
     c.run_many([kat_op(c, k) for k in kats])
     assert _run_plain("radix_check.js") == f"OK {len(kats)} {c.launches} {c.pbs_count}"
 

@@ -35,7 +35,8 @@ import numpy as np
 from . import MU, ClientKey, Engine
 
 _M64 = 1 << 64
-WIDTHS = (8, 16, 32)
+MAX_LAUNCH = 1 << 19  # ciphertexts per engine call (P-GATE: 2 x 631 x 8 B x 512 Ki = 5.3 GB of I/O)
+WIDTHS = (8, 16, 32, 64, 128, 160, 256)   # ebool / euint* / eaddress of fhEVM (any width works)
 
 
 # --------------------------------------------------------------------------------------------
@@ -107,7 +108,9 @@ class Circuit:
         flat = np.concatenate([l.reshape(-1, self.dim) for l in lins], axis=0) if lins else \
             np.zeros((0, self.dim), np.uint64)
         if flat.shape[0]:
-            out = self.engine.pbs(flat, self.lut)
+            # one level = one launch, in chunks of MAX_LAUNCH ciphertexts (euint128 mul levels reach ~10^6)
+            outs = [self.engine.pbs(flat[o:o + MAX_LAUNCH], self.lut) for o in range(0, flat.shape[0], MAX_LAUNCH)]
+            out = outs[0] if len(outs) == 1 else np.concatenate(outs, axis=0)
             self.pbs_count += flat.shape[0]
             self.launches += 1
         else:
@@ -291,7 +294,7 @@ def g_div_rem_scalar(c: Circuit, a: np.ndarray, d: int) -> Op:
     for i in range(w - L, -1, -1):
         R = np.concatenate([a[:, i:i + 1], R], axis=1)         # (R << 1) | a_i  : L..w bits
         r = R.shape[1]
-        dbits = c.trivial(np.broadcast_to(((d >> np.arange(r)) & 1).astype(bool), (B, r)))
+        dbits = c.trivial(np.broadcast_to(np.array([(d >> j) & 1 for j in range(r)], dtype=bool), (B, r)))
         t, ge = yield from g_add(c, R, NOT(dbits), True, want_sum=True, want_carry=True)
         q[:, i] = ge
         R = yield from g_select(ge, t, R)
@@ -345,8 +348,12 @@ class FheUint:
 
     @staticmethod
     def _bits_of(values, width: int) -> np.ndarray:
-        v = np.atleast_1d(np.asarray(values, dtype=np.uint64))
-        return ((v[:, None] >> np.arange(width, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
+        """(B, width) bool, LSB first; values are ints of any size (euint64/128/256 and wider)."""
+        if width <= 64:
+            v = np.atleast_1d(np.asarray(values, dtype=np.uint64))
+            return ((v[:, None] >> np.arange(width, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
+        vs = [int(x) for x in np.atleast_1d(np.asarray(values, dtype=object))]
+        return np.array([[(x >> j) & 1 for j in range(width)] for x in vs], dtype=bool).reshape(len(vs), width)
 
     @classmethod
     def encrypt(cls, circuit: Circuit, ck: ClientKey, values, width: int, seed: Optional[int] = None,
@@ -404,9 +411,13 @@ class FheUint:
 
 
 def decrypt_bits(ck: ClientKey, bits: np.ndarray) -> np.ndarray:
+    """(B,) uint64 for w <= 64; an object array of Python ints for wider values."""
     B, w = bits.shape[0], bits.shape[1]
-    b = ck.decrypt_bool(bits.reshape(-1, bits.shape[-1])).reshape(B, w).astype(np.uint64)
-    return (b << np.arange(w, dtype=np.uint64)[None, :]).sum(axis=1).astype(np.uint64)
+    b = ck.decrypt_bool(bits.reshape(-1, bits.shape[-1])).reshape(B, w)
+    if w <= 64:
+        b = b.astype(np.uint64)
+        return (b << np.arange(w, dtype=np.uint64)[None, :]).sum(axis=1).astype(np.uint64)
+    return np.array([sum(1 << j for j in range(w) if row[j]) for row in b], dtype=object)
 
 
 BINARY_OPS = ("add", "sub", "mul", "div", "rem", "and", "or", "xor", "shl", "shr", "rotl", "rotr",
@@ -449,7 +460,7 @@ def fhevm_op(c: Circuit, op: str, lhs, rhs=None) -> Op:
 
     def bits(x):
         return x.cast(w).bits if isinstance(x, FheUint) else c.trivial(
-            np.broadcast_to(FheUint._bits_of(np.full(B, int(x) % (1 << w), dtype=np.uint64), w), (B, w)))
+            np.broadcast_to(FheUint._bits_of([int(x) % (1 << w)], w), (B, w)))
 
     if op == "mul":
         if not l_enc:

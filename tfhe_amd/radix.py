@@ -39,6 +39,9 @@ def _biv(f: Callable[[int, int], int]) -> Tuple[int, ...]:
     return _table(lambda v: f(v // MSG, v % MSG))
 
 
+MAX_LAUNCH = 1 << 18  # ciphertexts per engine call (P-FHEVM: 2 x 2049 x 8 B x 256 Ki = 8.6 GB of I/O)
+
+
 class RadixCircuit:
     """Lockstep executor: each level is a list of (lin array (..., dim+1), table) pairs; every
     distinct table becomes one LUT of the launch and each ciphertext indexes its own."""
@@ -82,7 +85,12 @@ class RadixCircuit:
             flat_parts.append(a.reshape(cnt, self.dim))
             idx_parts.append(np.full(cnt, index[t], dtype=np.uint32))
         flat = np.concatenate(flat_parts, axis=0)
-        out = self._pbs(flat, tables, np.concatenate(idx_parts))
+        idx = np.concatenate(idx_parts)
+        # one level = one launch; levels of wide operators (euint128 mul: ~10^5 PBS per operand pair) go in
+        # chunks of MAX_LAUNCH ciphertexts so host and device staging stay bounded
+        outs = [self._pbs(flat[o:o + MAX_LAUNCH], tables, idx[o:o + MAX_LAUNCH])
+                for o in range(0, flat.shape[0], MAX_LAUNCH)]
+        out = outs[0] if len(outs) == 1 else np.concatenate(outs, axis=0)
         self.pbs_count += flat.shape[0]
         self.launches += 1
         res, off = [], 0
@@ -173,8 +181,12 @@ class RadixUint:
 
     @staticmethod
     def _digits(values, w):
-        v = np.atleast_1d(np.asarray(values, dtype=np.uint64))
-        return (v[:, None] >> (2 * np.arange(w // 2, dtype=np.uint64))[None, :]) & np.uint64(3)
+        """(B, w/2) base-4 digits, least significant first; values are ints of any size."""
+        if w <= 64:
+            v = np.atleast_1d(np.asarray(values, dtype=np.uint64))
+            return (v[:, None] >> (2 * np.arange(w // 2, dtype=np.uint64))[None, :]) & np.uint64(3)
+        vs = [int(x) for x in np.atleast_1d(np.asarray(values, dtype=object))]
+        return np.array([[(x >> (2 * j)) & 3 for j in range(w // 2)] for x in vs], dtype=np.uint64).reshape(len(vs), w // 2)
 
     @classmethod
     def encrypt(cls, c: RadixCircuit, ck, values, w: int, seed: Optional[int] = None, stream0: int = 0) -> "RadixUint":
@@ -190,8 +202,8 @@ class RadixUint:
         B, nb = self.blocks.shape[:2]
         d = ck.decrypt(self.blocks.reshape(B * nb, -1), SPACE).reshape(B, nb).astype(object)
         w = self.width
-        return np.array([sum(int(d[i, j]) << (2 * j) for j in range(nb)) % (1 << w) for i in range(B)],
-                        dtype=np.uint64)
+        vals = [sum(int(d[i, j]) << (2 * j) for j in range(nb)) % (1 << w) for i in range(B)]
+        return np.array(vals, dtype=np.uint64 if w <= 64 else object)
 
     def cast(self, w: int) -> "RadixUint":
         nb = w // 2
