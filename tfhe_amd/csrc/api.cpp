@@ -520,6 +520,16 @@ int for_each_slice(tfhe_ctx* c, size_t B, F&& fn) {
 
 }  // namespace
 
+#if F2_STAMPS
+namespace tfhe {
+hipError_t read_fft2k_stamps(unsigned long long* out);
+}
+// diagnostic builds only (-DF2_STAMPS=1): the P-FHEVM batch kernel's phase stamps (tools/stamps.py)
+extern "C" int tfhe_hip_debug_fft2k_stamps(unsigned long long* out) {
+  return tfhe::read_fft2k_stamps(out) == hipSuccess ? 0 : TFHE_HIP_EDEVICE;
+}
+#endif
+
 // error slot shared with pks_api.cpp / sns_api.cpp
 int tfhe_hip_set_error(int code, const char* msg) {
   g_err = msg;

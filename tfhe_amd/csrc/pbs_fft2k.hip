@@ -51,6 +51,27 @@ __device__ __forceinline__ int decomp_23x1_hi(u32 hi) {
   return (int)((st + 0x3FFFFFu) & 0x7FFFFFu) - 0x3FFFFF;
 }
 
+// The pair exchanges' barriers (workgroup-wide s_barrier; the two waves of a pair need each other's
+// LDS writes).  Diagnostic builds (-DF2_STAMPS=1) also sum the cycles waves spend in them.
+#ifndef F2_STAMPS
+#define F2_STAMPS 0
+#endif
+#if F2_STAMPS
+__device__ unsigned long long f2_pair_wait[16][8];
+#endif
+__device__ __forceinline__ void pair_sync() {
+#if F2_STAMPS
+  unsigned long long t0, t1;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  __syncthreads();
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  if ((threadIdx.x & 63) == 0 && (blockIdx.x & 63) == 0 && (blockIdx.x >> 6) < 16)
+    f2_pair_wait[blockIdx.x >> 6][threadIdx.x >> 6] += t1 - t0;
+#else
+  __syncthreads();
+#endif
+}
+
 // forward: 16 reals per lane (slot e < 8 real part, e + 8 imaginary part) -> half spectrum in xr/xi
 // (slot s: frequency k'(L, 4h + (s & 3)) + 512 (s >> 2)).  Contains two pair barriers: every wave of
 // the workgroup calls it in lockstep.  T0 / T1: the pair's regions (wave 0 / wave 1).
@@ -63,7 +84,7 @@ __device__ __forceinline__ void fwd_half(double (&xr)[8], double (&xi)[8], int h
   dft512_fwd(xr, xi, Tm, lane, tb, twp);
 #pragma unroll
   for (int e = 0; e < 8; e++) Tm[64 * e + lane] = make_double2(xr[e], xi[e]);
-  __syncthreads();
+  pair_sync();
 #pragma unroll
   for (int q = 0; q < 4; q++) {
     const int e = 4 * h + q;
@@ -75,7 +96,7 @@ __device__ __forceinline__ void fwd_half(double (&xr)[8], double (&xi)[8], int h
     xr[q + 4] = e0.x - tr;
     xi[q + 4] = e0.y - ti;
   }
-  __syncthreads();
+  pair_sync();
 }
 
 // inverse, first half: uncombine this wave's 4 slot pairs into the pair's exchange (E_0 -> T0,
@@ -91,7 +112,7 @@ __device__ __forceinline__ void inv_exchange(double (&xr)[8], double (&xi)[8], i
     T0[64 * e + lane] = make_double2(lr + hr, li + hi);
     T1[64 * e + lane] = make_double2(dr, di);
   }
-  __syncthreads();
+  pair_sync();
   const double2* Tm = h ? T1 : T0;
 #pragma unroll
   for (int e = 0; e < 8; e++) {
@@ -99,7 +120,7 @@ __device__ __forceinline__ void inv_exchange(double (&xr)[8], double (&xi)[8], i
     xr[e] = v.x;
     xi[e] = v.y;
   }
-  __syncthreads();
+  pair_sync();
 }
 
 // inverse, second half (wave-private): 512-point inverse + untwist -> reals (slot e < 8: re, e + 8: im)
@@ -173,6 +194,33 @@ typedef __attribute__((address_space(3))) const double lds_f64;
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) const f64x2 lds_c64;  // one complex: a single ds_read_b128
 
+// F2_ACC_AGPR: the two accumulator polynomials live in AGPRs between their uses (rotation and the
+// accumulate after each inverse), moved by v_accvgpr_read / write, to take the 33 spilled VGPRs off
+// scratch.  Rejected: with any AGPR in use at 2 waves / SIMD the allocator splits the unified 256 registers
+// 128 / 128 and spills 58-72 VGPRs instead (hipcc ROCm 7.2; no source-level knob for the split)
+#ifndef F2_ACC_AGPR
+#define F2_ACC_AGPR 0
+#endif
+struct AccRegs {
+  u32 lo[16], hi[16];
+};
+__device__ __forceinline__ void acc_put(AccRegs& s, const u64 (&v)[16]) {
+#pragma unroll
+  for (int e = 0; e < 16; e++) {
+    asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(s.lo[e]) : "v"((u32)v[e]));
+    asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(s.hi[e]) : "v"((u32)(v[e] >> 32)));
+  }
+}
+__device__ __forceinline__ void acc_get(u64 (&v)[16], const AccRegs& s) {
+#pragma unroll
+  for (int e = 0; e < 16; e++) {
+    u32 lo, hi;
+    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(lo) : "a"(s.lo[e]));
+    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(hi) : "a"(s.hi[e]));
+    v[e] = ((u64)hi << 32) | lo;
+  }
+}
+
 // BSK_i[c][0..1] (32 KB) into K: wave w loads the 1 KB blocks 4w .. 4w + 3 (wave-uniform scalar bases)
 __device__ __forceinline__ void load_pair(const double2* __restrict__ bsk, int i, int c, F2Shared& sh, int wave_s,
                                           int lane) {
@@ -193,7 +241,7 @@ __device__ __forceinline__ int rsplit(int c) { return ((c & 1) << 10) | ((c >> 1
 __device__ __forceinline__ void rotate_decompose(const u64 (&acc)[16], int a, int h, int lane, u64* R, int (&dig)[16]) {
 #pragma unroll
   for (int e = 0; e < 16; e++) R[rsplit(coef(h, lane, e))] = acc[e];
-  __syncthreads();
+  pair_sync();
   // (X^a v)[c] = (-1)^bit11(t) v[t mod 2048], t = c - a + 4096 (a < 4096)
   const int t0 = coef(h, lane, 0) + 2 * N2 - a;
 #pragma unroll
@@ -204,7 +252,7 @@ __device__ __forceinline__ void rotate_decompose(const u64 (&acc)[16], int a, in
     const u64 y = ((x ^ m) - m) - acc[e];
     dig[e] = decomp_23x1_hi((u32)(y >> 32));
   }
-  __syncthreads();
+  pair_sync();
 }
 
 // LDS address of this wave's slot 0 in K, laundered: with K's absolute offset folded in, the MAC's
@@ -248,6 +296,27 @@ __device__ __forceinline__ void mac_column(lds_c64* kp, const double (&ar)[8], c
     oi[s] = __builtin_fma(bi[s], v.x, oi[s]);
   }
 }
+
+// F2_STAMPS (diagnostic builds only, never the shipped library): s_memtime stamps at the phase
+// boundaries of the CMUX loop, summed per wave of every 64th workgroup into f2_stamps[slot][wave][phase]
+// (cdna_hip_programming.md, "In-kernel stamps"); read with tfhe_hip_debug_stamps.  Read the SHARES.
+constexpr int F2_NPH = 12;
+#if F2_STAMPS
+__device__ unsigned long long f2_stamps[16][F2_WAVES][F2_NPH];
+#define F2_STAMP(k)                                                                              \
+  do {                                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    unsigned long long _t;                                                                       \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                     \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    st_acc[k] += _t - st_prev;                                                                   \
+    st_prev = _t;                                                                                \
+  } while (0)
+#else
+#define F2_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 
 template <bool WRITE_ACC, bool WRITE_BIG>
 __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
@@ -297,14 +366,15 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
 #if F2_PRIO
   if (wave_s >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
-#if F2_MACORDER
-  // both components are transformed first (D_0 held in registers, not the 64 registers of O), then
-  // O_0 = D_0 K_{0,0} + D_1 K_{1,0} and O_1 = D_0 K_{0,1} + D_1 K_{1,1}: the key buffer holds output
-  // column 0 (K_{0,0}, K_{1,0}); column 1 streams into the transpose area while MAC 0 runs
+#if F2_MACORDER == 2
+  // column order with the first inverse between the two MACs: O_0 = D_0 K_{0,0} + D_1 K_{1,0}, then
+  // acc_0 += iFFT(O_0) while column 1 streams into the key buffer, then O_1 and its inverse.  At no point
+  // are O_0 and O_1 live together (the column-1 MAC of order 1 held both beside D_0, D_1 and the
+  // accumulators: 33 spilled VGPRs)
   for (int i = 0; i < n; i++) {
     const int a = ms4096(ct[i]);
     int dg[16];
-    double d0r[8], d0i[8], xr[8], xi[8], o0r[8], o0i[8], o1r[8], o1i[8];
+    double d0r[8], d0i[8], xr[8], xi[8], o0r[8], o0i[8];
     __syncthreads();  // the previous CMUX's inverse transforms are done with T
     rotate_decompose(accA, a, h, lane, R, dg);
 #pragma unroll
@@ -321,14 +391,9 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's share of column 0; fwd_half's barriers publish it
     fwd_half(xr, xi, h, lane, tb, T0, T1, twp, tt);
-    double2* const kt = &sh.T[0][0];
-    load_column(bsk, i, 1, kt, wave_s, lane);  // column 1 into the (now idle) transpose area, under MAC 0
     mac_column(kbase(&sh.K[0][0], h, lane), d0r, d0i, xr, xi, o0r, o0i);
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    __syncthreads();  // column 1 visible; every wave is done with column 0
-    if (i + 1 < n) load_column(bsk, i + 1, 0, &sh.K[0][0], wave_s, lane);
-    mac_column(kbase(kt, h, lane), d0r, d0i, xr, xi, o1r, o1i);
-    __syncthreads();  // every wave is done with column 1: the transpose area is free again
+    __syncthreads();  // every wave is done with column 0
+    load_column(bsk, i, 1, &sh.K[0][0], wave_s, lane);  // column 1, under the first inverse
     inv_exchange(o0r, o0i, h, lane, T0, T1, tt);
     inv_half(o0r, o0i, h, lane, tb, Tm, twp, tt);
 #pragma unroll
@@ -336,15 +401,118 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
       accA[e] += f64_to_torus_wide(o0r[e]);
       accA[e + 8] += f64_to_torus_wide(o0i[e]);
     }
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();  // column 1 visible
+    {
+      double o1r[8], o1i[8];
+      mac_column(kbase(&sh.K[0][0], h, lane), d0r, d0i, xr, xi, o1r, o1i);
+      __syncthreads();  // every wave is done with column 1 (and with the partner's transpose region)
+      if (i + 1 < n) load_column(bsk, i + 1, 0, &sh.K[0][0], wave_s, lane);
+      inv_exchange(o1r, o1i, h, lane, T0, T1, tt);
+      inv_half(o1r, o1i, h, lane, tb, Tm, twp, tt);
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        accB[e] += f64_to_torus_wide(o1r[e]);
+        accB[e + 8] += f64_to_torus_wide(o1i[e]);
+      }
+    }
+  }
+#elif F2_MACORDER
+  // both components are transformed first (D_0 held in registers, not the 64 registers of O), then
+  // O_0 = D_0 K_{0,0} + D_1 K_{1,0} and O_1 = D_0 K_{0,1} + D_1 K_{1,1}: the key buffer holds output
+  // column 0 (K_{0,0}, K_{1,0}); column 1 streams into the transpose area while MAC 0 runs
+#if F2_STAMPS
+  unsigned long long st_acc[F2_NPH] = {0}, st_prev;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
+#endif
+#if F2_ACC_AGPR
+  AccRegs sA, sB;
+  acc_put(sA, accA);
+  acc_put(sB, accB);
+#endif
+  for (int i = 0; i < n; i++) {
+    const int a = ms4096(ct[i]);
+    int dg[16];
+    double d0r[8], d0i[8], xr[8], xi[8], o0r[8], o0i[8], o1r[8], o1i[8];
+    F2_STAMP(11);
+    __syncthreads();  // the previous CMUX's inverse transforms are done with T
+    F2_STAMP(0);
+#if F2_ACC_AGPR
+    acc_get(accA, sA);
+#endif
+    rotate_decompose(accA, a, h, lane, R, dg);
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      d0r[e] = (double)dg[e];
+      d0i[e] = (double)dg[e + 8];
+    }
+    F2_STAMP(1);
+    fwd_half(d0r, d0i, h, lane, tb, T0, T1, twp, tt);
+    F2_STAMP(2);
+#if F2_ACC_AGPR
+    acc_get(accB, sB);
+#endif
+    rotate_decompose(accB, a, h, lane, R, dg);
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      xr[e] = (double)dg[e];
+      xi[e] = (double)dg[e + 8];
+    }
+    F2_STAMP(3);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's share of column 0; fwd_half's barriers publish it
+    F2_STAMP(4);
+    fwd_half(xr, xi, h, lane, tb, T0, T1, twp, tt);
+    F2_STAMP(5);
+    double2* const kt = &sh.T[0][0];
+    load_column(bsk, i, 1, kt, wave_s, lane);  // column 1 into the (now idle) transpose area, under MAC 0
+    mac_column(kbase(&sh.K[0][0], h, lane), d0r, d0i, xr, xi, o0r, o0i);
+    F2_STAMP(6);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();  // column 1 visible; every wave is done with column 0
+    F2_STAMP(7);
+    if (i + 1 < n) load_column(bsk, i + 1, 0, &sh.K[0][0], wave_s, lane);
+    mac_column(kbase(kt, h, lane), d0r, d0i, xr, xi, o1r, o1i);
+    __syncthreads();  // every wave is done with column 1: the transpose area is free again
+    F2_STAMP(8);
+    inv_exchange(o0r, o0i, h, lane, T0, T1, tt);
+    inv_half(o0r, o0i, h, lane, tb, Tm, twp, tt);
+#if F2_ACC_AGPR
+    acc_get(accA, sA);
+#endif
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      accA[e] += f64_to_torus_wide(o0r[e]);
+      accA[e + 8] += f64_to_torus_wide(o0i[e]);
+    }
+#if F2_ACC_AGPR
+    acc_put(sA, accA);
+#endif
+    F2_STAMP(9);
     __syncthreads();  // the partner's inverse transposes are done with its region
+    F2_STAMP(10);
     inv_exchange(o1r, o1i, h, lane, T0, T1, tt);
     inv_half(o1r, o1i, h, lane, tb, Tm, twp, tt);
+#if F2_ACC_AGPR
+    acc_get(accB, sB);
+#endif
 #pragma unroll
     for (int e = 0; e < 8; e++) {
       accB[e] += f64_to_torus_wide(o1r[e]);
       accB[e + 8] += f64_to_torus_wide(o1i[e]);
     }
+#if F2_ACC_AGPR
+    acc_put(sB, accB);
+#endif
   }
+#if F2_ACC_AGPR
+  acc_get(accA, sA);
+  acc_get(accB, sB);
+#endif
+#if F2_STAMPS
+  F2_STAMP(11);
+  if ((blockIdx.x & 63) == 0 && lane == 0 && (blockIdx.x >> 6) < 16)
+    for (int k = 0; k < F2_NPH; k++) f2_stamps[blockIdx.x >> 6][wave][k] = st_acc[k];
+#endif
 #else
   for (int i = 0; i < n; i++) {
     const int a = ms4096(ct[i]);
@@ -669,6 +837,15 @@ hipError_t launch_fft2k_inv(const double* in, size_t count, double* out, const d
                      (const double2*)tw);
   return hipGetLastError();
 }
+
+#if F2_STAMPS
+hipError_t read_fft2k_stamps(unsigned long long* out) {  // 16 x 8 x F2_NPH, then 16 x 8 pair-barrier waits
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(fft2k::f2_stamps), sizeof(fft2k::f2_stamps), 0, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return e;
+  return hipMemcpyFromSymbol(out + 16 * 8 * fft2k::F2_NPH, HIP_SYMBOL(fft2k::f2_pair_wait), sizeof(fft2k::f2_pair_wait), 0,
+                             hipMemcpyDeviceToHost);
+}
+#endif
 
 hipError_t launch_blind_rotate_fft2k(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
                                      int n_lut, const double* bsk_f, const double* tw, u64* out_big, u64* out_acc,
