@@ -530,6 +530,16 @@ extern "C" int tfhe_hip_debug_fft2k_stamps(unsigned long long* out) {
 }
 #endif
 
+#if FFT_STAMPS
+namespace tfhe {
+hipError_t read_fft_stamps(unsigned long long* out);
+}
+// diagnostic builds only (-DFFT_STAMPS=1): the P-GATE batch kernel's phase stamps (tools/stamps.py --gate)
+extern "C" int tfhe_hip_debug_fft_stamps(unsigned long long* out) {
+  return tfhe::read_fft_stamps(out) == hipSuccess ? 0 : TFHE_HIP_EDEVICE;
+}
+#endif
+
 // error slot shared with pks_api.cpp / sns_api.cpp
 int tfhe_hip_set_error(int code, const char* msg) {
   g_err = msg;

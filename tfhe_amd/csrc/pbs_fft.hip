@@ -152,6 +152,35 @@ constexpr int CHUNK_GLDS = CHUNK_C64 * 16 / 1024;  // 1 KB wave-instructions per
 // (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] = 7 | lgkmcnt[11:8] = 15 | vmcnt[5:4] in [15:14])
 [[maybe_unused]] constexpr int VMCNT_CHUNK = 0x0F70 | (CHUNK_GLDS / 8);
 
+// FFT_STAMPS (diagnostic builds only, never the shipped library): s_memtime stamps at the phase
+// boundaries of the CMUX loop, summed per wave of every 64th workgroup into fft_stamps[slot][wave][phase]
+// (read with tfhe_hip_debug_fft_stamps, tools/stamps.py --gate).  Read the SHARES: the stamps' waits
+// forbid overlaps the shipped kernel has.
+#ifndef FFT_STAMPS
+#define FFT_STAMPS 0
+#endif
+constexpr int FS_NPH = 8;  // rotate, level barrier, digits + twist, forward DFT, MAC, inverse 0, inverse 1, top
+#if FFT_STAMPS
+__device__ unsigned long long fft_stamps[16][FB_WAVES][FS_NPH];
+#define FS_STAMP(k)                                                                              \
+  do {                                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    unsigned long long _t;                                                                       \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                     \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    st_acc[k] += _t - st_prev;                                                                   \
+    st_prev = _t;                                                                                \
+  } while (0)
+#define FS_ARGS , unsigned long long (&st_acc)[FS_NPH], unsigned long long& st_prev
+#define FS_PASS , st_acc, st_prev
+#else
+#define FS_STAMP(k) \
+  do {              \
+  } while (0)
+#define FS_ARGS
+#define FS_PASS
+#endif
+
 struct FftShared {
   double2 T[FB_WAVES][T_C64];  // per-wave transpose / rotation scratch  72 KB
   double2 K[FFT_KBUF][CHUNK_C64];  // BSK level-step chunks in flight   16 KB each
@@ -173,7 +202,7 @@ __device__ __forceinline__ void load_chunk(const double2* __restrict__ bsk, int 
 __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rbase, int c, int i, int n_steps,
                                                    FftShared& sh, double2* T, int wave, int lane, TBase tb,
                                                    const double2* __restrict__ bsk, double (&o0r)[8],
-                                                   double (&o0i)[8], double (&o1r)[8], double (&o1i)[8]) {
+                                                   double (&o0i)[8], double (&o1r)[8], double (&o1i)[8] FS_ARGS) {
   u64* Tu = (u64*)T;
 #pragma unroll
   for (int e = 0; e < 16; e++) Tu[64 * e + lane] = acc[e];
@@ -188,6 +217,7 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rba
     st[e] = decomp_state(r - acc[e]);
   }
   lds_order();
+  FS_STAMP(0);
 #pragma unroll 1
   for (int q = 0; q < 3; q++) {  // level 2 - q: least significant first
     const int g = i * 6 + c * 3 + q;
@@ -203,6 +233,7 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rba
     glds_barrier();
     if (g + 1 < n_steps) load_chunk(bsk, g + 1, sh.K[(g + 1) & 1], wave, lane);
 #endif
+    FS_STAMP(1);
     const u32 bmask = q < 2 ? 1u : 0u;
     double xr[8], xi[8];
 #pragma unroll
@@ -211,7 +242,9 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rba
       xi[e] = (double)decomp_step(st[e + 8], bmask);
       cmul<false>(xr[e], xi[e], sh.tw[TW_TWIST + 64 * e + lane]);
     }
+    FS_STAMP(2);
     dft512_fwd(xr, xi, T, lane, tb, sh.tw);
+    FS_STAMP(3);
     const double2* k0 = sh.K[g % FFT_KBUF] + lane;
     const double2* k1 = sh.K[g % FFT_KBUF] + M + lane;
 #pragma unroll
@@ -226,6 +259,7 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rba
       o1i[e] = __builtin_fma(xr[e], v.y, o1i[e]);
       o1i[e] = __builtin_fma(xi[e], v.x, o1i[e]);
     }
+    FS_STAMP(4);
   }
 }
 
@@ -285,16 +319,27 @@ __global__ __launch_bounds__(FB_THREADS, 1) void blind_rotate_fft_kernel(
 #elif FFT_PRIO == 2
   if (wave & 1) __builtin_amdgcn_s_setprio(1);
 #endif
+#if FFT_STAMPS
+  unsigned long long st_acc[FS_NPH] = {0}, st_prev;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
+#endif
   for (int i = 0; i < n; i++) {
     const int rbase = lane - ms2048(ct[i]) + 2 * N1K;
     double o0r[8], o0i[8], o1r[8], o1i[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) { o0r[e] = 0; o0i[e] = 0; o1r[e] = 0; o1i[e] = 0; }
-    ext_prod_component(accA, rbase, 0, i, n_steps, sh, T, wave, lane, tb, bsk, o0r, o0i, o1r, o1i);
-    ext_prod_component(accB, rbase, 1, i, n_steps, sh, T, wave, lane, tb, bsk, o0r, o0i, o1r, o1i);
+    FS_STAMP(7);
+    ext_prod_component(accA, rbase, 0, i, n_steps, sh, T, wave, lane, tb, bsk, o0r, o0i, o1r, o1i FS_PASS);
+    ext_prod_component(accB, rbase, 1, i, n_steps, sh, T, wave, lane, tb, bsk, o0r, o0i, o1r, o1i FS_PASS);
     accumulate(accA, o0r, o0i, T, lane, tb, sh.tw);
+    FS_STAMP(5);
     accumulate(accB, o1r, o1i, T, lane, tb, sh.tw);
+    FS_STAMP(6);
   }
+#if FFT_STAMPS
+  if ((blockIdx.x & 63) == 0 && lane == 0 && (blockIdx.x >> 6) < 16)
+    for (int k = 0; k < FS_NPH; k++) fft_stamps[blockIdx.x >> 6][wave][k] = st_acc[k];
+#endif
 
   if (!live) return;
   if (WRITE_ACC) {
@@ -523,6 +568,12 @@ void make_fft_tables(double* t) {
       twiddle(((L >> 3) * ((L & 7) + 8 * e)) % M, M, &t[2 * (TW_I + 64 * e + L)], &t[2 * (TW_I + 64 * e + L) + 1]);
     }
 }
+
+#if FFT_STAMPS
+hipError_t read_fft_stamps(unsigned long long* out) {  // 16 x 8 x FS_NPH
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(fftk::fft_stamps), sizeof(fftk::fft_stamps), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 hipError_t launch_bsk_to_fourier(const u64* bsk_std, double* bsk_f, size_t polys, const double* tw, hipStream_t s) {
   hipLaunchKernelGGL(fftk::bsk_to_fourier_kernel, dim3((unsigned)polys), dim3(64), 0, s, bsk_std, (double2*)bsk_f,
