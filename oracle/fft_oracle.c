@@ -36,6 +36,9 @@
  *                    holds frequency k'(L, 4h + (s & 3)) + 512 (s >> 2), k'(L, e) = (L>>3) + 8 (L&7) + 64 e.
  *                    Inverse: E_0 = lo + hi, E_1 = cmul(lo - hi, conj(w^k')), the 512-point inverses,
  *                    untwist by conj(zeta^{2m+h}).  1/M = 2^-10 folded into the BSK.
+ *   N = 1024         the twist is merged into the passes (see fft_tab.twAm / twIm): z = v * zeta^{64 e} for
+ *                    slot e > 0 before pass A, whose table is zeta^{L (1 + 4 e)} for all 8 slots; inverse pass
+ *                    B' uses zeta^{(n0 + 8 n1)(4 k0 + 1)} and the output slot e > 0 gets conj(zeta^{64 e})
  *   MAC              re = fma(D.re, K.re, re); re = fma(-D.im, K.im, re);
  *                    im = fma(D.re, K.im, im); im = fma(D.im, K.re, im)   from (0, 0), over
  *                    c = 0..k and, within c, the levels least significant first (l = L-1 .. 0:
@@ -100,6 +103,11 @@ typedef struct fft_tab {
   or_c64 twA[8][64];    /* w^{L k0}, w = e^{2 pi i / M} */
   or_c64 twB[8][64];    /* w^{8 (L & 7) k1} */
   or_c64 twI[8][64];    /* w^{(L >> 3) ((L & 7) + 8 e)} (inverse pass B') */
+  /* N = 1024 merged twist (pbs_fft.hip / fft512.h): zeta^j = zeta^L zeta^{64 e} for j = L + 64 e; the slot
+   * constant zeta^{64 e} multiplies before pass A, zeta^L rides in pass A's table (all 8 slots), and the
+   * inverse carries zeta^{n0 + 8 n1} in pass B''s table and conj(zeta^{64 e}) after pass A' */
+  or_c64 twAm[8][64];   /* zeta^{L (1 + 4 e)} */
+  or_c64 twIm[8][64];   /* zeta^{(n0 + 8 e)(4 k0 + 1)}, L = n0 + 8 k0 */
 } fft_tab;
 
 static fft_tab g_tab;
@@ -115,6 +123,9 @@ static const fft_tab* tab(void) {
           or_fft_twiddle((L * e) % FFT_M, FFT_M, &g_tab.twA[e][L].re, &g_tab.twA[e][L].im);
           or_fft_twiddle((8 * (L & 7) * e) % FFT_M, FFT_M, &g_tab.twB[e][L].re, &g_tab.twB[e][L].im);
           or_fft_twiddle(((L >> 3) * ((L & 7) + 8 * e)) % FFT_M, FFT_M, &g_tab.twI[e][L].re, &g_tab.twI[e][L].im);
+          or_fft_twiddle((L * (1 + 4 * e)) % (4 * FFT_M), 4 * FFT_M, &g_tab.twAm[e][L].re, &g_tab.twAm[e][L].im);
+          or_fft_twiddle((((L & 7) + 8 * e) * (4 * (L >> 3) + 1)) % (4 * FFT_M), 4 * FFT_M, &g_tab.twIm[e][L].re,
+                         &g_tab.twIm[e][L].im);
         }
       __atomic_store_n(&g_tab_ready, 1, __ATOMIC_RELEASE);
     }
@@ -168,14 +179,17 @@ static void dft8(or_c64 x[8], int inv) {
   for (int k = 0; k < 8; k++) x[k] = u[brv3[k]];
 }
 
-/* forward 3-pass DFT: natural order in, device order out */
-static void dft512_fwd(const or_c64* in, or_c64* out) {
+/* forward 3-pass DFT: natural order in, device order out (merged: pass A multiplies every slot by twAm) */
+static void dft512_fwd_m(const or_c64* in, or_c64* out, int merged) {
   const fft_tab* T = tab();
   or_c64 A[64][8], Bv[64][8], x[8];
   for (int L = 0; L < 64; L++) {
     for (int e = 0; e < 8; e++) x[e] = in[L + 64 * e];
     dft8(x, 0);
-    for (int e = 1; e < 8; e++) x[e] = cmul(x[e], T->twA[e][L].re, T->twA[e][L].im);
+    if (merged)
+      for (int e = 0; e < 8; e++) x[e] = cmul(x[e], T->twAm[e][L].re, T->twAm[e][L].im);
+    else
+      for (int e = 1; e < 8; e++) x[e] = cmul(x[e], T->twA[e][L].re, T->twA[e][L].im);
     memcpy(A[L], x, sizeof(x));
   }
   for (int L = 0; L < 64; L++) { /* lane n0 + 8 k0 */
@@ -191,8 +205,10 @@ static void dft512_fwd(const or_c64* in, or_c64* out) {
   }
 }
 
-/* inverse 3-pass DFT (no 1/M): device order in, natural order out */
-static void dft512_inv(const or_c64* in, or_c64* out) {
+static void dft512_fwd(const or_c64* in, or_c64* out) { dft512_fwd_m(in, out, 0); }
+
+/* inverse 3-pass DFT (no 1/M): device order in, natural order out (merged: pass B' uses twIm) */
+static void dft512_inv_m(const or_c64* in, or_c64* out, int merged) {
   const fft_tab* T = tab();
   or_c64 S1[64][8], S2[64][8], x[8];
   for (int L = 0; L < 64; L++) { /* lane k1 + 8 k0: k2 -> n0 */
@@ -204,7 +220,10 @@ static void dft512_inv(const or_c64* in, or_c64* out) {
   for (int L = 0; L < 64; L++) { /* lane n0 + 8 k0: k1 -> n1 */
     for (int e = 0; e < 8; e++) x[e] = S1[e + 8 * (L >> 3)][L & 7];
     dft8(x, 1);
-    for (int e = 0; e < 8; e++) x[e] = cmul(x[e], T->twI[e][L].re, -T->twI[e][L].im);
+    if (merged)
+      for (int e = 0; e < 8; e++) x[e] = cmul(x[e], T->twIm[e][L].re, -T->twIm[e][L].im);
+    else
+      for (int e = 0; e < 8; e++) x[e] = cmul(x[e], T->twI[e][L].re, -T->twI[e][L].im);
     memcpy(S2[L], x, sizeof(x));
   }
   for (int L = 0; L < 64; L++) { /* lane n0 + 8 n1: k0 -> n2 */
@@ -213,6 +232,8 @@ static void dft512_inv(const or_c64* in, or_c64* out) {
     for (int e = 0; e < 8; e++) out[L + 64 * e] = x[e];
   }
 }
+
+static void dft512_inv(const or_c64* in, or_c64* out) { dft512_inv_m(in, out, 0); }
 
 /* ---- N = 2048: two 512-point halves + one combine pass ------------------------------------ */
 typedef struct fft2k_tab {
@@ -287,11 +308,12 @@ void or_fft_fwd(const double* a, uint32_t N, or_c64* out) {
   if (N != 2 * FFT_M) abort();
   const fft_tab* T = tab();
   or_c64 z[FFT_M];
-  for (int j = 0; j < FFT_M; j++) {
+  for (int j = 0; j < FFT_M; j++) { /* j = L + 64 e: slot constant zeta^{64 e} (e > 0), zeta^L in pass A */
     const or_c64 v = {a[j], a[j + FFT_M]};
-    z[j] = cmul(v, T->twist[j].re, T->twist[j].im);
+    const int e = j >> 6;
+    z[j] = e ? cmul(v, T->twist[64 * e].re, T->twist[64 * e].im) : v;
   }
-  dft512_fwd(z, out);
+  dft512_fwd_m(z, out, 1);
 }
 
 void or_fft_inv(const or_c64* in, uint32_t N, double* out) {
@@ -299,9 +321,10 @@ void or_fft_inv(const or_c64* in, uint32_t N, double* out) {
   if (N != 2 * FFT_M) abort();
   const fft_tab* T = tab();
   or_c64 z[FFT_M];
-  dft512_inv(in, z);
-  for (int j = 0; j < FFT_M; j++) {
-    const or_c64 v = cmul(z[j], T->twist[j].re, -T->twist[j].im);
+  dft512_inv_m(in, z, 1);
+  for (int j = 0; j < FFT_M; j++) { /* conj(zeta^{64 e}) after pass A' (e > 0); conj(zeta^L) rode in pass B' */
+    const int e = j >> 6;
+    const or_c64 v = e ? cmul(z[j], T->twist[64 * e].re, -T->twist[64 * e].im) : z[j];
     out[j] = v.re;
     out[j + FFT_M] = v.im;
   }

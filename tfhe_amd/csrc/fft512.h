@@ -107,12 +107,14 @@ struct TBase {
       : b1((lane >> 3) * S1 + (lane & 7)), b2((lane & 7) * S2 + 8 * (lane >> 3)) {}
 };
 
-// forward 512-point DFT: natural order in (lane L, slot e <-> L + 64 e), device order out
+// forward 512-point DFT: natural order in (lane L, slot e <-> L + 64 e), device order out.
+// TW0: pass A multiplies slot 0 too (the N = 1024 tables fold the lane part of the twist into pass A)
+template <bool TW0 = false>
 __device__ __forceinline__ void dft512_fwd(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
                                            const double2* tw) {
   dft8<false>(xr, xi);
 #pragma unroll
-  for (int e = 1; e < 8; e++) cmul<false>(xr[e], xi[e], tw[TW_A + 64 * e + lane]);
+  for (int e = TW0 ? 0 : 1; e < 8; e++) cmul<false>(xr[e], xi[e], tw[TW_A + 64 * e + lane]);
 #pragma unroll
   for (int e = 0; e < 8; e++) T[lane + S1 * e] = make_double2(xr[e], xi[e]);
   lds_order();
@@ -169,6 +171,61 @@ __device__ __forceinline__ void dft512_inv(double (&xr)[8], double (&xi)[8], dou
   }
   lds_order();
   dft8<true>(xr, xi);
+}
+
+// ---------------------------------------------------------------------------------------------
+// N = 1024 (P-GATE) merged twist.  z_j = a_j zeta^j with j = L + 64 e splits as zeta^L * zeta^(64 e): the
+// slot part c_e = zeta^(64 e) is a per-slot constant (an SGPR operand, no table read) applied before
+// pass A, and the lane part zeta^L commutes with pass A's 8-point DFT over the slots, so it is folded
+// into pass A's table: TW_A[e][L] = w^(L e) zeta^L = zeta^(L (1 + 4 e)).  The inverse does the mirror
+// image: zeta^(n0 + 8 n1) rides in pass B''s table (TW_I[e][L] = zeta^((n0 + 8 e)(4 k0 + 1)), L = n0 + 8
+// k0), conj(c_e) is applied after pass A'.  Saves 15 of the 54 LDS reads of a forward digit transform
+// and 8 of an inverse (oracle/fft_oracle.c: or_fft_fwd / or_fft_inv at N = 1024 restate the order).
+// The constants come from the table generator's own series, evaluated at compile time (IEEE double,
+// no contraction in constant evaluation) so they equal the host tables bit for bit.
+namespace ctw {
+constexpr double sin_s(double x) {
+  double x2 = x * x, term = x, sum = 0.0;
+  for (int i = 1; i <= 21; i += 2) { sum += term; term = -term * x2 / (double)((i + 1) * (i + 2)); }
+  return sum;
+}
+constexpr double cos_s(double x) {
+  double x2 = x * x, term = 1.0, sum = 0.0;
+  for (int i = 0; i <= 20; i += 2) { sum += term; term = -term * x2 / (double)((i + 1) * (i + 2)); }
+  return sum;
+}
+struct c64 {
+  double x, y;
+};
+// cos / sin (2 pi t / 2048) for t = 64 e, e = 0..7 (t <= 448 < M / 4: octant and quarter cases only)
+constexpr c64 slot(int e) {
+  const unsigned t = 64u * (unsigned)e, m = 2048u;
+  if (8 * t > m) {
+    const double x = (double)(m / 4 - t) * (6.28318530717958647692 / (double)m);
+    return c64{sin_s(x), cos_s(x)};
+  }
+  const double x = (double)t * (6.28318530717958647692 / (double)m);
+  return c64{cos_s(x), sin_s(x)};
+}
+constexpr c64 SLOT[8] = {slot(0), slot(1), slot(2), slot(3), slot(4), slot(5), slot(6), slot(7)};
+}  // namespace ctw
+
+// z * c_e (forward) / z * conj(c_e) (inverse) for slot e > 0, c_e a compile-time constant; the
+// operation order of cmul
+template <bool INV>
+__device__ __forceinline__ void twist_slots(double (&xr)[8], double (&xi)[8]) {
+#pragma unroll
+  for (int e = 1; e < 8; e++) {
+    const double wr = ctw::SLOT[e].x, wi = ctw::SLOT[e].y;
+    const double p = xr[e], q = xi[e];
+    if (!INV) {
+      xr[e] = __builtin_fma(p, wr, -(q * wi));
+      xi[e] = __builtin_fma(p, wi, q * wr);
+    } else {
+      xr[e] = __builtin_fma(p, wr, q * wi);
+      xi[e] = __builtin_fma(p, -wi, q * wr);
+    }
+  }
 }
 
 // (double)(int64)x, correctly rounded: exact hi * 2^32 plus exact lo, one rounding

@@ -37,23 +37,23 @@ namespace tfhe {
 namespace fftk {
 
 // forward transform of a real polynomial held as 16 doubles per lane (slot e <-> coefficient 64 e + L)
+// (twist: slot constants here, the lane part inside pass A — fft512.h, "N = 1024 merged twist")
 __device__ __forceinline__ void fft_fwd_real(const double (&a)[16], double (&xr)[8], double (&xi)[8], double2* T,
                                              int lane, const double2* tw) {
 #pragma unroll
   for (int e = 0; e < 8; e++) {
     xr[e] = a[e];
     xi[e] = a[e + 8];
-    cmul<false>(xr[e], xi[e], tw[TW_TWIST + 64 * e + lane]);
   }
-  dft512_fwd(xr, xi, T, lane, TBase(lane), tw);
+  twist_slots<false>(xr, xi);
+  dft512_fwd<true>(xr, xi, T, lane, TBase(lane), tw);
 }
 
 // inverse transform (no 1/M) + untwist: slot e -> coefficient 64 e + L (re), 64 (e + 8) + L (im)
 __device__ __forceinline__ void fft_inv_real(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
                                              const double2* tw) {
   dft512_inv(xr, xi, T, lane, tb, tw);
-#pragma unroll
-  for (int e = 0; e < 8; e++) cmul<true>(xr[e], xi[e], tw[TW_TWIST + 64 * e + lane]);
+  twist_slots<true>(xr, xi);  // the lane part of the untwist rode in pass B''s table
 }
 
 __device__ __forceinline__ int ms2048(u64 x) { return (int)((((x >> 52) + 1) >> 1) & 2047u); }
@@ -240,10 +240,10 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rba
     for (int e = 0; e < 8; e++) {
       xr[e] = (double)decomp_step(st[e], bmask);
       xi[e] = (double)decomp_step(st[e + 8], bmask);
-      cmul<false>(xr[e], xi[e], sh.tw[TW_TWIST + 64 * e + lane]);
     }
+    twist_slots<false>(xr, xi);
     FS_STAMP(2);
-    dft512_fwd(xr, xi, T, lane, tb, sh.tw);
+    dft512_fwd<true>(xr, xi, T, lane, tb, sh.tw);
     FS_STAMP(3);
     const double2* k0 = sh.K[g % FFT_KBUF] + lane;
     const double2* k1 = sh.K[g % FFT_KBUF] + M + lane;
@@ -443,9 +443,9 @@ __global__ __launch_bounds__(FL_THREADS, 1) void blind_rotate_fft_lat_kernel(
       for (int e = 0; e < 8; e++) {
         xr[e] = (double)dg[e];
         xi[e] = (double)dg[e + 8];
-        cmul<false>(xr[e], xi[e], sh.tw[TW_TWIST + 64 * e + lane]);
       }
-      dft512_fwd(xr, xi, sh.T[wave], lane, tb, sh.tw);
+      twist_slots<false>(xr, xi);
+      dft512_fwd<true>(xr, xi, sh.T[wave], lane, tb, sh.tw);
 #pragma unroll
       for (int e = 0; e < 8; e++) sh.F[wave][64 * e + lane] = make_double2(xr[e], xi[e]);
     }
@@ -558,15 +558,29 @@ void fft_twiddle(uint32_t t, uint32_t m, double* c, double* s) { fftk::twiddle(t
 
 size_t fft_tables_len() { return 2 * fftk::TW_C64; }
 
+// N = 1024 tables with the twist merged into the passes (fft512.h, "N = 1024 merged twist"):
+//   TW_A[e][L] = zeta^(L (1 + 4 e)),  TW_B as before,  TW_I[e][L] = zeta^((n0 + 8 e)(4 k0 + 1)) (L = n0 + 8 k0),
+// zeta = e^(2 pi i / 2048); TW_TWIST keeps zeta^j (the slot constants are its entries j = 64 e)
 void make_fft_tables(double* t) {
   using namespace fftk;
   for (uint32_t j = 0; j < (uint32_t)M; j++) twiddle(j, 4 * M, &t[2 * (TW_TWIST + j)], &t[2 * (TW_TWIST + j) + 1]);
   for (uint32_t e = 0; e < 8; e++)
     for (uint32_t L = 0; L < 64; L++) {
-      twiddle((L * e) % M, M, &t[2 * (TW_A + 64 * e + L)], &t[2 * (TW_A + 64 * e + L) + 1]);
+      twiddle((L * (1 + 4 * e)) % (4 * M), 4 * M, &t[2 * (TW_A + 64 * e + L)], &t[2 * (TW_A + 64 * e + L) + 1]);
       twiddle((8 * (L & 7) * e) % M, M, &t[2 * (TW_B + 64 * e + L)], &t[2 * (TW_B + 64 * e + L) + 1]);
-      twiddle(((L >> 3) * ((L & 7) + 8 * e)) % M, M, &t[2 * (TW_I + 64 * e + L)], &t[2 * (TW_I + 64 * e + L) + 1]);
+      twiddle((((L & 7) + 8 * e) * (4 * (L >> 3) + 1)) % (4 * M), 4 * M, &t[2 * (TW_I + 64 * e + L)],
+              &t[2 * (TW_I + 64 * e + L) + 1]);
     }
+}
+
+// the compile-time slot constants equal the table generator's zeta^(64 e) bit for bit
+bool fft_slot_constants_ok() {
+  for (int e = 0; e < 8; e++) {
+    double c, s;
+    fftk::twiddle(64u * e, 2048u, &c, &s);
+    if (c != fftk::ctw::SLOT[e].x || s != fftk::ctw::SLOT[e].y) return false;
+  }
+  return true;
 }
 
 #if FFT_STAMPS

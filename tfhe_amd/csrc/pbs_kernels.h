@@ -31,6 +31,7 @@ hipError_t launch_keyswitch_mfma(const u64* in_big, size_t B, int big_dim, const
 // Fourier BSK = polys x 512 complex
 size_t fft_tables_len();  // doubles
 void make_fft_tables(double* tw);
+bool fft_slot_constants_ok();  // the N = 1024 kernels' compile-time twist constants == the host tables
 hipError_t launch_bsk_to_fourier(const u64* bsk_std, double* bsk_f, size_t polys, const double* tw, hipStream_t s);
 // batches of at most latency_max_batch ciphertexts use the latency kernel (one ciphertext per workgroup)
 hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
