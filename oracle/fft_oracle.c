@@ -20,17 +20,21 @@
  *                    internal rotations by e^{+-i pi/4 j} are the explicit forms in w8() below
  *   3 passes         M = 512 = 8 x 8 x 8 over a 64 x 8 grid (the device's lane x register grid),
  *                    w = e^{2 pi i / M}, n = n0 + 8 n1 + 64 n2, k = k0 + 8 k1 + 64 k2:
- *                    A: lane L = n0 + 8 n1 transforms n2, then x[k0] *= w^{L k0}           (k0 > 0)
+ *                    A: lane L = n0 + 8 n1 transforms n2, then x[k0] *= w^{L k0} (k0 > 0; with the twist
+ *                       merged, see N = 1024 / N = 2048 below, every k0 by the merged table)
  *                    B: lane n0 + 8 k0 transforms n1, then x[k1] *= w^{8 n0 k1}            (k1 > 0)
  *                    C: lane k1 + 8 k0 transforms n0 -> Z[k] in slot k2
  *                    so spectra are kept in DEVICE ORDER: slot d = L + 64 e holds frequency
  *                    k(d) = (L >> 3) + 8 (L & 7) + 64 e (the BSK is converted by the same routine)
  *   inverse          the passes reversed (decimation in time), device order in, natural order out:
  *                    C': lane k1 + 8 k0 transforms k2 -> n0, x[n0] *= conj(w^{8 n0 k1})   (n0 > 0)
- *                    B': lane n0 + 8 k0 transforms k1 -> n1, x[n1] *= conj(w^{k0 (n0 + 8 n1)}) (all)
+ *                    B': lane n0 + 8 k0 transforms k1 -> n1, x[n1] *= conj(w^{k0 (n0 + 8 n1)}) (all; the
+ *                        merged tables also carry the lane part of the untwist)
  *                    A': lane n0 + 8 n1 transforms k0 -> n2 = z[L + 64 n2]
  *   N = 2048         (P-FHEVM, preset 3) two 512-point halves: z_j = (a_j + i a_{j+1024}) zeta^j,
- *                    zeta = e^{i pi/2048}; E_h = the 512-point DFT above of z_{2m+h} (h = 0, 1), then
+ *                    zeta = e^{i pi/2048}; E_h = the 512-point DFT above of z_{2m+h} (h = 0, 1) with the
+ *                    twist merged per parity (fft2k_tab.twA / twI: slot constant zeta^{128 e} before pass A,
+ *                    zeta^{2 L + h} in pass A's table; the mirror image in the inverse), then
  *                    t = cmul(E_1[k'], w^k'), w = e^{2 pi i/1024}: Z[k'] = E_0 + t, Z[k'+512] = E_0 - t.
  *                    Device order of the spectrum (two waves per polynomial): index h*512 + 64 s + L
  *                    holds frequency k'(L, 4h + (s & 3)) + 512 (s >> 2), k'(L, e) = (L>>3) + 8 (L&7) + 64 e.
@@ -100,9 +104,7 @@ void or_fft_twiddle(uint32_t t, uint32_t M, double* c, double* s) {
 
 typedef struct fft_tab {
   or_c64 twist[FFT_M];  /* zeta^j, zeta = e^{i pi / N} */
-  or_c64 twA[8][64];    /* w^{L k0}, w = e^{2 pi i / M} */
-  or_c64 twB[8][64];    /* w^{8 (L & 7) k1} */
-  or_c64 twI[8][64];    /* w^{(L >> 3) ((L & 7) + 8 e)} (inverse pass B') */
+  or_c64 twB[8][64];    /* w^{8 (L & 7) k1}, w = e^{2 pi i / M} */
   /* N = 1024 merged twist (pbs_fft.hip / fft512.h): zeta^j = zeta^L zeta^{64 e} for j = L + 64 e; the slot
    * constant zeta^{64 e} multiplies before pass A, zeta^L rides in pass A's table (all 8 slots), and the
    * inverse carries zeta^{n0 + 8 n1} in pass B''s table and conj(zeta^{64 e}) after pass A' */
@@ -120,9 +122,7 @@ static const fft_tab* tab(void) {
       for (uint32_t j = 0; j < FFT_M; j++) or_fft_twiddle(j, 2 * FFT_M * 2, &g_tab.twist[j].re, &g_tab.twist[j].im);
       for (uint32_t e = 0; e < 8; e++)
         for (uint32_t L = 0; L < 64; L++) {
-          or_fft_twiddle((L * e) % FFT_M, FFT_M, &g_tab.twA[e][L].re, &g_tab.twA[e][L].im);
           or_fft_twiddle((8 * (L & 7) * e) % FFT_M, FFT_M, &g_tab.twB[e][L].re, &g_tab.twB[e][L].im);
-          or_fft_twiddle(((L >> 3) * ((L & 7) + 8 * e)) % FFT_M, FFT_M, &g_tab.twI[e][L].re, &g_tab.twI[e][L].im);
           or_fft_twiddle((L * (1 + 4 * e)) % (4 * FFT_M), 4 * FFT_M, &g_tab.twAm[e][L].re, &g_tab.twAm[e][L].im);
           or_fft_twiddle((((L & 7) + 8 * e) * (4 * (L >> 3) + 1)) % (4 * FFT_M), 4 * FFT_M, &g_tab.twIm[e][L].re,
                          &g_tab.twIm[e][L].im);
@@ -179,17 +179,15 @@ static void dft8(or_c64 x[8], int inv) {
   for (int k = 0; k < 8; k++) x[k] = u[brv3[k]];
 }
 
-/* forward 3-pass DFT: natural order in, device order out (merged: pass A multiplies every slot by twAm) */
-static void dft512_fwd_m(const or_c64* in, or_c64* out, int merged) {
+/* forward 3-pass DFT: natural order in, device order out; pass A multiplies slots merged ? 0..7 : 1..7 by twa
+ * (the twist-merged tables multiply every slot) */
+static void dft512_fwd_tab(const or_c64* in, or_c64* out, const or_c64 (*twa)[64], int merged) {
   const fft_tab* T = tab();
   or_c64 A[64][8], Bv[64][8], x[8];
   for (int L = 0; L < 64; L++) {
     for (int e = 0; e < 8; e++) x[e] = in[L + 64 * e];
     dft8(x, 0);
-    if (merged)
-      for (int e = 0; e < 8; e++) x[e] = cmul(x[e], T->twAm[e][L].re, T->twAm[e][L].im);
-    else
-      for (int e = 1; e < 8; e++) x[e] = cmul(x[e], T->twA[e][L].re, T->twA[e][L].im);
+    for (int e = merged ? 0 : 1; e < 8; e++) x[e] = cmul(x[e], twa[e][L].re, twa[e][L].im);
     memcpy(A[L], x, sizeof(x));
   }
   for (int L = 0; L < 64; L++) { /* lane n0 + 8 k0 */
@@ -205,10 +203,10 @@ static void dft512_fwd_m(const or_c64* in, or_c64* out, int merged) {
   }
 }
 
-static void dft512_fwd(const or_c64* in, or_c64* out) { dft512_fwd_m(in, out, 0); }
+
 
 /* inverse 3-pass DFT (no 1/M): device order in, natural order out (merged: pass B' uses twIm) */
-static void dft512_inv_m(const or_c64* in, or_c64* out, int merged) {
+static void dft512_inv_tab(const or_c64* in, or_c64* out, const or_c64 (*twi)[64]) {
   const fft_tab* T = tab();
   or_c64 S1[64][8], S2[64][8], x[8];
   for (int L = 0; L < 64; L++) { /* lane k1 + 8 k0: k2 -> n0 */
@@ -220,10 +218,7 @@ static void dft512_inv_m(const or_c64* in, or_c64* out, int merged) {
   for (int L = 0; L < 64; L++) { /* lane n0 + 8 k0: k1 -> n1 */
     for (int e = 0; e < 8; e++) x[e] = S1[e + 8 * (L >> 3)][L & 7];
     dft8(x, 1);
-    if (merged)
-      for (int e = 0; e < 8; e++) x[e] = cmul(x[e], T->twIm[e][L].re, -T->twIm[e][L].im);
-    else
-      for (int e = 0; e < 8; e++) x[e] = cmul(x[e], T->twI[e][L].re, -T->twI[e][L].im);
+    for (int e = 0; e < 8; e++) x[e] = cmul(x[e], twi[e][L].re, -twi[e][L].im);
     memcpy(S2[L], x, sizeof(x));
   }
   for (int L = 0; L < 64; L++) { /* lane n0 + 8 n1: k0 -> n2 */
@@ -233,12 +228,17 @@ static void dft512_inv_m(const or_c64* in, or_c64* out, int merged) {
   }
 }
 
-static void dft512_inv(const or_c64* in, or_c64* out) { dft512_inv_m(in, out, 0); }
+
 
 /* ---- N = 2048: two 512-point halves + one combine pass ------------------------------------ */
 typedef struct fft2k_tab {
   or_c64 twist[2 * FFT_M];  /* zeta^j, zeta = e^{i pi / 2048} */
   or_c64 wc[2][4][64];      /* w^{k'(L, 4h + p)}, w = e^{2 pi i / 1024} */
+  /* twist merged into the passes per parity h (pbs_fft2k.hip): zeta^{2 m + h} = zeta^{2 L + h} zeta^{128 e}
+   * for m = L + 64 e; the slot constant zeta^{128 e} multiplies before pass A, zeta^{2 L + h} rides in pass
+   * A's table; inverse: zeta^{2 (n0 + 8 n1) + h} in pass B''s table, conj(zeta^{128 e}) after pass A' */
+  or_c64 twA[2][8][64];     /* zeta^{L (8 e + 2) + h} */
+  or_c64 twI[2][8][64];     /* zeta^{(n0 + 8 e)(8 k0 + 2) + h}, L = n0 + 8 k0 */
 } fft2k_tab;
 static fft2k_tab g_tab2k;
 static int g_tab2k_ready = 0;
@@ -254,6 +254,13 @@ static const fft2k_tab* tab2k(void) {
         for (int q = 0; q < 4; q++)
           for (int L = 0; L < 64; L++)
             or_fft_twiddle((uint32_t)kdev(L, 4 * h + q), 1024, &g_tab2k.wc[h][q][L].re, &g_tab2k.wc[h][q][L].im);
+      for (uint32_t h = 0; h < 2; h++)
+        for (uint32_t e = 0; e < 8; e++)
+          for (uint32_t L = 0; L < 64; L++) {
+            or_fft_twiddle((L * (8 * e + 2) + h) % 4096, 4096, &g_tab2k.twA[h][e][L].re, &g_tab2k.twA[h][e][L].im);
+            or_fft_twiddle((((L & 7) + 8 * e) * (8 * (L >> 3) + 2) + h) % 4096, 4096, &g_tab2k.twI[h][e][L].re,
+                           &g_tab2k.twI[h][e][L].im);
+          }
       __atomic_store_n(&g_tab2k_ready, 1, __ATOMIC_RELEASE);
     }
   }
@@ -264,12 +271,12 @@ static void fft2k_fwd(const double* a, or_c64* out) {
   const fft2k_tab* T = tab2k();
   or_c64 z[2][FFT_M], E[2][FFT_M];
   for (int h = 0; h < 2; h++) {
-    for (int m = 0; m < FFT_M; m++) {
-      const int j = 2 * m + h;
+    for (int m = 0; m < FFT_M; m++) { /* m = L + 64 e: slot constant zeta^{128 e} (e > 0) */
+      const int j = 2 * m + h, e = m >> 6;
       const or_c64 v = {a[j], a[j + 2 * FFT_M]};
-      z[h][m] = cmul(v, T->twist[j].re, T->twist[j].im);
+      z[h][m] = e ? cmul(v, T->twist[128 * e].re, T->twist[128 * e].im) : v;
     }
-    dft512_fwd(z[h], E[h]);
+    dft512_fwd_tab(z[h], E[h], T->twA[h], 1);
   }
   for (int h = 0; h < 2; h++)
     for (int q = 0; q < 4; q++)
@@ -293,10 +300,10 @@ static void fft2k_inv(const or_c64* in, double* out) {
         E[1][d] = cmul(csub(lo, hi), T->wc[h][q][L].re, -T->wc[h][q][L].im);
       }
   for (int h = 0; h < 2; h++) {
-    dft512_inv(E[h], z[h]);
-    for (int m = 0; m < FFT_M; m++) {
-      const int j = 2 * m + h;
-      const or_c64 v = cmul(z[h][m], T->twist[j].re, -T->twist[j].im);
+    dft512_inv_tab(E[h], z[h], T->twI[h]);
+    for (int m = 0; m < FFT_M; m++) { /* conj(zeta^{128 e}) after pass A' (e > 0) */
+      const int j = 2 * m + h, e = m >> 6;
+      const or_c64 v = e ? cmul(z[h][m], T->twist[128 * e].re, -T->twist[128 * e].im) : z[h][m];
       out[j] = v.re;
       out[j + 2 * FFT_M] = v.im;
     }
@@ -313,7 +320,7 @@ void or_fft_fwd(const double* a, uint32_t N, or_c64* out) {
     const int e = j >> 6;
     z[j] = e ? cmul(v, T->twist[64 * e].re, T->twist[64 * e].im) : v;
   }
-  dft512_fwd_m(z, out, 1);
+  dft512_fwd_tab(z, out, T->twAm, 1);
 }
 
 void or_fft_inv(const or_c64* in, uint32_t N, double* out) {
@@ -321,7 +328,7 @@ void or_fft_inv(const or_c64* in, uint32_t N, double* out) {
   if (N != 2 * FFT_M) abort();
   const fft_tab* T = tab();
   or_c64 z[FFT_M];
-  dft512_inv_m(in, z, 1);
+  dft512_inv_tab(in, z, T->twIm);
   for (int j = 0; j < FFT_M; j++) { /* conj(zeta^{64 e}) after pass A' (e > 0); conj(zeta^L) rode in pass B' */
     const int e = j >> 6;
     const or_c64 v = e ? cmul(z[j], T->twist[64 * e].re, -T->twist[64 * e].im) : z[j];

@@ -457,7 +457,7 @@ int shard_init(tfhe_ctx* c, shard& s) {
     std::vector<double> tw(p.N == 2048 ? fft2k_tables_len() : fft_tables_len());
     if (p.N == 2048) make_fft2k_tables(tw.data());
     else make_fft_tables(tw.data());
-    if (p.N != 2048 && !fft_slot_constants_ok())
+    if (!fft_slot_constants_ok())
       return fail(TFHE_HIP_EUNSUPPORTED, "FFT64: compile-time twist constants differ from the host tables");
     HIP_TRY(hipMalloc(&s.d_tw, tw.size() * 8));
     HIP_TRY(hipMemcpy(s.d_tw, tw.data(), tw.size() * 8, hipMemcpyHostToDevice));

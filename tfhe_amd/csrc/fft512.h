@@ -109,12 +109,13 @@ struct TBase {
 
 // forward 512-point DFT: natural order in (lane L, slot e <-> L + 64 e), device order out.
 // TW0: pass A multiplies slot 0 too (the N = 1024 tables fold the lane part of the twist into pass A)
+// (twA / twB: the pass A / pass B tables, 512 complex each, [64 e + L])
 template <bool TW0 = false>
-__device__ __forceinline__ void dft512_fwd(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
-                                           const double2* tw) {
+__device__ __forceinline__ void dft512_fwd_t(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
+                                             const double2* twA, const double2* twB) {
   dft8<false>(xr, xi);
 #pragma unroll
-  for (int e = TW0 ? 0 : 1; e < 8; e++) cmul<false>(xr[e], xi[e], tw[TW_A + 64 * e + lane]);
+  for (int e = TW0 ? 0 : 1; e < 8; e++) cmul<false>(xr[e], xi[e], twA[64 * e + lane]);
 #pragma unroll
   for (int e = 0; e < 8; e++) T[lane + S1 * e] = make_double2(xr[e], xi[e]);
   lds_order();
@@ -127,7 +128,7 @@ __device__ __forceinline__ void dft512_fwd(double (&xr)[8], double (&xi)[8], dou
   lds_order();
   dft8<false>(xr, xi);
 #pragma unroll
-  for (int e = 1; e < 8; e++) cmul<false>(xr[e], xi[e], tw[TW_B + 64 * e + lane]);
+  for (int e = 1; e < 8; e++) cmul<false>(xr[e], xi[e], twB[64 * e + lane]);
 #pragma unroll
   for (int e = 0; e < 8; e++) T[lane + S2 * e] = make_double2(xr[e], xi[e]);
   lds_order();
@@ -141,12 +142,19 @@ __device__ __forceinline__ void dft512_fwd(double (&xr)[8], double (&xi)[8], dou
   dft8<false>(xr, xi);
 }
 
-// inverse (no 1/M): device order in, natural order out — the forward's passes reversed
-__device__ __forceinline__ void dft512_inv(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
+template <bool TW0 = false>
+__device__ __forceinline__ void dft512_fwd(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
                                            const double2* tw) {
+  dft512_fwd_t<TW0>(xr, xi, T, lane, tb, tw + TW_A, tw + TW_B);
+}
+
+// inverse (no 1/M): device order in, natural order out — the forward's passes reversed
+// (twB / twI: the pass C' / pass B' tables)
+__device__ __forceinline__ void dft512_inv_t(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
+                                             const double2* twB, const double2* twI) {
   dft8<true>(xr, xi);
 #pragma unroll
-  for (int e = 1; e < 8; e++) cmul<true>(xr[e], xi[e], tw[TW_B + 64 * e + lane]);
+  for (int e = 1; e < 8; e++) cmul<true>(xr[e], xi[e], twB[64 * e + lane]);
 #pragma unroll
   for (int e = 0; e < 8; e++) T[tb.b2 + e] = make_double2(xr[e], xi[e]);
   lds_order();
@@ -159,7 +167,7 @@ __device__ __forceinline__ void dft512_inv(double (&xr)[8], double (&xi)[8], dou
   lds_order();
   dft8<true>(xr, xi);
 #pragma unroll
-  for (int e = 0; e < 8; e++) cmul<true>(xr[e], xi[e], tw[TW_I + 64 * e + lane]);
+  for (int e = 0; e < 8; e++) cmul<true>(xr[e], xi[e], twI[64 * e + lane]);
 #pragma unroll
   for (int e = 0; e < 8; e++) T[tb.b1 + 8 * e] = make_double2(xr[e], xi[e]);
   lds_order();
@@ -173,6 +181,11 @@ __device__ __forceinline__ void dft512_inv(double (&xr)[8], double (&xi)[8], dou
   dft8<true>(xr, xi);
 }
 
+__device__ __forceinline__ void dft512_inv(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
+                                           const double2* tw) {
+  dft512_inv_t(xr, xi, T, lane, tb, tw + TW_B, tw + TW_I);
+}
+
 // ---------------------------------------------------------------------------------------------
 // N = 1024 (P-GATE) merged twist.  z_j = a_j zeta^j with j = L + 64 e splits as zeta^L * zeta^(64 e): the
 // slot part c_e = zeta^(64 e) is a per-slot constant (an SGPR operand, no table read) applied before
@@ -181,6 +194,8 @@ __device__ __forceinline__ void dft512_inv(double (&xr)[8], double (&xi)[8], dou
 // image: zeta^(n0 + 8 n1) rides in pass B''s table (TW_I[e][L] = zeta^((n0 + 8 e)(4 k0 + 1)), L = n0 + 8
 // k0), conj(c_e) is applied after pass A'.  Saves 15 of the 54 LDS reads of a forward digit transform
 // and 8 of an inverse (oracle/fft_oracle.c: or_fft_fwd / or_fft_inv at N = 1024 restate the order).
+// N = 2048 (pbs_fft2k.hip) does the same per parity h: zeta_4096^(2 m + h) = zeta^(2 L + h) zeta^(128 e), the
+// slot constants are the same values (128 e / 4096 = 64 e / 2048), the tables A'_h, I'_h per parity.
 // The constants come from the table generator's own series, evaluated at compile time (IEEE double,
 // no contraction in constant evaluation) so they equal the host tables bit for bit.
 namespace ctw {

@@ -576,9 +576,10 @@ void make_fft_tables(double* t) {
 // the compile-time slot constants equal the table generator's zeta^(64 e) bit for bit
 bool fft_slot_constants_ok() {
   for (int e = 0; e < 8; e++) {
-    double c, s;
-    fftk::twiddle(64u * e, 2048u, &c, &s);
-    if (c != fftk::ctw::SLOT[e].x || s != fftk::ctw::SLOT[e].y) return false;
+    double c, s, c2, s2;
+    fftk::twiddle(64u * e, 2048u, &c, &s);      // N = 1024
+    fftk::twiddle(128u * e, 4096u, &c2, &s2);   // N = 2048
+    if (c != fftk::ctw::SLOT[e].x || s != fftk::ctw::SLOT[e].y || c2 != c || s2 != s) return false;
   }
   return true;
 }

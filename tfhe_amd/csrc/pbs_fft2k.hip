@@ -13,7 +13,7 @@
 // Blind rotation: workgroup = 4 ciphertexts x 2 waves.  LDS (152 KB of a gfx950 CU's 160):
 //   T   8 x 9,216 B   per-wave transpose scratch; a pair's two regions also hold the 2048-u64
 //                     rotation image and the combine / uncombine exchanges
-//   tw  48 KB         all tables: 512-point passes A | B | I, twist (both parities), combine
+//   tw  48 KB         all tables: pass A'/B' per parity (twist merged in), pass B, combine
 //   K   2 x 16 KB     BSK_i[c][0..1] of the component in flight, loaded by global_load_lds one phase
 //                     ahead (K_{1,*} during component 1's rotation and transform, K_{0,*} of the next
 //                     CMUX during the inverse transforms), published by the transform's barriers
@@ -29,11 +29,11 @@ namespace fft2k {
 using namespace fftk;
 
 constexpr int N2 = 2048, M2 = 1024;
-// table (complex, the same layout in global memory and in LDS): twist of parity 0 | pass tables A | B | I
-// at fft512.h's TW_A / TW_B / TW_I (so the pass-table base is the table itself: no negative LDS offsets)
-// | twist of parity 1 | combine twiddles [h][q][L]
-constexpr int G_TW0 = 0, G_PASS = TW_A, G_TW1 = 2048, G_WC = 2560, G_C64 = 3072;
-static_assert(TW_A == 512 && TW_B == 1024 && TW_I == 1536, "fft512.h pass-table offsets");
+// table (complex, the same layout in global memory and in LDS), the twist merged into the passes per
+// parity h (fft512.h, "merged twist"): pass A'_0 | A'_1 | B | pass B' I'_0 | I'_1 | combine [h][q][L]
+//   A'_h[e][L] = zeta^(L (8 e + 2) + h),  I'_h[e][L] = zeta^((n0 + 8 e)(8 k0 + 2) + h) (L = n0 + 8 k0),
+//   zeta = e^(2 pi i / 4096); B as the 512-point tables of fft512.h
+constexpr int G_A0 = 0, G_A1 = 512, G_B = 1024, G_I0 = 1536, G_I1 = 2048, G_WC = 2560, G_C64 = 3072;
 constexpr int F2_PAIRS = 4, F2_WAVES = 8, F2_THREADS = 64 * F2_WAVES;
 constexpr int CHUNK_GLDS = M2 * 16 / 1024;  // 1 KB wave-instructions per BSK polynomial (16)
 
@@ -76,12 +76,10 @@ __device__ __forceinline__ void pair_sync() {
 // (slot s: frequency k'(L, 4h + (s & 3)) + 512 (s >> 2)).  Contains two pair barriers: every wave of
 // the workgroup calls it in lockstep.  T0 / T1: the pair's regions (wave 0 / wave 1).
 __device__ __forceinline__ void fwd_half(double (&xr)[8], double (&xi)[8], int h, int lane, TBase tb,
-                                         double2* T0, double2* T1, const double2* twp, const double2* tg) {
+                                         double2* T0, double2* T1, const double2* tg) {
   double2* Tm = h ? T1 : T0;
-  const double2* twist = tg + (h ? G_TW1 : G_TW0);
-#pragma unroll
-  for (int e = 0; e < 8; e++) cmul<false>(xr[e], xi[e], twist[64 * e + lane]);
-  dft512_fwd(xr, xi, Tm, lane, tb, twp);
+  twist_slots<false>(xr, xi);
+  dft512_fwd_t<true>(xr, xi, Tm, lane, tb, tg + (h ? G_A1 : G_A0), tg + G_B);
 #pragma unroll
   for (int e = 0; e < 8; e++) Tm[64 * e + lane] = make_double2(xr[e], xi[e]);
   pair_sync();
@@ -125,11 +123,9 @@ __device__ __forceinline__ void inv_exchange(double (&xr)[8], double (&xi)[8], i
 
 // inverse, second half (wave-private): 512-point inverse + untwist -> reals (slot e < 8: re, e + 8: im)
 __device__ __forceinline__ void inv_half(double (&xr)[8], double (&xi)[8], int h, int lane, TBase tb, double2* Tm,
-                                         const double2* twp, const double2* tg) {
-  dft512_inv(xr, xi, Tm, lane, tb, twp);
-  const double2* twist = tg + (h ? G_TW1 : G_TW0);
-#pragma unroll
-  for (int e = 0; e < 8; e++) cmul<true>(xr[e], xi[e], twist[64 * e + lane]);
+                                         const double2* tg) {
+  dft512_inv_t(xr, xi, Tm, lane, tb, tg + G_B, tg + (h ? G_I1 : G_I0));
+  twist_slots<true>(xr, xi);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -145,7 +141,7 @@ __global__ __launch_bounds__(128) void fwd2k_kernel(const u64* __restrict__ in, 
     xr[e] = i64_to_f64(src[coef(h, lane, e)]);
     xi[e] = i64_to_f64(src[coef(h, lane, e + 8)]);
   }
-  fwd_half(xr, xi, h, lane, TBase(lane), T[0], T[1], tg + G_PASS - TW_A, tg);
+  fwd_half(xr, xi, h, lane, TBase(lane), T[0], T[1], tg);
   double2* dst = out + (size_t)blockIdx.x * M2 + h * 512;
 #pragma unroll
   for (int s = 0; s < 8; s++) dst[64 * s + lane] = make_double2(xr[s] * scale, xi[s] * scale);
@@ -164,7 +160,7 @@ __global__ __launch_bounds__(128) void inv2k_kernel(const double2* __restrict__ 
     xi[s] = v.y;
   }
   inv_exchange(xr, xi, h, lane, T[0], T[1], tg);
-  inv_half(xr, xi, h, lane, TBase(lane), T[h], tg + G_PASS - TW_A, tg);
+  inv_half(xr, xi, h, lane, TBase(lane), T[h], tg);
   double* dst = out + (size_t)blockIdx.x * N2;
 #pragma unroll
   for (int e = 0; e < 8; e++) {
@@ -334,7 +330,6 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
   double2* Tm = sh.T[wave];
   u64* R = (u64*)T0;  // 16 KB across the pair's two regions
   const double2* tt = sh.tw;
-  const double2* twp = sh.tw + G_PASS - TW_A;
   const TBase tb(lane);
 
   for (int q = threadIdx.x; q < G_C64; q += F2_THREADS) sh.tw[q] = tg[q];
@@ -382,7 +377,7 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
       d0r[e] = (double)dg[e];
       d0i[e] = (double)dg[e + 8];
     }
-    fwd_half(d0r, d0i, h, lane, tb, T0, T1, twp, tt);
+    fwd_half(d0r, d0i, h, lane, tb, T0, T1, tt);
     rotate_decompose(accB, a, h, lane, R, dg);
 #pragma unroll
     for (int e = 0; e < 8; e++) {
@@ -390,12 +385,12 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
       xi[e] = (double)dg[e + 8];
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's share of column 0; fwd_half's barriers publish it
-    fwd_half(xr, xi, h, lane, tb, T0, T1, twp, tt);
+    fwd_half(xr, xi, h, lane, tb, T0, T1, tt);
     mac_column(kbase(&sh.K[0][0], h, lane), d0r, d0i, xr, xi, o0r, o0i);
     __syncthreads();  // every wave is done with column 0
     load_column(bsk, i, 1, &sh.K[0][0], wave_s, lane);  // column 1, under the first inverse
     inv_exchange(o0r, o0i, h, lane, T0, T1, tt);
-    inv_half(o0r, o0i, h, lane, tb, Tm, twp, tt);
+    inv_half(o0r, o0i, h, lane, tb, Tm, tt);
 #pragma unroll
     for (int e = 0; e < 8; e++) {
       accA[e] += f64_to_torus_wide(o0r[e]);
@@ -409,7 +404,7 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
       __syncthreads();  // every wave is done with column 1 (and with the partner's transpose region)
       if (i + 1 < n) load_column(bsk, i + 1, 0, &sh.K[0][0], wave_s, lane);
       inv_exchange(o1r, o1i, h, lane, T0, T1, tt);
-      inv_half(o1r, o1i, h, lane, tb, Tm, twp, tt);
+      inv_half(o1r, o1i, h, lane, tb, Tm, tt);
 #pragma unroll
       for (int e = 0; e < 8; e++) {
         accB[e] += f64_to_torus_wide(o1r[e]);
@@ -447,7 +442,7 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
       d0i[e] = (double)dg[e + 8];
     }
     F2_STAMP(1);
-    fwd_half(d0r, d0i, h, lane, tb, T0, T1, twp, tt);
+    fwd_half(d0r, d0i, h, lane, tb, T0, T1, tt);
     F2_STAMP(2);
 #if F2_ACC_AGPR
     acc_get(accB, sB);
@@ -461,7 +456,7 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     F2_STAMP(3);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's share of column 0; fwd_half's barriers publish it
     F2_STAMP(4);
-    fwd_half(xr, xi, h, lane, tb, T0, T1, twp, tt);
+    fwd_half(xr, xi, h, lane, tb, T0, T1, tt);
     F2_STAMP(5);
     double2* const kt = &sh.T[0][0];
     load_column(bsk, i, 1, kt, wave_s, lane);  // column 1 into the (now idle) transpose area, under MAC 0
@@ -475,7 +470,7 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     __syncthreads();  // every wave is done with column 1: the transpose area is free again
     F2_STAMP(8);
     inv_exchange(o0r, o0i, h, lane, T0, T1, tt);
-    inv_half(o0r, o0i, h, lane, tb, Tm, twp, tt);
+    inv_half(o0r, o0i, h, lane, tb, Tm, tt);
 #if F2_ACC_AGPR
     acc_get(accA, sA);
 #endif
@@ -491,7 +486,7 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     __syncthreads();  // the partner's inverse transposes are done with its region
     F2_STAMP(10);
     inv_exchange(o1r, o1i, h, lane, T0, T1, tt);
-    inv_half(o1r, o1i, h, lane, tb, Tm, twp, tt);
+    inv_half(o1r, o1i, h, lane, tb, Tm, tt);
 #if F2_ACC_AGPR
     acc_get(accB, sB);
 #endif
@@ -526,7 +521,7 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
       xi[e] = (double)dg[e + 8];
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's share of K_{0,*}; fwd_half's barriers publish it
-    fwd_half(xr, xi, h, lane, tb, T0, T1, twp, tt);
+    fwd_half(xr, xi, h, lane, tb, T0, T1, tt);
     {  // MAC, c = 0 (oracle order: from (0, 0)); slot s of this wave = BSK index h * 512 + 64 s + L
       lds_c64* kp = kbase(&sh.K[0][0], h, lane);
 #pragma unroll
@@ -552,7 +547,7 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
       xi[e] = (double)dg[e + 8];
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): K_{1,*}
-    fwd_half(xr, xi, h, lane, tb, T0, T1, twp, tt);
+    fwd_half(xr, xi, h, lane, tb, T0, T1, tt);
 
     {  // MAC, c = 1
       lds_c64* kp = kbase(&sh.K[0][0], h, lane);
@@ -573,7 +568,7 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     __syncthreads();  // every wave is done with K_{1,*} and with the pair exchanges
     if (i + 1 < n) load_pair(bsk, i + 1, 0, sh, wave_s, lane);
     inv_exchange(o0r, o0i, h, lane, T0, T1, tt);
-    inv_half(o0r, o0i, h, lane, tb, Tm, twp, tt);
+    inv_half(o0r, o0i, h, lane, tb, Tm, tt);
 #pragma unroll
     for (int e = 0; e < 8; e++) {
       accA[e] += f64_to_torus_wide(o0r[e]);
@@ -581,7 +576,7 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     }
     __syncthreads();  // the partner's inverse transposes are done with its region
     inv_exchange(o1r, o1i, h, lane, T0, T1, tt);
-    inv_half(o1r, o1i, h, lane, tb, Tm, twp, tt);
+    inv_half(o1r, o1i, h, lane, tb, Tm, tt);
 #pragma unroll
     for (int e = 0; e < 8; e++) {
       accB[e] += f64_to_torus_wide(o1r[e]);
@@ -645,7 +640,6 @@ __global__ __launch_bounds__(F2L_THREADS, 1) void blind_rotate_fft2k_lat_kernel(
   const u64* ct = lwe_in + b * (size_t)(n + 1);
   const TBase tb(lane);
   const double2* tt = sh.tw;
-  const double2* twp = sh.tw + G_PASS - TW_A;
   double2* O = sh.T[0];  // 2 x 1024 complex across the four transpose areas
 
   for (int q = threadIdx.x; q < G_C64; q += F2L_THREADS) sh.tw[q] = tg[q];
@@ -693,9 +687,9 @@ __global__ __launch_bounds__(F2L_THREADS, 1) void blind_rotate_fft2k_lat_kernel(
           if (u == 0) xr[e] = dv;
           else xi[e] = dv;
         }
-        cmul<false>(xr[e], xi[e], tt[(h ? G_TW1 : G_TW0) + 64 * e + lane]);
       }
-      dft512_fwd(xr, xi, sh.T[wave], lane, tb, twp);
+      twist_slots<false>(xr, xi);
+      dft512_fwd_t<true>(xr, xi, sh.T[wave], lane, tb, tt + (h ? G_A1 : G_A0), tt + G_B);
 #pragma unroll
       for (int e = 0; e < 8; e++) sh.T[wave][64 * e + lane] = make_double2(xr[e], xi[e]);
     }
@@ -751,7 +745,7 @@ __global__ __launch_bounds__(F2L_THREADS, 1) void blind_rotate_fft2k_lat_kernel(
     }
     __syncthreads();  // O is read before the inverse transposes overwrite the areas
     if (wave < 4) {
-      inv_half(xr, xi, h, lane, tb, sh.T[wave], twp, tt);
+      inv_half(xr, xi, h, lane, tb, sh.T[wave], tt);
       u64* acc = sh.A[c];
 #pragma unroll
       for (int e = 0; e < 8; e++) {
@@ -800,14 +794,13 @@ void make_fft2k_tables(double* t) {
   for (uint32_t e = 0; e < 8; e++)
     for (uint32_t L = 0; L < 64; L++) {
       const int q = 64 * e + L;
-      fft_twiddle((L * e) % Mh, Mh, &t[2 * (fftk::TW_A + q)], &t[2 * (fftk::TW_A + q) + 1]);
-      fft_twiddle((8 * (L & 7) * e) % Mh, Mh, &t[2 * (fftk::TW_B + q)], &t[2 * (fftk::TW_B + q) + 1]);
-      fft_twiddle(((L >> 3) * ((L & 7) + 8 * e)) % Mh, Mh, &t[2 * (fftk::TW_I + q)], &t[2 * (fftk::TW_I + q) + 1]);
+      fft_twiddle((8 * (L & 7) * e) % Mh, Mh, &t[2 * (G_B + q)], &t[2 * (G_B + q) + 1]);
+      for (uint32_t h = 0; h < 2; h++) {
+        const int a = (h ? G_A1 : G_A0) + q, i = (h ? G_I1 : G_I0) + q;
+        fft_twiddle((L * (8 * e + 2) + h) % 4096, 4096, &t[2 * a], &t[2 * a + 1]);
+        fft_twiddle((((L & 7) + 8 * e) * (8 * (L >> 3) + 2) + h) % 4096, 4096, &t[2 * i], &t[2 * i + 1]);
+      }
     }
-  for (uint32_t m = 0; m < 512; m++) {
-    fft_twiddle(2 * m, 4096, &t[2 * (G_TW0 + m)], &t[2 * (G_TW0 + m) + 1]);
-    fft_twiddle(2 * m + 1, 4096, &t[2 * (G_TW1 + m)], &t[2 * (G_TW1 + m) + 1]);
-  }
   for (int h = 0; h < 2; h++)
     for (int q = 0; q < 4; q++)
       for (int L = 0; L < 64; L++) {
