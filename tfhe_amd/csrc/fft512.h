@@ -186,6 +186,47 @@ __device__ __forceinline__ void dft512_inv(double (&xr)[8], double (&xi)[8], dou
   dft512_inv_t(xr, xi, T, lane, tb, tw + TW_B, tw + TW_I);
 }
 
+// this lane's inverse twiddles (pass C' slots 1..7, pass B' slots 0..7) in registers, for back-to-back inverses
+struct InvTw {
+  double2 b[8], i[8];
+  __device__ __forceinline__ void load(const double2* tw, int lane) {
+#pragma unroll
+    for (int e = 1; e < 8; e++) b[e] = tw[TW_B + 64 * e + lane];
+#pragma unroll
+    for (int e = 0; e < 8; e++) i[e] = tw[TW_I + 64 * e + lane];
+  }
+};
+__device__ __forceinline__ void dft512_inv_r(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
+                                             const InvTw& w) {
+  dft8<true>(xr, xi);
+#pragma unroll
+  for (int e = 1; e < 8; e++) cmul<true>(xr[e], xi[e], w.b[e]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[tb.b2 + e] = make_double2(xr[e], xi[e]);
+  lds_order();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[lane + S2 * e];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  lds_order();
+  dft8<true>(xr, xi);
+#pragma unroll
+  for (int e = 0; e < 8; e++) cmul<true>(xr[e], xi[e], w.i[e]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[tb.b1 + 8 * e] = make_double2(xr[e], xi[e]);
+  lds_order();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[lane + S1 * e];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  lds_order();
+  dft8<true>(xr, xi);
+}
+
 // ---------------------------------------------------------------------------------------------
 // N = 1024 (P-GATE) merged twist.  z_j = a_j zeta^j with j = L + 64 e splits as zeta^L * zeta^(64 e): the
 // slot part c_e = zeta^(64 e) is a per-slot constant (an SGPR operand, no table read) applied before

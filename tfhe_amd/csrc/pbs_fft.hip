@@ -144,6 +144,10 @@ __global__ __launch_bounds__(64) void fft_inv_kernel(const double2* __restrict__
 #ifndef FFT_KBUF
 #define FFT_KBUF 2
 #endif
+// FFT_INVTW: the two inverse transforms of a CMUX share one read of the inverse twiddles (registers)
+#ifndef FFT_INVTW
+#define FFT_INVTW 1
+#endif
 constexpr int FB_WAVES = 8;
 constexpr int FB_THREADS = 64 * FB_WAVES;
 constexpr int CHUNK_C64 = 2 * M;                   // one level step: rows (c, l), j = 0, 1 (16 KB)
@@ -331,9 +335,31 @@ __global__ __launch_bounds__(FB_THREADS, 1) void blind_rotate_fft_kernel(
     FS_STAMP(7);
     ext_prod_component(accA, rbase, 0, i, n_steps, sh, T, wave, lane, tb, bsk, o0r, o0i, o1r, o1i FS_PASS);
     ext_prod_component(accB, rbase, 1, i, n_steps, sh, T, wave, lane, tb, bsk, o0r, o0i, o1r, o1i FS_PASS);
+#if FFT_INVTW
+    {  // both inverses with the twiddles read once
+      InvTw w;
+      w.load(sh.tw, lane);
+      dft512_inv_r(o0r, o0i, T, lane, tb, w);
+      twist_slots<true>(o0r, o0i);
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        accA[e] += f64_to_torus(o0r[e]);
+        accA[e + 8] += f64_to_torus(o0i[e]);
+      }
+      FS_STAMP(5);
+      dft512_inv_r(o1r, o1i, T, lane, tb, w);
+      twist_slots<true>(o1r, o1i);
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        accB[e] += f64_to_torus(o1r[e]);
+        accB[e + 8] += f64_to_torus(o1i[e]);
+      }
+    }
+#else
     accumulate(accA, o0r, o0i, T, lane, tb, sh.tw);
     FS_STAMP(5);
     accumulate(accB, o1r, o1i, T, lane, tb, sh.tw);
+#endif
     FS_STAMP(6);
   }
 #if FFT_STAMPS
