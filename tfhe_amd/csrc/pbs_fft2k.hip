@@ -75,50 +75,68 @@ __device__ __forceinline__ void pair_sync() {
 // forward: 16 reals per lane (slot e < 8 real part, e + 8 imaginary part) -> half spectrum in xr/xi
 // (slot s: frequency k'(L, 4h + (s & 3)) + 512 (s >> 2)).  Contains two pair barriers: every wave of
 // the workgroup calls it in lockstep.  T0 / T1: the pair's regions (wave 0 / wave 1).
+// The exchange moves only what the partner needs: wave h combines at slots 4h + q, so wave 0 sends E_0 at
+// slots 4..7 and wave 1 sends E_1 at slots 0..3 (4 writes and 4 reads per wave; its own 4 stay in registers).
+template <int H>
+__device__ __forceinline__ void combine_fwd(double (&xr)[8], double (&xi)[8], int lane, double2* Tm,
+                                            const double2* Tp, const double2* tg) {
+#pragma unroll
+  for (int q = 0; q < 4; q++) Tm[64 * (4 * (1 - H) + q) + lane] = make_double2(xr[4 * (1 - H) + q], xi[4 * (1 - H) + q]);
+  pair_sync();
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int e = 4 * H + q;
+    const double2 p = Tp[64 * e + lane];
+    const double e0r = H ? p.x : xr[e], e0i = H ? p.y : xi[e];
+    double tr = H ? xr[e] : p.x, ti = H ? xi[e] : p.y;
+    cmul<false>(tr, ti, tg[G_WC + 256 * H + 64 * q + lane]);
+    xr[q] = e0r + tr;
+    xi[q] = e0i + ti;
+    xr[q + 4] = e0r - tr;
+    xi[q + 4] = e0i - ti;
+  }
+  pair_sync();
+}
 __device__ __forceinline__ void fwd_half(double (&xr)[8], double (&xi)[8], int h, int lane, TBase tb,
                                          double2* T0, double2* T1, const double2* tg) {
   double2* Tm = h ? T1 : T0;
   twist_slots<false>(xr, xi);
   dft512_fwd_t<true>(xr, xi, Tm, lane, tb, tg + (h ? G_A1 : G_A0), tg + G_B);
-#pragma unroll
-  for (int e = 0; e < 8; e++) Tm[64 * e + lane] = make_double2(xr[e], xi[e]);
-  pair_sync();
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const int e = 4 * h + q;
-    const double2 e0 = T0[64 * e + lane], e1 = T1[64 * e + lane];
-    double tr = e1.x, ti = e1.y;
-    cmul<false>(tr, ti, tg[G_WC + 256 * h + 64 * q + lane]);
-    xr[q] = e0.x + tr;
-    xi[q] = e0.y + ti;
-    xr[q + 4] = e0.x - tr;
-    xi[q + 4] = e0.y - ti;
-  }
-  pair_sync();
+  if (__builtin_amdgcn_readfirstlane(h)) combine_fwd<1>(xr, xi, lane, T1, T0, tg);
+  else combine_fwd<0>(xr, xi, lane, T0, T1, tg);
 }
 
-// inverse, first half: uncombine this wave's 4 slot pairs into the pair's exchange (E_0 -> T0,
-// E_1 -> T1, slot 4h + q), then each wave reads its full E_h.  Two pair barriers.
-__device__ __forceinline__ void inv_exchange(double (&xr)[8], double (&xi)[8], int h, int lane, double2* T0,
-                                             double2* T1, const double2* tg) {
+// inverse, first half: uncombine this wave's 4 slot pairs (slot 4h + q) into E_0 and E_1; keep E_h, send
+// E_(1-h) to the partner through this wave's region, take the partner's E_h at slots 4(1-h) + q.  Two
+// pair barriers.
+template <int H>
+__device__ __forceinline__ void uncombine_inv(double (&xr)[8], double (&xi)[8], int lane, double2* Tm,
+                                              const double2* Tp, const double2* tg) {
 #pragma unroll
   for (int q = 0; q < 4; q++) {
-    const int e = 4 * h + q;
+    const int e = 4 * H + q;
     const double lr = xr[q], li = xi[q], hr = xr[q + 4], hi = xi[q + 4];
     double dr = lr - hr, di = li - hi;
-    cmul<true>(dr, di, tg[G_WC + 256 * h + 64 * q + lane]);
-    T0[64 * e + lane] = make_double2(lr + hr, li + hi);
-    T1[64 * e + lane] = make_double2(dr, di);
+    cmul<true>(dr, di, tg[G_WC + 256 * H + 64 * q + lane]);
+    const double sr = lr + hr, si = li + hi;  // E_0 at slot e; (dr, di) = E_1 at slot e
+    Tm[64 * e + lane] = H ? make_double2(sr, si) : make_double2(dr, di);
+    xr[e] = H ? dr : sr;
+    xi[e] = H ? di : si;
   }
   pair_sync();
-  const double2* Tm = h ? T1 : T0;
 #pragma unroll
-  for (int e = 0; e < 8; e++) {
-    const double2 v = Tm[64 * e + lane];
+  for (int q = 0; q < 4; q++) {
+    const int e = 4 * (1 - H) + q;
+    const double2 v = Tp[64 * e + lane];
     xr[e] = v.x;
     xi[e] = v.y;
   }
   pair_sync();
+}
+__device__ __forceinline__ void inv_exchange(double (&xr)[8], double (&xi)[8], int h, int lane, double2* T0,
+                                             double2* T1, const double2* tg) {
+  if (__builtin_amdgcn_readfirstlane(h)) uncombine_inv<1>(xr, xi, lane, T1, T0, tg);
+  else uncombine_inv<0>(xr, xi, lane, T0, T1, tg);
 }
 
 // inverse, second half (wave-private): 512-point inverse + untwist -> reals (slot e < 8: re, e + 8: im)
