@@ -50,6 +50,26 @@ __device__ __forceinline__ u64 addm(u64 a, u64 b, u64 p) {
 }
 __device__ __forceinline__ u64 subm(u64 a, u64 b, u64 p) { return a >= b ? a - b : a + (p - b); }
 
+// The two primes as compile-time constants (prime-specialised Montgomery: with p = 2^64 - 2^a + 1 a
+// constant, the m * p product folds into shifts and adds — 21 instead of 30 VALU per product,
+// measured on the ISA); P_Q / PINV_Q equal SnsConst.p / pinv_neg (make_sns_const, checked there)
+template <int Q>
+struct Prime;
+template <>
+struct Prime<0> {
+  static constexpr u64 p = 0xFFFFFFFF00000001ull, pinv = 0xFFFFFFFEFFFFFFFFull;
+};
+template <>
+struct Prime<1> {
+  static constexpr u64 p = 0xFFFFFFFC00000001ull, pinv = 0xFFFFFFFBFFFFFFFFull;
+};
+template <int Q>
+__device__ __forceinline__ u64 mont_q(u64 a, u64 b) { return mont(a, b, Prime<Q>::p, Prime<Q>::pinv); }
+template <int Q>
+__device__ __forceinline__ u64 addm_q(u64 a, u64 b) { return addm(a, b, Prime<Q>::p); }
+template <int Q>
+__device__ __forceinline__ u64 subm_q(u64 a, u64 b) { return subm(a, b, Prime<Q>::p); }
+
 __device__ __forceinline__ u128 mulhi128(u128 x, u128 y) {
   const u64 x0 = (u64)x, x1 = (u64)(x >> 64), y0 = (u64)y, y1 = (u64)(y >> 64);
   const u128 p00 = (u128)x0 * y0, p01 = (u128)x0 * y1, p10 = (u128)x1 * y0, p11 = (u128)x1 * y1;
@@ -59,41 +79,129 @@ __device__ __forceinline__ u128 mulhi128(u128 x, u128 y) {
 
 // residues -> x in [0, Q) -> torus y = x + floor((x c + 2^127) / 2^128)
 __device__ __forceinline__ u128 lift_to_torus(u64 r1, u64 r2, const SnsConst& K) {
-  const u64 p1 = K.p[0], p2 = K.p[1];
+  constexpr u64 p1 = Prime<0>::p, p2 = Prime<1>::p;
   const u64 r1m = r1 >= p2 ? r1 - p2 : r1;
-  const u64 t = mont(subm(r2, r1m, p2), K.p1inv_m, p2, K.pinv_neg[1]);
+  const u64 t = mont_q<1>(subm_q<1>(r2, r1m), K.p1inv_m);
   const u128 x = (u128)r1 + (u128)p1 * t;
   const u128 c = ((u128)K.conv_hi << 64) | K.conv_lo;
   const u128 lo = x * c;
   return x + mulhi128(x, c) + (u128)((lo >> 127) & 1);
 }
 
-__device__ void ntt_fwd_lds(u64* a, const u64* tw, u64 p, u64 pinv) {
-  for (int m = 1, t = SN / 2; m < SN; m <<= 1, t >>= 1) {
-    for (int b = threadIdx.x; b < SN / 2; b += ST) {
-      const int i = b / t, j = 2 * i * t + (b % t);
-      const u64 S = tw[m + i];
-      const u64 U = a[j], V = mont(a[j + t], S, p, pinv);
-      a[j] = addm(U, V, p);
-      a[j + t] = subm(U, V, p);
-    }
-    __syncthreads();
-  }
+// Negacyclic NTTs of 2048 points in LDS by 256 threads, the radix-2 stages grouped in registers: each
+// thread takes an 8-element set closed under 3 consecutive stages (7 twiddles), so a transform is 4 LDS
+// passes and 4 barriers instead of 11 (the last / first pass of 2 stages takes two 4-element sets).
+// Cooley-Tukey forward (psi_rev, natural -> bit-reversed) and Gentleman-Sande inverse (ipsi_rev,
+// bit-reversed -> natural, N^-1 folded into the last pass); the same butterflies as the stage-by-stage
+// form, so the same exact residues.
+template <int Q>
+__device__ __forceinline__ void ct_bfly(u64& u, u64& v, u64 S) {
+  const u64 V = mont_q<Q>(v, S);
+  v = subm_q<Q>(u, V);
+  u = addm_q<Q>(u, V);
+}
+template <int Q>
+__device__ __forceinline__ void gs_bfly(u64& u, u64& v, u64 S) {
+  const u64 U = u, V = v;
+  u = addm_q<Q>(U, V);
+  v = mont_q<Q>(subm_q<Q>(U, V), S);
 }
 
-__device__ void ntt_inv_lds(u64* a, const u64* itw, u64 ninv, u64 p, u64 pinv) {
-  for (int m = SN / 2, t = 1; m >= 1; m >>= 1, t <<= 1) {
-    for (int b = threadIdx.x; b < SN / 2; b += ST) {
-      const int i = b / t, j = 2 * i * t + (b % t);
-      const u64 S = itw[m + i];
-      const u64 U = a[j], V = a[j + t];
-      a[j] = addm(U, V, p);
-      a[j + t] = mont(subm(U, V, p), S, p, pinv);
-    }
-    __syncthreads();
-  }
-  for (int x = threadIdx.x; x < SN; x += ST) a[x] = mont(a[x], ninv, p, pinv);
+// CT stages (m, t), (2m, t/2), (4m, t/4) on the set 2 i t + j + k t/4, k < 8
+template <int Q, int M, int T>
+__device__ __forceinline__ void ct_pass3(u64* a, const u64* __restrict__ tw) {
+  constexpr int Q4 = T / 4;
+  const int th = threadIdx.x, i = th / Q4, j = th % Q4;
+  u64* base = a + 2 * i * T + j;
+  u64 x[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) x[k] = base[k * Q4];
+  const u64 s1 = tw[M + i], s2a = tw[2 * M + 2 * i], s2b = tw[2 * M + 2 * i + 1];
+  const u64 s3[4] = {tw[4 * M + 4 * i], tw[4 * M + 4 * i + 1], tw[4 * M + 4 * i + 2], tw[4 * M + 4 * i + 3]};
+#pragma unroll
+  for (int k = 0; k < 4; k++) ct_bfly<Q>(x[k], x[k + 4], s1);
+  ct_bfly<Q>(x[0], x[2], s2a);
+  ct_bfly<Q>(x[1], x[3], s2a);
+  ct_bfly<Q>(x[4], x[6], s2b);
+  ct_bfly<Q>(x[5], x[7], s2b);
+#pragma unroll
+  for (int s = 0; s < 4; s++) ct_bfly<Q>(x[2 * s], x[2 * s + 1], s3[s]);
+#pragma unroll
+  for (int k = 0; k < 8; k++) base[k * Q4] = x[k];
   __syncthreads();
+}
+
+template <int Q>
+__device__ void ntt_fwd_lds(u64* a, const u64* tw) {
+  static_assert(SN == 2048 && ST == 256, "pass plan");
+  ct_pass3<Q, 1, 1024>(a, tw);
+  ct_pass3<Q, 8, 128>(a, tw);
+  ct_pass3<Q, 64, 16>(a, tw);
+  // stages (512, 2), (1024, 1): sets 4 i + k, k < 4, two per thread
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const int i = threadIdx.x + r * ST;
+    u64* base = a + 4 * i;
+    u64 x0 = base[0], x1 = base[1], x2 = base[2], x3 = base[3];
+    const u64 s1 = tw[512 + i];
+    ct_bfly<Q>(x0, x2, s1);
+    ct_bfly<Q>(x1, x3, s1);
+    ct_bfly<Q>(x0, x1, tw[1024 + 2 * i]);
+    ct_bfly<Q>(x2, x3, tw[1024 + 2 * i + 1]);
+    base[0] = x0;
+    base[1] = x1;
+    base[2] = x2;
+    base[3] = x3;
+  }
+  __syncthreads();
+}
+
+// GS stages (t, m), (2t, m/2), (4t, m/4) on the set 8 i t + j + k t, k < 8 (i = block index at m/4)
+template <int Q, int M, int T, bool NINV>
+__device__ __forceinline__ void gs_pass3(u64* a, const u64* __restrict__ itw, u64 ninv) {
+  const int th = threadIdx.x, i = th / T, j = th % T;
+  u64* base = a + 8 * i * T + j;
+  u64 x[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) x[k] = base[k * T];
+  const u64 s1[4] = {itw[M + 4 * i], itw[M + 4 * i + 1], itw[M + 4 * i + 2], itw[M + 4 * i + 3]};
+  const u64 s2a = itw[M / 2 + 2 * i], s2b = itw[M / 2 + 2 * i + 1], s3 = itw[M / 4 + i];
+#pragma unroll
+  for (int s = 0; s < 4; s++) gs_bfly<Q>(x[2 * s], x[2 * s + 1], s1[s]);
+  gs_bfly<Q>(x[0], x[2], s2a);
+  gs_bfly<Q>(x[1], x[3], s2a);
+  gs_bfly<Q>(x[4], x[6], s2b);
+  gs_bfly<Q>(x[5], x[7], s2b);
+#pragma unroll
+  for (int k = 0; k < 4; k++) gs_bfly<Q>(x[k], x[k + 4], s3);
+#pragma unroll
+  for (int k = 0; k < 8; k++) base[k * T] = NINV ? mont_q<Q>(x[k], ninv) : x[k];
+  __syncthreads();
+}
+
+template <int Q>
+__device__ void ntt_inv_lds(u64* a, const u64* itw, u64 ninv) {
+  static_assert(SN == 2048 && ST == 256, "pass plan");
+  // stages (t 1, m 1024), (t 2, m 512): sets 4 i + k, two per thread
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const int i = threadIdx.x + r * ST;
+    u64* base = a + 4 * i;
+    u64 x0 = base[0], x1 = base[1], x2 = base[2], x3 = base[3];
+    gs_bfly<Q>(x0, x1, itw[1024 + 2 * i]);
+    gs_bfly<Q>(x2, x3, itw[1024 + 2 * i + 1]);
+    const u64 s2 = itw[512 + i];
+    gs_bfly<Q>(x0, x2, s2);
+    gs_bfly<Q>(x1, x3, s2);
+    base[0] = x0;
+    base[1] = x1;
+    base[2] = x2;
+    base[3] = x3;
+  }
+  __syncthreads();
+  gs_pass3<Q, 256, 4, false>(a, itw, ninv);
+  gs_pass3<Q, 32, 32, false>(a, itw, ninv);
+  gs_pass3<Q, 4, 256, true>(a, itw, ninv);
 }
 
 __device__ __forceinline__ u32 mod_switch_4096(u64 x) { return (u32)(((x >> 51) + 1) >> 1) & 4095u; }
@@ -107,8 +215,13 @@ __global__ void __launch_bounds__(ST) sns_bsk_to_ntt_kernel(const u64* __restric
   const SnsConst& K = *Kc;
   for (int x = threadIdx.x; x < SN; x += ST) a[x] = in[poly * SN + x];
   __syncthreads();
-  ntt_fwd_lds(a, K.psi_rev[q], K.p[q], K.pinv_neg[q]);
-  for (int x = threadIdx.x; x < SN; x += ST) out[poly * SN + x] = mont(a[x], K.r2[q], K.p[q], K.pinv_neg[q]);
+  if (q) {
+    ntt_fwd_lds<1>(a, K.psi_rev[1]);
+    for (int x = threadIdx.x; x < SN; x += ST) out[poly * SN + x] = mont_q<1>(a[x], K.r2[1]);
+  } else {
+    ntt_fwd_lds<0>(a, K.psi_rev[0]);
+    for (int x = threadIdx.x; x < SN; x += ST) out[poly * SN + x] = mont_q<0>(a[x], K.r2[0]);
+  }
 }
 
 // acc = X^{-b~} (0, 0, lut)
@@ -132,6 +245,19 @@ __global__ void sns_init_kernel(const u64* __restrict__ lwe, int n, const u64* _
     const u64 v = lut[x];
     a[(size_t)SK * 2 * SN + (size_t)q * SN + dst] = (neg && v) ? K.p[q] - v : v;
   }
+}
+
+// one digit polynomial of step 1 in prime Q: residues, forward NTT, out
+template <int Q>
+__device__ __forceinline__ void step1_level(const int* dg, u64* buf, const SnsConst& K, u64* out) {
+  for (int t = threadIdx.x; t < SN; t += ST) {
+    const int d = dg[t];
+    buf[t] = d >= 0 ? (u64)d : Prime<Q>::p - (u64)(-d);
+  }
+  __syncthreads();
+  ntt_fwd_lds<Q>(buf, K.psi_rev[Q]);
+  for (int t = threadIdx.x; t < SN; t += ST) out[t] = buf[t];
+  __syncthreads();
 }
 
 __global__ void __launch_bounds__(ST) sns_step1_kernel(const u64* __restrict__ lwe, int n, int i,
@@ -158,8 +284,8 @@ __global__ void __launch_bounds__(ST) sns_step1_kernel(const u64* __restrict__ l
   }
   __syncthreads();
   for (int t = threadIdx.x; t < SN; t += ST) {
-    const u64 r1 = subm(rot[0][t], a[t], K.p[0]);
-    const u64 r2 = subm(rot[1][t], a[SN + t], K.p[1]);
+    const u64 r1 = subm_q<0>(rot[0][t], a[t]);
+    const u64 r2 = subm_q<1>(rot[1][t], a[SN + t]);
     // signed decomposition of the torus image: 72 bits, 3 digits of 24 (tfhe-rs SignedDecomposer)
     const u128 y = lift_to_torus(r1, r2, K);
     u128 state = ((y >> 55) + 1) >> 1;
@@ -173,39 +299,36 @@ __global__ void __launch_bounds__(ST) sns_step1_kernel(const u64* __restrict__ l
     }
   }
   __syncthreads();
-  for (int l = 0; l < SL; l++)
-    for (int q = 0; q < 2; q++) {
-      const u64 p = K.p[q];
-      for (int t = threadIdx.x; t < SN; t += ST) {
-        const int d = dig[l][t];
-        buf[t] = d >= 0 ? (u64)d : p - (u64)(-d);
-      }
-      __syncthreads();
-      ntt_fwd_lds(buf, K.psi_rev[q], p, K.pinv_neg[q]);
-      u64* out = D + (((size_t)ct * SR + c * SL + l) * 2 + q) * SN;
-      for (int t = threadIdx.x; t < SN; t += ST) out[t] = buf[t];
-      __syncthreads();
-    }
+  for (int l = 0; l < SL; l++) {
+    step1_level<0>(dig[l], buf, K, D + (((size_t)ct * SR + c * SL + l) * 2 + 0) * SN);
+    step1_level<1>(dig[l], buf, K, D + (((size_t)ct * SR + c * SL + l) * 2 + 1) * SN);
+  }
+}
+
+// step 2 for prime Q: 9-term MAC, inverse NTT, accumulate
+template <int Q>
+__device__ __forceinline__ void step2_body(const u64* __restrict__ D, const u64* __restrict__ bsk_i,
+                                           u64* __restrict__ acc, const SnsConst& K, u64* buf, int j, int ct) {
+  const u64* d = D + (size_t)ct * SR * 2 * SN + (size_t)Q * SN;
+  const u64* b = bsk_i + ((size_t)j * 2 + Q) * SN;  // [r][j][prime][N]
+  for (int t = threadIdx.x; t < SN; t += ST) {
+    u64 s = 0;
+#pragma unroll
+    for (int r = 0; r < SR; r++) s = addm_q<Q>(s, mont_q<Q>(d[(size_t)r * 2 * SN + t], b[(size_t)r * (SK + 1) * 2 * SN + t]));
+    buf[t] = s;
+  }
+  __syncthreads();
+  ntt_inv_lds<Q>(buf, K.ipsi_rev[Q], K.ninv[Q]);
+  u64* a = acc + (((size_t)ct * (SK + 1) + j) * 2 + Q) * SN;
+  for (int t = threadIdx.x; t < SN; t += ST) a[t] = addm_q<Q>(a[t], buf[t]);
 }
 
 __global__ void __launch_bounds__(ST) sns_step2_kernel(const u64* __restrict__ D, const u64* __restrict__ bsk_i,
                                                        u64* __restrict__ acc, const SnsConst* __restrict__ Kc) {
   __shared__ u64 buf[SN];
   const int q = blockIdx.x & 1, j = (blockIdx.x >> 1) % (SK + 1), ct = (blockIdx.x >> 1) / (SK + 1);
-  const SnsConst& K = *Kc;
-  const u64 p = K.p[q], pinv = K.pinv_neg[q];
-  const u64* d = D + (size_t)ct * SR * 2 * SN + (size_t)q * SN;
-  const u64* b = bsk_i + ((size_t)j * 2 + q) * SN;  // [r][j][prime][N]
-  for (int t = threadIdx.x; t < SN; t += ST) {
-    u64 s = 0;
-#pragma unroll
-    for (int r = 0; r < SR; r++) s = addm(s, mont(d[(size_t)r * 2 * SN + t], b[(size_t)r * (SK + 1) * 2 * SN + t], p, pinv), p);
-    buf[t] = s;
-  }
-  __syncthreads();
-  ntt_inv_lds(buf, K.ipsi_rev[q], K.ninv[q], p, pinv);
-  u64* a = acc + (((size_t)ct * (SK + 1) + j) * 2 + q) * SN;
-  for (int t = threadIdx.x; t < SN; t += ST) a[t] = addm(a[t], buf[t], p);
+  if (q) step2_body<1>(D, bsk_i, acc, *Kc, buf, j, ct);
+  else step2_body<0>(D, bsk_i, acc, *Kc, buf, j, ct);
 }
 
 // acc -> LWE over Z_2^128 (dim k N, + body), (lo, hi) pairs
@@ -259,6 +382,7 @@ void make_sns_const(void* out) {
     u64 inv = 1;  // p^-1 mod 2^64 by Newton
     for (int it = 0; it < 7; it++) inv *= 2 - p * inv;
     K.pinv_neg[q] = (u64)0 - inv;
+    static_assert(Prime<0>::p == 0xFFFFFFFF00000001ull && Prime<1>::p == 0xFFFFFFFC00000001ull, "SnS primes");
     const u64 R = (u64)(((u128)1 << 64) % p);
     K.r2[q] = hmul(R, R, p);
     u64 nr = 2;
