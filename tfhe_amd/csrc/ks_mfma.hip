@@ -138,6 +138,87 @@ __global__ __launch_bounds__(64 * KM_WAVES) void ks_gemm_kernel(const v4i* __res
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Packing keyswitch GEMM on the matrix cores (pks.hip's T = D x PKSK mod 2^64).
+// The digits are tfhe-rs SignedDecomposer digits at base 2^B (B <= 16): two signed bytes each,
+// d = d0 + 2^8 d1 (d0 in [-128, 127], |d1| <= 2^(B-9)), so
+//   sum_k d[k] PKSK[k][n] = sum_t 2^(8t) (D0 x S_t + D1 x S_(t-1))[n]      (mod 2^64, S_-1 = 0)
+// with S_t the key's balanced byte planes (ksk_planes_kernel, the same recoding as the keyswitch).
+// Fifteen int8 GEMMs per (row, column) tile, all exact in int32: |acc| <= K * 2 * 128 * 128 = 2^27 at
+// K = 4096.  Layouts as above: digit bytes A0 / A1[mt][ks][lane][16], planes P[nt][ks][t][lane][16].
+__global__ void pks_digits_mfma_kernel(const u64* __restrict__ lwes, size_t count, size_t rows, int in_dim, int BL,
+                                       int LV, unsigned char* __restrict__ A0, unsigned char* __restrict__ A1) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * (size_t)in_dim) return;
+  const size_t m = idx / in_dim;
+  const int j = (int)(idx % in_dim);
+  const int K = in_dim * LV, KS = K / 64;
+  const u64 x = m < count ? lwes[m * (size_t)(in_dim + 1) + j] : 0ull;
+  const int prec = BL * LV, nonrep = 64 - prec;
+  u64 state = m < count ? (((x >> (nonrep - 1)) + 1) >> 1) & ((1ull << prec) - 1) : 0ull;
+  const u64 mask = (1ull << BL) - 1;
+  for (int l = LV - 1; l >= 0; l--) {  // k = j * LV + l (level l = 0 the most significant)
+    const u64 res = state & mask;
+    state >>= BL;
+    const u64 carry = ((((res - 1) | state) & res) >> (BL - 1)) & 1;
+    state += carry;
+    const int d = (int)((long long)res - (long long)(carry << BL));
+    const int d0 = ((d + 128) & 255) - 128, d1 = (d - d0) >> 8;
+    const int k = j * LV + l;
+    const size_t off = ((m >> 4) * KS + (k >> 6)) * 1024 + frag_off((int)(m & 15), k);
+    A0[off] = (unsigned char)(signed char)d0;
+    A1[off] = (unsigned char)(signed char)d1;
+  }
+}
+
+constexpr int PM_WAVES = 4, PM_MT = 4, PM_ROWS = 16 * PM_MT * PM_WAVES;  // 256 rows x 16 columns per workgroup
+
+__global__ __launch_bounds__(64 * PM_WAVES) void pks_gemm_mfma_kernel(const v4i* __restrict__ A0,
+                                                                      const v4i* __restrict__ A1,
+                                                                      const v4i* __restrict__ P, int KS, size_t M,
+                                                                      int Nc, u64* __restrict__ T) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nt = blockIdx.x;
+  const size_t mt0 = ((size_t)blockIdx.y * PM_WAVES + wave) * PM_MT;
+  const v4i* a0 = A0 + mt0 * KS * 64 + lane;
+  const v4i* a1 = A1 + mt0 * KS * 64 + lane;
+  const v4i* p = P + (size_t)nt * KS * KM_PLANES * 64 + lane;
+  v4i acc[PM_MT][KM_PLANES];
+#pragma unroll
+  for (int m = 0; m < PM_MT; m++)
+#pragma unroll
+    for (int t = 0; t < KM_PLANES; t++) acc[m][t] = (v4i){0, 0, 0, 0};
+  for (int ks = 0; ks < KS; ks++) {
+    v4i f0[PM_MT], f1[PM_MT], bf[KM_PLANES];
+#pragma unroll
+    for (int m = 0; m < PM_MT; m++) {
+      f0[m] = a0[((size_t)m * KS + ks) * 64];
+      f1[m] = a1[((size_t)m * KS + ks) * 64];
+    }
+#pragma unroll
+    for (int t = 0; t < KM_PLANES; t++) bf[t] = p[((size_t)ks * KM_PLANES + t) * 64];
+#pragma unroll
+    for (int m = 0; m < PM_MT; m++)
+#pragma unroll
+      for (int t = 0; t < KM_PLANES; t++) {
+        acc[m][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f0[m], bf[t], acc[m][t], 0, 0, 0);
+        if (t > 0) acc[m][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f1[m], bf[t - 1], acc[m][t], 0, 0, 0);
+      }
+  }
+  const int col = nt * 16 + (lane & 15);
+#pragma unroll
+  for (int m = 0; m < PM_MT; m++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const size_t row = (mt0 + m) * 16 + 4 * (lane >> 4) + r;
+      if (row >= M) continue;
+      u64 v = 0;
+#pragma unroll
+      for (int t = 0; t < KM_PLANES; t++) v += (u64)(long long)acc[m][t][r] << (8 * t);
+      T[row * (size_t)Nc + col] = v;
+    }
+}
+
 int ks_k(int big_dim, int levels) { return big_dim * levels; }
 int ks_nt(int n) { return (n + 1 + 15) / 16; }
 size_t ks_rows(size_t B) { return (B + KM_ROWS - 1) / KM_ROWS * KM_ROWS; }
@@ -156,6 +237,26 @@ hipError_t launch_ksk_planes(const u64* ksk, int big_dim, int levels, int n, voi
   const size_t total = (size_t)K * ks_nt(n) * 16;
   hipLaunchKernelGGL(ksk_planes_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ksk, K, n, ks_nt(n),
                      (signed char*)planes);
+  return hipGetLastError();
+}
+
+size_t pks_mfma_rows(size_t count) { return (count + PM_ROWS - 1) / PM_ROWS * PM_ROWS; }
+
+// T[count][Nc] = D x PKSK (mod 2^64) on the matrix cores; A0 / A1: pks_mfma_rows(count) * in_dim * LV bytes each;
+// planes from launch_ksk_planes(pksk, in_dim, LV, Nc - 1, ...)
+hipError_t launch_pks_gemm_mfma(const u64* lwes, size_t count, int in_dim, int base_log, int LV, int Nc,
+                                const void* planes, void* A0, void* A1, u64* T, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  const int K = in_dim * LV;
+  if (K % 64 || Nc % 16 || base_log < 2 || base_log > 16 || base_log * LV >= 64 ||
+      (long long)K * 2 * 128 * 128 >= (1ll << 31))
+    return hipErrorInvalidValue;
+  const size_t rows = pks_mfma_rows(count), el = rows * (size_t)in_dim;
+  hipLaunchKernelGGL(pks_digits_mfma_kernel, dim3((unsigned)((el + 255) / 256)), dim3(256), 0, s, lwes, count, rows,
+                     in_dim, base_log, LV, (unsigned char*)A0, (unsigned char*)A1);
+  dim3 grid((unsigned)(Nc / 16), (unsigned)(rows / PM_ROWS));
+  hipLaunchKernelGGL(pks_gemm_mfma_kernel, grid, dim3(64 * PM_WAVES), 0, s, (const v4i*)A0, (const v4i*)A1,
+                     (const v4i*)planes, K / 64, count, Nc, T);
   return hipGetLastError();
 }
 

@@ -74,6 +74,12 @@ hipError_t launch_sns_extract(const u64* acc, size_t B, u64* out, const void* d_
 hipError_t launch_pks_corr(const u64* pksk, int K, int Nc, int base_log, u64* corr, hipStream_t s);
 hipError_t launch_pks_pack(const u64* lwes, size_t count, int in_dim, int base_log, int L, int k, int N, int lpg,
                            const u64* pksk, const u64* corr, u32* A, u64* T, u64* out, hipStream_t s);
+// the same on the matrix cores (ks_mfma.hip): the GEMM, then pks.hip's shift-and-sum
+size_t pks_mfma_rows(size_t count);
+hipError_t launch_pks_gemm_mfma(const u64* lwes, size_t count, int in_dim, int base_log, int LV, int Nc,
+                                const void* planes, void* A0, void* A1, u64* T, hipStream_t s);
+hipError_t launch_pks_pack_mfma(const u64* lwes, size_t count, int in_dim, int base_log, int L, int k, int N, int lpg,
+                                const void* planes, void* A0, void* A1, u64* T, u64* out, hipStream_t s);
 // modulus-switch noise reduction (ms_reduce.hip), in place on B x (n+1); picks (device, nullable)
 hipError_t launch_ms_reduce(u64* lwe, size_t B, int n, const u64* zeros, int count, int log2_2N, double bound,
                             double r_sigma, double var128, int* picks, hipStream_t s);

@@ -139,4 +139,15 @@ hipError_t launch_pks_pack(const u64* lwes, size_t count, int in_dim, int base_l
   return hipGetLastError();
 }
 
+hipError_t launch_pks_pack_mfma(const u64* lwes, size_t count, int in_dim, int base_log, int L, int k, int N, int lpg,
+                                const void* planes, void* A0, void* A1, u64* T, u64* out, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  const int Nc = (k + 1) * N;
+  hipError_t e = launch_pks_gemm_mfma(lwes, count, in_dim, base_log, L, Nc, planes, A0, A1, T, s);
+  if (e != hipSuccess) return e;
+  const size_t groups = (count + lpg - 1) / lpg, outs = groups * (size_t)Nc;
+  pks_shift_sum_kernel<<<(unsigned)((outs + 255) / 256), 256, 0, s>>>(T, lwes, count, in_dim, k, N, lpg, groups, out);
+  return hipGetLastError();
+}
+
 }  // namespace tfhe

@@ -2,6 +2,7 @@
 // key residency, workspace, chunked launches.  Kernels: pks.hip; host key material: client.cpp.
 #include <hip/hip_runtime_api.h>
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -72,6 +73,12 @@ struct tfhe_pks_ctx {
   u32* d_A = nullptr;
   u64* d_T = nullptr;
   size_t rows_cap = 0;  // LWEs the A / T workspaces hold
+  // matrix-core path (default; TFHE_HIP_PKS_VALU=1 keeps the VALU GEMM): the key's byte planes and the
+  // two digit-byte operands
+  bool valu = false;
+  void* d_planes = nullptr;
+  void* d_A0 = nullptr;
+  void* d_A1 = nullptr;
   u64* d_io = nullptr;
   size_t io_cap = 0;  // bytes
   std::mutex mu;
@@ -81,13 +88,19 @@ namespace {
 
 int ensure_rows(tfhe_pks_ctx* c, size_t rows) {
   if (c->rows_cap >= rows) return 0;
-  (void)hipFree(c->d_A);
-  (void)hipFree(c->d_T);
+  for (void* p : {(void*)c->d_A, (void*)c->d_T, c->d_A0, c->d_A1}) (void)hipFree(p);
   c->d_A = nullptr;
   c->d_T = nullptr;
+  c->d_A0 = c->d_A1 = nullptr;
   c->rows_cap = 0;
   const size_t K = (size_t)c->pp.in_dim * c->pp.level, Nc = (size_t)(c->pp.out_k + 1) * c->pp.out_N;
-  PKS_TRY(hipMalloc(&c->d_A, rows * K * sizeof(u32)));
+  if (c->valu) {
+    PKS_TRY(hipMalloc(&c->d_A, rows * K * sizeof(u32)));
+  } else {
+    const size_t r = tfhe::pks_mfma_rows(rows);
+    PKS_TRY(hipMalloc(&c->d_A0, r * K));
+    PKS_TRY(hipMalloc(&c->d_A1, r * K));
+  }
   PKS_TRY(hipMalloc(&c->d_T, rows * Nc * sizeof(u64)));
   c->rows_cap = rows;
   return 0;
@@ -102,9 +115,14 @@ int pack_device(tfhe_pks_ctx* c, const u64* d_lwes, size_t count, u64* d_out, hi
   if (rc) return rc;
   for (size_t first = 0; first < count; first += rows) {
     const size_t n = std::min(rows, count - first);
-    PKS_TRY(tfhe::launch_pks_pack(d_lwes + first * (p.in_dim + 1), n, (int)p.in_dim, (int)p.base_log, (int)p.level,
-                                  (int)p.out_k, (int)p.out_N, (int)lpg, c->d_pksk, c->d_corr, c->d_A, c->d_T,
-                                  d_out + (first / lpg) * Nc, s));
+    if (c->valu)
+      PKS_TRY(tfhe::launch_pks_pack(d_lwes + first * (p.in_dim + 1), n, (int)p.in_dim, (int)p.base_log, (int)p.level,
+                                    (int)p.out_k, (int)p.out_N, (int)lpg, c->d_pksk, c->d_corr, c->d_A, c->d_T,
+                                    d_out + (first / lpg) * Nc, s));
+    else
+      PKS_TRY(tfhe::launch_pks_pack_mfma(d_lwes + first * (p.in_dim + 1), n, (int)p.in_dim, (int)p.base_log,
+                                         (int)p.level, (int)p.out_k, (int)p.out_N, (int)lpg, c->d_planes, c->d_A0,
+                                         c->d_A1, c->d_T, d_out + (first / lpg) * Nc, s));
   }
   return 0;
 }
@@ -142,6 +160,11 @@ int tfhe_hip_pks_create(const tfhe_pks_params* pp, int device, tfhe_pks_ctx** ou
   tfhe_pks_ctx* c = new tfhe_pks_ctx();
   c->pp = *pp;
   c->device = device;
+  {
+    const char* e = getenv("TFHE_HIP_PKS_VALU");
+    // the matrix-core GEMM needs int8 digit bytes (base <= 16) and 64-deep k steps
+    c->valu = (e && e[0] == '1') || pp->base_log > 16 || (pp->in_dim * pp->level) % 64 != 0;
+  }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(TFHE_HIP_EDEVICE, "pks_create: hipStreamCreate failed");
@@ -160,6 +183,9 @@ void tfhe_hip_pks_destroy(tfhe_pks_ctx* c) {
     (void)hipFree(c->d_A);
     (void)hipFree(c->d_T);
     (void)hipFree(c->d_io);
+    (void)hipFree(c->d_planes);
+    (void)hipFree(c->d_A0);
+    (void)hipFree(c->d_A1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
   }
   delete c;
@@ -178,6 +204,11 @@ int tfhe_hip_pks_load_key(tfhe_pks_ctx* c, const uint64_t* pksk, size_t len) {
   PKS_TRY(hipMemcpyAsync(c->d_pksk, pksk, len * 8, hipMemcpyHostToDevice, c->stream));
   PKS_TRY(tfhe::launch_pks_corr(c->d_pksk, (int)(c->pp.in_dim * c->pp.level), (int)Nc, (int)c->pp.base_log, c->d_corr,
                                 c->stream));
+  if (!c->valu) {  // balanced byte planes of the key (ks_mfma.hip's recoding, Nc columns)
+    if (!c->d_planes)
+      PKS_TRY(hipMalloc(&c->d_planes, tfhe::ks_planes_bytes((int)c->pp.in_dim, (int)c->pp.level, (int)Nc - 1)));
+    PKS_TRY(tfhe::launch_ksk_planes(c->d_pksk, (int)c->pp.in_dim, (int)c->pp.level, (int)Nc - 1, c->d_planes, c->stream));
+  }
   PKS_TRY(hipStreamSynchronize(c->stream));
   c->key = true;
   return 0;
