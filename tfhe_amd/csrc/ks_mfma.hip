@@ -171,52 +171,65 @@ __global__ void pks_digits_mfma_kernel(const u64* __restrict__ lwes, size_t coun
   }
 }
 
-constexpr int PM_WAVES = 4, PM_MT = 4, PM_ROWS = 16 * PM_MT * PM_WAVES;  // 256 rows x 16 columns per workgroup
+// workgroup = 4 waves stacked along the rows; wave = PM_MT row tiles x PM_NT column tiles x 8 planes
+#ifndef PM_NT
+#define PM_NT 2
+#endif
+constexpr int PM_WAVES = 4, PM_MT = 4, PM_ROWS = 16 * PM_MT * PM_WAVES;  // 256 rows x 16 PM_NT columns
 
-__global__ __launch_bounds__(64 * PM_WAVES) void pks_gemm_mfma_kernel(const v4i* __restrict__ A0,
+__global__ __launch_bounds__(64 * PM_WAVES, 1) void pks_gemm_mfma_kernel(const v4i* __restrict__ A0,
                                                                       const v4i* __restrict__ A1,
                                                                       const v4i* __restrict__ P, int KS, size_t M,
                                                                       int Nc, u64* __restrict__ T) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nt = blockIdx.x;
+  const int nt0 = blockIdx.x * PM_NT;
   const size_t mt0 = ((size_t)blockIdx.y * PM_WAVES + wave) * PM_MT;
   const v4i* a0 = A0 + mt0 * KS * 64 + lane;
   const v4i* a1 = A1 + mt0 * KS * 64 + lane;
-  const v4i* p = P + (size_t)nt * KS * KM_PLANES * 64 + lane;
-  v4i acc[PM_MT][KM_PLANES];
+  const v4i* p = P + (size_t)nt0 * KS * KM_PLANES * 64 + lane;
+  v4i acc[PM_MT][PM_NT][KM_PLANES];
 #pragma unroll
   for (int m = 0; m < PM_MT; m++)
 #pragma unroll
-    for (int t = 0; t < KM_PLANES; t++) acc[m][t] = (v4i){0, 0, 0, 0};
+    for (int c = 0; c < PM_NT; c++)
+#pragma unroll
+      for (int t = 0; t < KM_PLANES; t++) acc[m][c][t] = (v4i){0, 0, 0, 0};
   for (int ks = 0; ks < KS; ks++) {
-    v4i f0[PM_MT], f1[PM_MT], bf[KM_PLANES];
+    v4i f0[PM_MT], f1[PM_MT];
 #pragma unroll
     for (int m = 0; m < PM_MT; m++) {
       f0[m] = a0[((size_t)m * KS + ks) * 64];
       f1[m] = a1[((size_t)m * KS + ks) * 64];
     }
 #pragma unroll
-    for (int t = 0; t < KM_PLANES; t++) bf[t] = p[((size_t)ks * KM_PLANES + t) * 64];
+    for (int c = 0; c < PM_NT; c++) {
+      v4i bf[KM_PLANES];
+#pragma unroll
+      for (int t = 0; t < KM_PLANES; t++) bf[t] = p[(((size_t)c * KS + ks) * KM_PLANES + t) * 64];
+#pragma unroll
+      for (int m = 0; m < PM_MT; m++)
+#pragma unroll
+        for (int t = 0; t < KM_PLANES; t++) {
+          acc[m][c][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f0[m], bf[t], acc[m][c][t], 0, 0, 0);
+          if (t > 0) acc[m][c][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f1[m], bf[t - 1], acc[m][c][t], 0, 0, 0);
+        }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < PM_NT; c++) {
+    const int col = (nt0 + c) * 16 + (lane & 15);
 #pragma unroll
     for (int m = 0; m < PM_MT; m++)
 #pragma unroll
-      for (int t = 0; t < KM_PLANES; t++) {
-        acc[m][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f0[m], bf[t], acc[m][t], 0, 0, 0);
-        if (t > 0) acc[m][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f1[m], bf[t - 1], acc[m][t], 0, 0, 0);
+      for (int r = 0; r < 4; r++) {
+        const size_t row = (mt0 + m) * 16 + 4 * (lane >> 4) + r;
+        if (row >= M) continue;
+        u64 v = 0;
+#pragma unroll
+        for (int t = 0; t < KM_PLANES; t++) v += (u64)(long long)acc[m][c][t][r] << (8 * t);
+        T[row * (size_t)Nc + col] = v;
       }
   }
-  const int col = nt * 16 + (lane & 15);
-#pragma unroll
-  for (int m = 0; m < PM_MT; m++)
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const size_t row = (mt0 + m) * 16 + 4 * (lane >> 4) + r;
-      if (row >= M) continue;
-      u64 v = 0;
-#pragma unroll
-      for (int t = 0; t < KM_PLANES; t++) v += (u64)(long long)acc[m][t][r] << (8 * t);
-      T[row * (size_t)Nc + col] = v;
-    }
 }
 
 int ks_k(int big_dim, int levels) { return big_dim * levels; }
@@ -248,13 +261,13 @@ hipError_t launch_pks_gemm_mfma(const u64* lwes, size_t count, int in_dim, int b
                                 const void* planes, void* A0, void* A1, u64* T, hipStream_t s) {
   if (count == 0) return hipSuccess;
   const int K = in_dim * LV;
-  if (K % 64 || Nc % 16 || base_log < 2 || base_log > 16 || base_log * LV >= 64 ||
+  if (K % 64 || Nc % (16 * PM_NT) || base_log < 2 || base_log > 16 || base_log * LV >= 64 ||
       (long long)K * 2 * 128 * 128 >= (1ll << 31))
     return hipErrorInvalidValue;
   const size_t rows = pks_mfma_rows(count), el = rows * (size_t)in_dim;
   hipLaunchKernelGGL(pks_digits_mfma_kernel, dim3((unsigned)((el + 255) / 256)), dim3(256), 0, s, lwes, count, rows,
                      in_dim, base_log, LV, (unsigned char*)A0, (unsigned char*)A1);
-  dim3 grid((unsigned)(Nc / 16), (unsigned)(rows / PM_ROWS));
+  dim3 grid((unsigned)(Nc / (16 * PM_NT)), (unsigned)(rows / PM_ROWS));
   hipLaunchKernelGGL(pks_gemm_mfma_kernel, grid, dim3(64 * PM_WAVES), 0, s, (const v4i*)A0, (const v4i*)A1,
                      (const v4i*)planes, K / 64, count, Nc, T);
   return hipGetLastError();
