@@ -14,6 +14,7 @@
 // NTTs are the negacyclic Cooley-Tukey / Gentleman-Sande pair with bit-reversed psi tables (input
 // natural -> spectrum bit-reversed -> natural), 2048 points in LDS, 256 threads.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "pbs_kernels.h"
 
@@ -260,14 +261,11 @@ __device__ __forceinline__ void step1_level(const int* dg, u64* buf, const SnsCo
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(ST) sns_step1_kernel(const u64* __restrict__ lwe, int n, int i,
-                                                       const u64* __restrict__ acc, u64* __restrict__ D,
-                                                       const SnsConst* __restrict__ Kc) {
-  __shared__ u64 rot[2][SN];
-  __shared__ int dig[SL][SN];
-  __shared__ u64 buf[SN];
-  const int ct = blockIdx.x / (SK + 1), c = blockIdx.x % (SK + 1);
-  const SnsConst& K = *Kc;
+// step 1 of CMUX i for (ciphertext ct, component c): X^{a_i} acc_c - acc_c, CRT lift, torus map, 3 digit
+// levels, forward NTT of each in both primes -> D; shared scratch rot (2 x N u64), dig (3 x N int), buf (N u64)
+__device__ void step1_body(const u64* __restrict__ lwe, int n, int i, const u64* __restrict__ acc,
+                           u64* __restrict__ D, const SnsConst& K, int ct, int c, u64 (*rot)[SN], int (*dig)[SN],
+                           u64* buf) {
   const u32 ai = mod_switch_4096(lwe[(size_t)ct * (n + 1) + i]);
   const u64* a = acc + ((size_t)ct * (SK + 1) + c) * 2 * SN;
   for (int x = threadIdx.x; x < 2 * SN; x += ST) {
@@ -305,6 +303,15 @@ __global__ void __launch_bounds__(ST) sns_step1_kernel(const u64* __restrict__ l
   }
 }
 
+__global__ void __launch_bounds__(ST) sns_step1_kernel(const u64* __restrict__ lwe, int n, int i,
+                                                       const u64* __restrict__ acc, u64* __restrict__ D,
+                                                       const SnsConst* __restrict__ Kc) {
+  __shared__ u64 rot[2][SN];
+  __shared__ int dig[SL][SN];
+  __shared__ u64 buf[SN];
+  step1_body(lwe, n, i, acc, D, *Kc, blockIdx.x / (SK + 1), blockIdx.x % (SK + 1), rot, dig, buf);
+}
+
 // step 2 for prime Q: 9-term MAC, inverse NTT, accumulate
 template <int Q>
 __device__ __forceinline__ void step2_body(const u64* __restrict__ D, const u64* __restrict__ bsk_i,
@@ -329,6 +336,31 @@ __global__ void __launch_bounds__(ST) sns_step2_kernel(const u64* __restrict__ D
   const int q = blockIdx.x & 1, j = (blockIdx.x >> 1) % (SK + 1), ct = (blockIdx.x >> 1) / (SK + 1);
   if (q) step2_body<1>(D, bsk_i, acc, *Kc, buf, j, ct);
   else step2_body<0>(D, bsk_i, acc, *Kc, buf, j, ct);
+}
+
+// The whole squash blind rotation of one ciphertext in ONE launch (TFHE_HIP_SNS_FUSED=1; not the
+// default — see launch_sns_blind_rotate): a workgroup per ciphertext walks the CMUX loop, step 1 for the 3 components then step 2 for the 6 (output, prime) pairs, workgroup barriers
+// between; D and acc stay in global memory (per-ciphertext 288 KB + 96 KB, cache-resident), the BSK row of
+// CMUX i is shared by all resident workgroups through L2.  Same arithmetic as the two-kernel loop.
+__global__ void __launch_bounds__(ST) sns_fused_kernel(const u64* __restrict__ lwe, int n,
+                                                       const u64* __restrict__ bsk_ntt, u64* __restrict__ acc,
+                                                       u64* __restrict__ D, const SnsConst* __restrict__ Kc) {
+  __shared__ u64 rot[2][SN];
+  __shared__ int dig[SL][SN];
+  __shared__ u64 buf[SN];
+  const SnsConst& K = *Kc;
+  const int ct = blockIdx.x;
+  const size_t bsk_row = (size_t)SR * (SK + 1) * 2 * SN;
+  for (int i = 0; i < n; i++) {
+    for (int c = 0; c <= SK; c++) step1_body(lwe, n, i, acc, D, K, ct, c, rot, dig, buf);
+    const u64* bsk_i = bsk_ntt + bsk_row * i;
+    for (int j = 0; j <= SK; j++) {
+      step2_body<0>(D, bsk_i, acc, K, buf, j, ct);
+      __syncthreads();
+      step2_body<1>(D, bsk_i, acc, K, buf, j, ct);
+      __syncthreads();
+    }
+  }
 }
 
 // acc -> LWE over Z_2^128 (dim k N, + body), (lo, hi) pairs
@@ -428,6 +460,16 @@ hipError_t launch_sns_blind_rotate(const u64* lwe, size_t B, int n, const u64* l
                                    u64* D, const void* d_const, hipStream_t s) {
   const SnsConst* K = (const SnsConst*)d_const;
   sns_init_kernel<<<(unsigned)B, 256, 0, s>>>(lwe, n, lut, acc, K);
+  // TFHE_HIP_SNS_FUSED=1: the single-launch form (measured 2.4x slower: 1024 workgroups of 4 waves with
+  // the 9 jobs of a CMUX in sequence expose far less parallelism than 3072 + 6144 workgroups per CMUX)
+  static const bool fused = [] {
+    const char* e = getenv("TFHE_HIP_SNS_FUSED");
+    return e && e[0] == '1';
+  }();
+  if (fused) {
+    sns_fused_kernel<<<(unsigned)B, ST, 0, s>>>(lwe, n, bsk_ntt, acc, D, K);
+    return hipGetLastError();
+  }
   const size_t bsk_i = (size_t)SR * (SK + 1) * 2 * SN;
   for (int i = 0; i < n; i++) {
     sns_step1_kernel<<<(unsigned)(B * (SK + 1)), ST, 0, s>>>(lwe, n, i, acc, D, K);
