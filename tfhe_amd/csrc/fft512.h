@@ -100,6 +100,67 @@ __device__ __forceinline__ void dft8(double (&xr)[8], double (&xi)[8]) {
   xr[7] = zr[6] - zr[7]; xi[7] = zi[6] - zi[7];
 }
 
+// Transpose 1 in registers (FFT_T1_PERM=1; measured and NOT the default: the P-GATE batch kernel 27.40 ->
+// 28.80 ms, the N = 2048 kernel 52.18 -> 52.00 ms — the 96 cross-lane moves and selects per transpose cost
+// more VALU time than the 16 LDS operations and two waits they replace): slot bits (0, 1, 2) <-> lane bits (3, 4, 5), the
+// permutation the T1 round trip through LDS performs in both directions (it is an involution).  Lane bit
+// 5 <-> slot bit 2 is v_permlane32_swap, lane bit 4 <-> slot bit 1 v_permlane16_swap (gfx950: each swaps
+// one operand's upper 32-lane half / odd 16-lane rows with the other's lower half / even rows, probed in
+// tools/microbench/permlane_probe.hip), lane bit 3 <-> slot bit 0 a DPP row_ror:8 exchange with selects.
+// Pure data movement: the transform's arithmetic and results are unchanged.
+#ifndef FFT_T1_PERM
+#define FFT_T1_PERM 0
+#endif
+typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void swap32_d(double& a, double& b) {
+  const u32x2v x = __builtin_bit_cast(u32x2v, a), y = __builtin_bit_cast(u32x2v, b);
+  const auto lo = __builtin_amdgcn_permlane32_swap(x.x, y.x, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(x.y, y.y, false, false);
+  a = __builtin_bit_cast(double, (u32x2v){lo[0], hi[0]});
+  b = __builtin_bit_cast(double, (u32x2v){lo[1], hi[1]});
+}
+__device__ __forceinline__ void swap16_d(double& a, double& b) {
+  const u32x2v x = __builtin_bit_cast(u32x2v, a), y = __builtin_bit_cast(u32x2v, b);
+  const auto lo = __builtin_amdgcn_permlane16_swap(x.x, y.x, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(x.y, y.y, false, false);
+  a = __builtin_bit_cast(double, (u32x2v){lo[0], hi[0]});
+  b = __builtin_bit_cast(double, (u32x2v){lo[1], hi[1]});
+}
+// 2 x 2 transpose of (a, b) with lane bit 3: new_a[L] = b3 ? b[L ^ 8] : a[L], new_b[L] = b3 ? b[L] : a[L ^ 8]
+__device__ __forceinline__ void swap8_u32(unsigned& a, unsigned& b, bool b3) {
+  const unsigned t = b3 ? a : b;
+  const unsigned u = (unsigned)__builtin_amdgcn_update_dpp(0, (int)t, 0x128, 0xF, 0xF, false);  // row_ror:8
+  a = b3 ? u : a;
+  b = b3 ? b : u;
+}
+__device__ __forceinline__ void swap8_d(double& a, double& b, bool b3) {
+  const u32x2v x = __builtin_bit_cast(u32x2v, a), y = __builtin_bit_cast(u32x2v, b);
+  unsigned xl = x.x, xh = x.y, yl = y.x, yh = y.y;
+  swap8_u32(xl, yl, b3);
+  swap8_u32(xh, yh, b3);
+  a = __builtin_bit_cast(double, (u32x2v){xl, xh});
+  b = __builtin_bit_cast(double, (u32x2v){yl, yh});
+}
+__device__ __forceinline__ void t1_regs(double (&xr)[8], double (&xi)[8], int lane) {
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    swap32_d(xr[e], xr[e + 4]);
+    swap32_d(xi[e], xi[e + 4]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; e++)
+    if ((e & 2) == 0) {
+      swap16_d(xr[e], xr[e + 2]);
+      swap16_d(xi[e], xi[e + 2]);
+    }
+  const bool b3 = (lane >> 3) & 1;
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    swap8_d(xr[e], xr[e + 1], b3);
+    swap8_d(xi[e], xi[e + 1], b3);
+  }
+}
+
 // per-lane transpose bases: b1 = T1 read / inverse write, b2 = T2 read / inverse write
 struct TBase {
   int b1, b2;
@@ -116,6 +177,9 @@ __device__ __forceinline__ void dft512_fwd_t(double (&xr)[8], double (&xi)[8], d
   dft8<false>(xr, xi);
 #pragma unroll
   for (int e = TW0 ? 0 : 1; e < 8; e++) cmul<false>(xr[e], xi[e], twA[64 * e + lane]);
+#if FFT_T1_PERM
+  t1_regs(xr, xi, lane);
+#else
 #pragma unroll
   for (int e = 0; e < 8; e++) T[lane + S1 * e] = make_double2(xr[e], xi[e]);
   lds_order();
@@ -126,6 +190,7 @@ __device__ __forceinline__ void dft512_fwd_t(double (&xr)[8], double (&xi)[8], d
     xi[e] = v.y;
   }
   lds_order();
+#endif
   dft8<false>(xr, xi);
 #pragma unroll
   for (int e = 1; e < 8; e++) cmul<false>(xr[e], xi[e], twB[64 * e + lane]);
@@ -168,6 +233,9 @@ __device__ __forceinline__ void dft512_inv_t(double (&xr)[8], double (&xi)[8], d
   dft8<true>(xr, xi);
 #pragma unroll
   for (int e = 0; e < 8; e++) cmul<true>(xr[e], xi[e], twI[64 * e + lane]);
+#if FFT_T1_PERM
+  t1_regs(xr, xi, lane);
+#else
 #pragma unroll
   for (int e = 0; e < 8; e++) T[tb.b1 + 8 * e] = make_double2(xr[e], xi[e]);
   lds_order();
@@ -178,6 +246,7 @@ __device__ __forceinline__ void dft512_inv_t(double (&xr)[8], double (&xi)[8], d
     xi[e] = v.y;
   }
   lds_order();
+#endif
   dft8<true>(xr, xi);
 }
 
@@ -214,6 +283,9 @@ __device__ __forceinline__ void dft512_inv_r(double (&xr)[8], double (&xi)[8], d
   dft8<true>(xr, xi);
 #pragma unroll
   for (int e = 0; e < 8; e++) cmul<true>(xr[e], xi[e], w.i[e]);
+#if FFT_T1_PERM
+  t1_regs(xr, xi, lane);
+#else
 #pragma unroll
   for (int e = 0; e < 8; e++) T[tb.b1 + 8 * e] = make_double2(xr[e], xi[e]);
   lds_order();
@@ -224,6 +296,7 @@ __device__ __forceinline__ void dft512_inv_r(double (&xr)[8], double (&xi)[8], d
     xi[e] = v.y;
   }
   lds_order();
+#endif
   dft8<true>(xr, xi);
 }
 
