@@ -14,13 +14,13 @@
 //   T   8 x 9,216 B   per-wave transpose scratch; a pair's two regions also hold the 2048-u64
 //                     rotation image and the combine / uncombine exchanges
 //   tw  48 KB         all tables: pass A'/B' per parity (twist merged in), pass B, combine
-//   K   2 x 16 KB     BSK_i[c][0..1] of the component in flight, loaded by global_load_lds one phase
-//                     ahead (K_{1,*} during component 1's rotation and transform, K_{0,*} of the next
-//                     CMUX during the inverse transforms), published by the transform's barriers
+//   K   2 x 16 KB     one output column of BSK_i (K_{0,j}, K_{1,j}), loaded by global_load_lds one
+//                     phase ahead (column 1 under the first inverse, the next CMUX's column 0 under
+//                     the second inverse, rotation and forward transforms)
 // Per CMUX: rotate + decompose both components (23 x 1 digits, no exchange of digits needed: each
-// wave decomposes its own coefficients), two forward transforms, the MAC
-//   O_j = fma chain over c = 0, 1 of D_c (.) BSK_i[c][j]   (the oracle's order, from (0, 0)),
-// and two inverse transforms back to this wave's coefficients of acc_0 and acc_1.
+// wave decomposes its own coefficients), two forward transforms, then per output column j the MAC
+//   O_j = fma chain over c = 0, 1 of D_c (.) BSK_i[c][j]   (the oracle's order, from (0, 0))
+// and the inverse transform back to this wave's coefficients of acc_j (F2_MACORDER 2).
 #include "fft512.h"
 #include "pbs_kernels.h"
 
@@ -77,7 +77,7 @@ __device__ __forceinline__ void pair_sync() {
 // the workgroup calls it in lockstep.  T0 / T1: the pair's regions (wave 0 / wave 1).
 // The exchange moves only what the partner needs: wave h combines at slots 4h + q, so wave 0 sends E_0 at
 // slots 4..7 and wave 1 sends E_1 at slots 0..3 (4 writes and 4 reads per wave; its own 4 stay in registers).
-template <int H>
+template <int H, bool TRAIL>
 __device__ __forceinline__ void combine_fwd(double (&xr)[8], double (&xi)[8], int lane, double2* Tm,
                                             const double2* Tp, const double2* tg) {
 #pragma unroll
@@ -95,23 +95,26 @@ __device__ __forceinline__ void combine_fwd(double (&xr)[8], double (&xi)[8], in
     xr[q + 4] = e0r - tr;
     xi[q + 4] = e0i - ti;
   }
-  pair_sync();
+  if (TRAIL) pair_sync();
 }
+// TRAIL = false: the caller's next barrier comes before either wave of the pair writes the region the
+// other one read (the partner's reads were at slots 4 (1 - h) + q of this wave's region)
+template <bool TRAIL = true>
 __device__ __forceinline__ void fwd_half(double (&xr)[8], double (&xi)[8], int h, int lane, TBase tb,
                                          double2* T0, double2* T1, const double2* tg) {
   double2* Tm = h ? T1 : T0;
   twist_slots<false>(xr, xi);
   dft512_fwd_t<true>(xr, xi, Tm, lane, tb, tg + (h ? G_A1 : G_A0), tg + G_B);
-  if (__builtin_amdgcn_readfirstlane(h)) combine_fwd<1>(xr, xi, lane, T1, T0, tg);
-  else combine_fwd<0>(xr, xi, lane, T0, T1, tg);
+  if (__builtin_amdgcn_readfirstlane(h)) combine_fwd<1, TRAIL>(xr, xi, lane, T1, T0, tg);
+  else combine_fwd<0, TRAIL>(xr, xi, lane, T0, T1, tg);
 }
 
 // inverse, first half: uncombine this wave's 4 slot pairs (slot 4h + q) into E_0 and E_1; keep E_h, send
 // E_(1-h) to the partner through this wave's region, take the partner's E_h at slots 4(1-h) + q.  Two
 // pair barriers.
-template <int H>
+template <int H, typename Mid>
 __device__ __forceinline__ void uncombine_inv(double (&xr)[8], double (&xi)[8], int lane, double2* Tm,
-                                              const double2* Tp, const double2* tg) {
+                                              const double2* Tp, const double2* tg, Mid&& mid) {
 #pragma unroll
   for (int q = 0; q < 4; q++) {
     const int e = 4 * H + q;
@@ -124,6 +127,7 @@ __device__ __forceinline__ void uncombine_inv(double (&xr)[8], double (&xi)[8], 
     xi[e] = H ? di : si;
   }
   pair_sync();
+  mid();
 #pragma unroll
   for (int q = 0; q < 4; q++) {
     const int e = 4 * (1 - H) + q;
@@ -133,10 +137,16 @@ __device__ __forceinline__ void uncombine_inv(double (&xr)[8], double (&xi)[8], 
   }
   pair_sync();
 }
+// mid(): run by every wave right after the exchange's first (workgroup-wide) barrier
+template <typename Mid>
+__device__ __forceinline__ void inv_exchange(double (&xr)[8], double (&xi)[8], int h, int lane, double2* T0,
+                                             double2* T1, const double2* tg, Mid&& mid) {
+  if (__builtin_amdgcn_readfirstlane(h)) uncombine_inv<1>(xr, xi, lane, T1, T0, tg, mid);
+  else uncombine_inv<0>(xr, xi, lane, T0, T1, tg, mid);
+}
 __device__ __forceinline__ void inv_exchange(double (&xr)[8], double (&xi)[8], int h, int lane, double2* T0,
                                              double2* T1, const double2* tg) {
-  if (__builtin_amdgcn_readfirstlane(h)) uncombine_inv<1>(xr, xi, lane, T1, T0, tg);
-  else uncombine_inv<0>(xr, xi, lane, T0, T1, tg);
+  inv_exchange(xr, xi, h, lane, T0, T1, tg, [] {});
 }
 
 // inverse, second half (wave-private): 512-point inverse + untwist -> reals (slot e < 8: re, e + 8: im)
@@ -192,9 +202,24 @@ __global__ __launch_bounds__(128) void inv2k_kernel(const double2* __restrict__ 
 #ifndef F2_PRIO
 #define F2_PRIO 1
 #endif
-// F2_MACORDER = 1: transform both components, then one MAC per output column (see the loop)
+// F2_MACORDER = 1: transform both components, then one MAC per output column, both MACs before the
+// inverses (35 spilled VGPRs: O_0, O_1, D_0, D_1 and the accumulators live together); 2 (default): the
+// first inverse between the two MACs, no spills (round 2: 52.1 -> 51.2 ms per 4096, same-box A/B)
 #ifndef F2_MACORDER
-#define F2_MACORDER 1
+#define F2_MACORDER 2
+#endif
+// barrier trims of the order-2 loop: A (default) the second forward transform's trailing pair barrier
+// (51.13 -> 51.02 ms); B the barrier before the next CMUX's column-0 load, C the one before the column-1
+// load, the loads then issued inside the next exchange after its first barrier (B: +-0, C: +0.2 %, all
+// three together 51.3 -> 51.8 ms; kept as switches)
+#ifndef F2_TRIM_A
+#define F2_TRIM_A 1
+#endif
+#ifndef F2_TRIM_B
+#define F2_TRIM_B 0
+#endif
+#ifndef F2_TRIM_C
+#define F2_TRIM_C 0
 #endif
 
 // the whole table first (every twiddle read: a per-lane base plus a 16-bit DS immediate offset), then
@@ -314,7 +339,7 @@ __device__ __forceinline__ void mac_column(lds_c64* kp, const double (&ar)[8], c
 // F2_STAMPS (diagnostic builds only, never the shipped library): s_memtime stamps at the phase
 // boundaries of the CMUX loop, summed per wave of every 64th workgroup into f2_stamps[slot][wave][phase]
 // (cdna_hip_programming.md, "In-kernel stamps"); read with tfhe_hip_debug_stamps.  Read the SHARES.
-constexpr int F2_NPH = 12;
+[[maybe_unused]] constexpr int F2_NPH = 12;
 #if F2_STAMPS
 __device__ unsigned long long f2_stamps[16][F2_WAVES][F2_NPH];
 #define F2_STAMP(k)                                                                              \
@@ -402,12 +427,18 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
       xr[e] = (double)dg[e];
       xi[e] = (double)dg[e + 8];
     }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's share of column 0; fwd_half's barriers publish it
-    fwd_half(xr, xi, h, lane, tb, T0, T1, tt);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's share of column 0; fwd_half's barrier publishes it
+    fwd_half<!F2_TRIM_A>(xr, xi, h, lane, tb, T0, T1, tt);  // the exchange below is the next barrier
     mac_column(kbase(&sh.K[0][0], h, lane), d0r, d0i, xr, xi, o0r, o0i);
+#if F2_TRIM_C
+    // column 1 into the key buffer under the first inverse, issued once every wave is past MAC 0 (the
+    // exchange's first barrier)
+    inv_exchange(o0r, o0i, h, lane, T0, T1, tt, [&] { load_column(bsk, i, 1, &sh.K[0][0], wave_s, lane); });
+#else
     __syncthreads();  // every wave is done with column 0
     load_column(bsk, i, 1, &sh.K[0][0], wave_s, lane);  // column 1, under the first inverse
     inv_exchange(o0r, o0i, h, lane, T0, T1, tt);
+#endif
     inv_half(o0r, o0i, h, lane, tb, Tm, tt);
 #pragma unroll
     for (int e = 0; e < 8; e++) {
@@ -419,9 +450,16 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     {
       double o1r[8], o1i[8];
       mac_column(kbase(&sh.K[0][0], h, lane), d0r, d0i, xr, xi, o1r, o1i);
-      __syncthreads();  // every wave is done with column 1 (and with the partner's transpose region)
+#if F2_TRIM_B
+      // the next CMUX's column 0, once every wave is past MAC 1
+      inv_exchange(o1r, o1i, h, lane, T0, T1, tt, [&] {
+        if (i + 1 < n) load_column(bsk, i + 1, 0, &sh.K[0][0], wave_s, lane);
+      });
+#else
+      __syncthreads();  // every wave is done with column 1
       if (i + 1 < n) load_column(bsk, i + 1, 0, &sh.K[0][0], wave_s, lane);
       inv_exchange(o1r, o1i, h, lane, T0, T1, tt);
+#endif
       inv_half(o1r, o1i, h, lane, tb, Tm, tt);
 #pragma unroll
       for (int e = 0; e < 8; e++) {
