@@ -149,7 +149,6 @@ __global__ __launch_bounds__(64) void fft_inv_kernel(const double2* __restrict__
 #define FFT_INVTW 1
 #endif
 constexpr int FB_WAVES = 8;
-constexpr int FB_THREADS = 64 * FB_WAVES;
 constexpr int CHUNK_C64 = 2 * M;                   // one level step: rows (c, l), j = 0, 1 (16 KB)
 constexpr int CHUNK_GLDS = CHUNK_C64 * 16 / 1024;  // 1 KB wave-instructions per chunk (16)
 // s_waitcnt vmcnt(CHUNK_GLDS / FB_WAVES): a wave issues that many global_load_lds per chunk
@@ -185,17 +184,21 @@ __device__ unsigned long long fft_stamps[16][FB_WAVES][FS_NPH];
 #define FS_PASS
 #endif
 
+// W waves = W ciphertexts per workgroup: 8 (two waves per SIMD) for full batches; 4 (one per SIMD) when
+// the batch is too small to give every CU a workgroup of 8 (FFT_W4_MAX)
+template <int W>
 struct FftShared {
-  double2 T[FB_WAVES][T_C64];  // per-wave transpose / rotation scratch  72 KB
+  double2 T[W][T_C64];         // per-wave transpose / rotation scratch  72 KB at W = 8
   double2 K[FFT_KBUF][CHUNK_C64];  // BSK level-step chunks in flight   16 KB each
   double2 tw[TW_C64];          // twist | pass A | pass B | inverse B'   32 KB
 };
 
+template <int W>
 __device__ __forceinline__ void load_chunk(const double2* __restrict__ bsk, int g, double2* dst, int wave, int lane) {
   const char* src = (const char*)(bsk + (size_t)g * CHUNK_C64);
 #pragma unroll
-  for (int q = 0; q < CHUNK_GLDS / FB_WAVES; q++) {
-    const int blk = wave * (CHUNK_GLDS / FB_WAVES) + q;
+  for (int q = 0; q < CHUNK_GLDS / W; q++) {
+    const int blk = wave * (CHUNK_GLDS / W) + q;
     __builtin_amdgcn_global_load_lds((const void*)(src + blk * 1024 + lane * 16),
                                      (__attribute__((address_space(3))) void*)((char*)dst + blk * 1024), 16, 0, 0);
   }
@@ -203,8 +206,9 @@ __device__ __forceinline__ void load_chunk(const double2* __restrict__ bsk, int 
 
 // component c of the external product for CMUX i: decompose (X^a - 1) acc_c; per level l (step
 // g = 6 i + 3 c + l) transform the digit polynomial and accumulate D (.) BSK_i[(c, l)][j] into O_j
+template <int W>
 __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rbase, int c, int i, int n_steps,
-                                                   FftShared& sh, double2* T, int wave, int lane, TBase tb,
+                                                   FftShared<W>& sh, double2* T, int wave, int lane, TBase tb,
                                                    const double2* __restrict__ bsk, double (&o0r)[8],
                                                    double (&o0i)[8], double (&o1r)[8], double (&o1i)[8] FS_ARGS) {
   u64* Tu = (u64*)T;
@@ -232,10 +236,10 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rba
     else __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
-    if (g + 2 < n_steps) load_chunk(bsk, g + 2, sh.K[(g + 2) % 3], wave, lane);
+    if (g + 2 < n_steps) load_chunk<W>(bsk, g + 2, sh.K[(g + 2) % 3], wave, lane);
 #else
     glds_barrier();
-    if (g + 1 < n_steps) load_chunk(bsk, g + 1, sh.K[(g + 1) & 1], wave, lane);
+    if (g + 1 < n_steps) load_chunk<W>(bsk, g + 1, sh.K[(g + 1) & 1], wave, lane);
 #endif
     FS_STAMP(1);
     const u32 bmask = q < 2 ? 1u : 0u;
@@ -278,24 +282,24 @@ __device__ __forceinline__ void accumulate(u64 (&acc)[16], double (&or_)[8], dou
   }
 }
 
-template <bool WRITE_ACC, bool WRITE_BIG>
-__global__ __launch_bounds__(FB_THREADS, 1) void blind_rotate_fft_kernel(
+template <int W, bool WRITE_ACC, bool WRITE_BIG>
+__global__ __launch_bounds__(64 * W, 1) void blind_rotate_fft_kernel(
     const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
     int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tw_g, u64* __restrict__ out_big,
     u64* __restrict__ out_acc) {
-  __shared__ __attribute__((aligned(16))) FftShared sh;
+  __shared__ __attribute__((aligned(16))) FftShared<W> sh;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const size_t b_raw = (size_t)blockIdx.x * FB_WAVES + wave;
+  const size_t b_raw = (size_t)blockIdx.x * W + wave;
   const bool live = b_raw < B;
   const size_t b = live ? b_raw : B - 1;  // padding waves run a copy of the last ciphertext, store nothing
   const u64* ct = lwe_in + b * (size_t)(n + 1);
   double2* T = sh.T[wave];
   const int n_steps = n * 6;
 
-  for (int q = threadIdx.x; q < TW_C64; q += FB_THREADS) sh.tw[q] = tw_g[q];
-  load_chunk(bsk, 0, sh.K[0], wave, lane);
+  for (int q = threadIdx.x; q < TW_C64; q += 64 * W) sh.tw[q] = tw_g[q];
+  load_chunk<W>(bsk, 0, sh.K[0], wave, lane);
 #if FFT_KBUF == 3
-  if (n_steps > 1) load_chunk(bsk, 1, sh.K[1], wave, lane);
+  if (n_steps > 1) load_chunk<W>(bsk, 1, sh.K[1], wave, lane);
 #endif
 
   // acc = (0, X^{-b~} * lut): LUT values arrive in the Z_p encoding, mapped to the torus first
@@ -319,7 +323,7 @@ __global__ __launch_bounds__(FB_THREADS, 1) void blind_rotate_fft_kernel(
 
   const TBase tb(lane);
 #if FFT_PRIO == 1
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  if (W == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
 #elif FFT_PRIO == 2
   if (wave & 1) __builtin_amdgcn_s_setprio(1);
 #endif
@@ -333,8 +337,8 @@ __global__ __launch_bounds__(FB_THREADS, 1) void blind_rotate_fft_kernel(
 #pragma unroll
     for (int e = 0; e < 8; e++) { o0r[e] = 0; o0i[e] = 0; o1r[e] = 0; o1i[e] = 0; }
     FS_STAMP(7);
-    ext_prod_component(accA, rbase, 0, i, n_steps, sh, T, wave, lane, tb, bsk, o0r, o0i, o1r, o1i FS_PASS);
-    ext_prod_component(accB, rbase, 1, i, n_steps, sh, T, wave, lane, tb, bsk, o0r, o0i, o1r, o1i FS_PASS);
+    ext_prod_component<W>(accA, rbase, 0, i, n_steps, sh, T, wave, lane, tb, bsk, o0r, o0i, o1r, o1i FS_PASS);
+    ext_prod_component<W>(accB, rbase, 1, i, n_steps, sh, T, wave, lane, tb, bsk, o0r, o0i, o1r, o1i FS_PASS);
 #if FFT_INVTW
     {  // both inverses with the twiddles read once
       InvTw w;
@@ -622,6 +626,28 @@ hipError_t launch_bsk_to_fourier(const u64* bsk_std, double* bsk_f, size_t polys
   return hipGetLastError();
 }
 
+// batches up to this size (per device, above the latency kernel's range) run 4-wave workgroups: at 8
+// ciphertexts per workgroup a batch of 1024 would leave half the CUs idle
+#ifndef FFT_W4_MAX
+#define FFT_W4_MAX 1024
+#endif
+template <int W>
+static hipError_t launch_batch(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index, int n_lut,
+                               const double2* bk, const double2* t, u64* out_big, u64* out_acc, hipStream_t s) {
+  using namespace fftk;
+  dim3 grid((unsigned)((B + W - 1) / W)), block(64 * W);
+  if (out_acc && out_big)
+    hipLaunchKernelGGL((blind_rotate_fft_kernel<W, true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                       n_lut, bk, t, out_big, out_acc);
+  else if (out_acc)
+    hipLaunchKernelGGL((blind_rotate_fft_kernel<W, true, false>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                       n_lut, bk, t, out_big, out_acc);
+  else
+    hipLaunchKernelGGL((blind_rotate_fft_kernel<W, false, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                       n_lut, bk, t, out_big, out_acc);
+  return hipGetLastError();
+}
+
 hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
                                    int n_lut, const double* bsk_f, const double* tw, u64* out_big, u64* out_acc,
                                    hipStream_t s, size_t latency_max_batch) {
@@ -641,17 +667,8 @@ hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64
                          n_lut, bk, t, out_big, out_acc);
     return hipGetLastError();
   }
-  dim3 grid((unsigned)((B + FB_WAVES - 1) / FB_WAVES)), block(FB_THREADS);
-  if (out_acc && out_big)
-    hipLaunchKernelGGL((blind_rotate_fft_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index, n_lut,
-                       bk, t, out_big, out_acc);
-  else if (out_acc)
-    hipLaunchKernelGGL((blind_rotate_fft_kernel<true, false>), grid, block, 0, s, lwe_in, n, B, luts, lut_index, n_lut,
-                       bk, t, out_big, out_acc);
-  else
-    hipLaunchKernelGGL((blind_rotate_fft_kernel<false, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
-                       n_lut, bk, t, out_big, out_acc);
-  return hipGetLastError();
+  if (B <= FFT_W4_MAX) return launch_batch<4>(lwe_in, B, n, luts, lut_index, n_lut, bk, t, out_big, out_acc, s);
+  return launch_batch<FB_WAVES>(lwe_in, B, n, luts, lut_index, n_lut, bk, t, out_big, out_acc, s);
 }
 
 hipError_t launch_sample_extract_torus(const u64* acc, size_t B, u64* out, hipStream_t s) {
