@@ -1,6 +1,6 @@
 """Blind-rotate kernel time vs batch size for the latency kernel and the batch kernel, measured with
 the library's HIP events; prints one JSON object.  Picks the crossover used as the default of
-tfhe_hip_set_latency_batch.   python tools/latency_sweep.py [gate|fhevm]"""
+tfhe_hip_set_latency_batch.   python tools/latency_sweep.py [gate|fhevm|gate_fft|fhevm_fft] [B,B,...]"""
 import json
 import os
 import sys
@@ -13,13 +13,18 @@ import tfhe_amd  # noqa: E402
 
 def main():
     import torch
-    fhevm = len(sys.argv) > 1 and sys.argv[1] == "fhevm"
-    params = tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM if fhevm else tfhe_amd.PRESET_GATE)
+    which = sys.argv[1] if len(sys.argv) > 1 else "gate"
+    fhevm = which.startswith("fhevm")
+    preset = {"gate": tfhe_amd.PRESET_GATE, "fhevm": tfhe_amd.PRESET_FHEVM, "gate_fft": tfhe_amd.PRESET_GATE_FFT,
+              "fhevm_fft": tfhe_amd.PRESET_FHEVM_FFT}[which]
+    params = tfhe_amd.Params.preset(preset)
+    sizes = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else \
+        [1, 8, 64, 256, 257, 512, 768, 1024, 1280, 1536, 2048, 4096]
     ck, sk = tfhe_amd.gen_keys(params, 0x7F4E0001)
     eng = tfhe_amd.Engine(params, 0).load_keys(sk)
     dev = torch.device("cuda", 0)
     res = {}
-    for B in [1, 8, 64, 256, 257, 512, 768, 1024, 1280, 1536, 2048, 4096]:
+    for B in sizes:
         want = np.arange(B) % (16 if fhevm else 2)
         cts = ck.encrypt(want, 16, seed=9) if fhevm else ck.encrypt_bool(want == 0, seed=9)
         lut = eng.generate_accumulator(lambda m: m, 16) if fhevm else eng.gate_lut()
