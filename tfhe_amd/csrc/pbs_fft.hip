@@ -130,7 +130,8 @@ __global__ __launch_bounds__(64) void fft_inv_kernel(const double2* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
-// Blind rotation + sample extraction (batch kernel): workgroup = 8 wavefronts = 8 ciphertexts.
+// Blind rotation + sample extraction (batch kernel): workgroup = W wavefronts = W ciphertexts (8; 4 for
+// batches of 513-1024, FFT_W4_MAX).
 // BSK chunk buffers: 2 = one level step in flight (default); 3 keeps two in flight (chunk g + 2 issued
 // while step g computes, the barrier before step g waits only for chunk g with a counted vmcnt):
 // measured 3 % slower on MI355X (31.2 vs 30.35 ms per 4096; the chunk arrives in time either way and
@@ -151,9 +152,8 @@ __global__ __launch_bounds__(64) void fft_inv_kernel(const double2* __restrict__
 constexpr int FB_WAVES = 8;
 constexpr int CHUNK_C64 = 2 * M;                   // one level step: rows (c, l), j = 0, 1 (16 KB)
 constexpr int CHUNK_GLDS = CHUNK_C64 * 16 / 1024;  // 1 KB wave-instructions per chunk (16)
-// s_waitcnt vmcnt(CHUNK_GLDS / FB_WAVES): a wave issues that many global_load_lds per chunk
-// (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] = 7 | lgkmcnt[11:8] = 15 | vmcnt[5:4] in [15:14])
-[[maybe_unused]] constexpr int VMCNT_CHUNK = 0x0F70 | (CHUNK_GLDS / 8);
+// KBUF 3: s_waitcnt vmcnt(CHUNK_GLDS / W), the global_load_lds a wave issues per chunk (gfx9 encoding:
+// vmcnt[3:0] | expcnt[6:4] = 7 | lgkmcnt[11:8] = 15 | vmcnt[5:4] in [15:14])
 
 // FFT_STAMPS (diagnostic builds only, never the shipped library): s_memtime stamps at the phase
 // boundaries of the CMUX loop, summed per wave of every 64th workgroup into fft_stamps[slot][wave][phase]
@@ -232,7 +232,7 @@ __device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rba
 #if FFT_KBUF == 3
     // chunk g is complete once at most chunk g + 1's loads (issued one step ago) are outstanding
     // raw s_barrier: __syncthreads()'s fence would drain vmcnt(0), chunk g + 1 included
-    if (g + 1 < n_steps) __builtin_amdgcn_s_waitcnt(VMCNT_CHUNK);
+    if (g + 1 < n_steps) __builtin_amdgcn_s_waitcnt(0x0F70 | (CHUNK_GLDS / W));  // vmcnt(loads per chunk)
     else __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
