@@ -466,8 +466,11 @@ class SnsKeys:
     @property
     def bsk_ntt(self) -> np.ndarray:
         if self._bsk_ntt is None:
-            self._bsk_ntt = np.zeros_like(self.bsk)
-            lib().or_sns_bsk_to_ntt(ctypes.byref(self.sp), _p(self.bsk), _p(self._bsk_ntt))
+            # the device rounds the key to multiples of 2^16 at load (or_sns_bsk_round): same here
+            rounded = np.zeros_like(self.bsk)
+            lib().or_sns_bsk_round(ctypes.byref(self.sp), _p(self.bsk), _p(rounded))
+            self._bsk_ntt = rounded
+            lib().or_sns_bsk_to_ntt(ctypes.byref(self.sp), _p(rounded), _p(self._bsk_ntt))
         return self._bsk_ntt
 
 

@@ -243,6 +243,29 @@ void or_sns_keygen(const or_sns_params* sp, uint64_t seed, const uint64_t* lwe_k
   free(skey);
 }
 
+/* Load-time rounding of the squashing key (the device's precision contract, tfhe_amd/csrc/sns_fft.h):
+ * every coefficient x (residues r1, r2) is centred in (-Q/2, Q/2] and rounded to the nearest multiple of
+ * 2^16 (ties up).  The rounding error (< 2^15 per mask and body coefficient) adds ~2^20 of phase noise
+ * to a key whose own noise is 2^30; in exchange the rounded key is 2^16 x a 112-bit integer, whose seven
+ * balanced 16-bit limbs make each digit x limb convolution an exact f64 FFT product on the device.
+ * Both device transforms (the f64 FFT and the NTT) apply it at load; the oracle applies it here. */
+void or_sns_bsk_round(const or_sns_params* sp, const uint64_t* bsk, uint64_t* out) {
+  const size_t N = sp->N, pairs = or_sns_bsk_len(sp) / (2 * N);
+  const u128 Q = q_value();
+#pragma omp parallel for schedule(static)
+  for (size_t pp = 0; pp < pairs; pp++)
+    for (size_t t = 0; t < N; t++) {
+      const u128 x = crt(bsk[(2 * pp) * N + t], bsk[(2 * pp + 1) * N + t]);
+      const __int128 xc = x > Q / 2 ? (__int128)(x - Q) : (__int128)x;
+      const __int128 rr = (xc + ((__int128)1 << 15)) >> 16; /* floor: arithmetic shift */
+      const __int128 v = rr * 65536;
+      for (int q = 0; q < 2; q++) {
+        const __int128 m = v % (__int128)SP[q];
+        out[(2 * pp + q) * N + t] = (uint64_t)(m < 0 ? m + (__int128)SP[q] : m);
+      }
+    }
+}
+
 void or_sns_bsk_to_ntt(const or_sns_params* sp, const uint64_t* bsk, uint64_t* bsk_ntt) {
   const size_t polys = or_sns_bsk_len(sp) / sp->N;
 #pragma omp parallel for schedule(static)

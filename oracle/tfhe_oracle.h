@@ -201,6 +201,8 @@ void or_sns_ntt_inv(int which, uint64_t* a, uint32_t N);
 size_t or_sns_bsk_len(const or_sns_params* sp);          /* n*(k+1)L*(k+1)*2*N: [i][c*L+l][j][prime][N] */
 void or_sns_keygen(const or_sns_params* sp, uint64_t seed, const uint64_t* lwe_key, uint64_t* glwe_key /* k*N */,
                    uint64_t* bsk /* nullable */);
+/* load-time rounding of the squashing key to multiples of 2^16 (centred mod Q; sns_oracle.c) */
+void or_sns_bsk_round(const or_sns_params* sp, const uint64_t* bsk, uint64_t* out);
 void or_sns_bsk_to_ntt(const or_sns_params* sp, const uint64_t* bsk, uint64_t* bsk_ntt);
 void or_sns_tor_to_q(const uint64_t* t, uint64_t* r);
 void or_sns_q_to_tor(const uint64_t* r, uint64_t* t);

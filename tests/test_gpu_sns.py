@@ -48,3 +48,19 @@ def test_squash_noise_batch(sns_setup, fhevm_engine, fhevm_keys):
     delta = 1 << 123
     noise = [((v - int(m) * delta + (1 << 127)) % (1 << 128)) - (1 << 127) for v, m in zip(key.phase(out), msgs)]
     assert max(abs(e) for e in noise) < 2 ** 72
+
+
+def test_ntt_path_agrees_with_fft_path(sns_setup, fhevm_engine, fhevm_keys, monkeypatch):
+    """The default f64 FFT external product (exact limb convolutions) and the Z_p NTT one
+    (TFHE_HIP_SNS_NTT=1) compute the same Z_Q product of the load-time rounded key: equal accumulators."""
+    sp, osp, key, okey, sq = sns_setup
+    ck, _ = fhevm_keys
+    msgs = np.array([0, 3, 9, 15, 6], dtype=np.uint64)
+    small, _ = fhevm_engine.ms_reduce(fhevm_engine.keyswitch(ck.encrypt(msgs, 16, seed=0xC0FFEE73)))
+    monkeypatch.setenv("TFHE_HIP_SNS_NTT", "1")
+    sq_ntt = S.Squasher(sp, 0).load_key(key)
+    try:
+        assert np.array_equal(sq_ntt.blind_rotate(small), sq.blind_rotate(small))
+        assert np.array_equal(key.decrypt(sq_ntt.squash(small)), msgs)
+    finally:
+        sq_ntt.close()

@@ -64,3 +64,49 @@ def test_oracle_squash_end_to_end(oracle_mod):
     assert [((v + delta // 2) // delta) % 16 for v in ph] == [int(m) for m in msgs]
     noise = [((v - int(m) * delta + (1 << 127)) % (1 << 128)) - (1 << 127) for v, m in zip(ph, msgs)]
     assert max(abs(e) for e in noise) < 2 ** 70      # squashed: ~2^65 of the 2^128 torus
+
+
+def test_key_rounding(oracle_mod):
+    """or_sns_bsk_round (the device's load-time rounding): every coefficient becomes the multiple of
+    2^16 nearest to its centred value mod Q, so a rounded key is 2^16 x a 112-bit integer (seven
+    balanced 16-bit limbs) and moves each coefficient by at most 2^15."""
+    import ctypes
+    osp = oracle_mod.sns_params(0)
+    osp.n = 1
+    keys = oracle_mod.SnsKeys(osp, KEY_SEED, np.array([1], dtype=np.uint64))
+    out = np.zeros_like(keys.bsk)
+    oracle_mod.lib().or_sns_bsk_round(ctypes.byref(osp), oracle_mod._p(keys.bsk), oracle_mod._p(out))
+    p1, p2 = 0xFFFFFFFF00000001, 0xFFFFFFFC00000001
+    Q = p1 * p2
+    inv = pow(p1, -1, p2)
+
+    def crt(r1, r2):
+        return int(r1) + p1 * (((int(r2) - int(r1)) * inv) % p2)
+
+    pairs = keys.bsk.reshape(-1, 2, 2048)
+    rpairs = out.reshape(-1, 2, 2048)
+    rng = np.random.default_rng(5)
+    for pp in rng.integers(0, pairs.shape[0], 6):
+        for t in rng.integers(0, 2048, 40):
+            x = crt(pairs[pp, 0, t], pairs[pp, 1, t])
+            y = crt(rpairs[pp, 0, t], rpairs[pp, 1, t])
+            xc = x - Q if x > Q // 2 else x
+            yc = y - Q if y > Q // 2 else y
+            assert yc % 65536 == 0 and abs(yc - xc) <= 32768 and abs(yc // 65536) < 2 ** 111
+
+
+def test_fft_limb_product_exactness(tmp_path):
+    """tools/sns_fft_check.cpp runs the device's FFT stage functions (tfhe_amd/csrc/sns_fft.h) on the
+    host: 9-term digit x limb products at N = 2048 with uniform and extreme-magnitude random operands
+    land within 0.07 of the exact integers (rint() exact with margin), and the adversarial all-maximum
+    operand (|value| = 2^52.2, no f64 headroom) is reported as the one inexact case."""
+    import subprocess
+    root = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+    exe = tmp_path / "sns_fft_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", f"{root}/tfhe_amd/csrc", f"{root}/tools/sns_fft_check.cpp",
+                    "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), "6"], capture_output=True, text=True).stdout
+    errs = [(int(l.split()[3].rstrip(":")), float(l.split("=")[1].split(",")[0])) for l in out.splitlines()
+            if l.startswith("trial")]
+    assert len(errs) == 6
+    assert all(e < 0.07 for mode, e in errs if mode != 2)

@@ -14,9 +14,11 @@
 // NTTs are the negacyclic Cooley-Tukey / Gentleman-Sande pair with bit-reversed psi tables (input
 // natural -> spectrum bit-reversed -> natural), 2048 points in LDS, 256 threads.
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdlib.h>
 
 #include "pbs_kernels.h"
+#include "sns_fft.h"
 
 namespace tfhe {
 namespace {
@@ -67,6 +69,16 @@ struct Prime<1> {
 template <int Q>
 __device__ __forceinline__ u64 mont_q(u64 a, u64 b) { return mont(a, b, Prime<Q>::p, Prime<Q>::pinv); }
 template <int Q>
+constexpr u64 prime_r2() {  // R^2 mod p (R = 2^64 = 2^64 - p mod p)
+  return (u64)(((u128)((u64)0 - Prime<Q>::p) * (u128)((u64)0 - Prime<Q>::p)) % Prime<Q>::p);
+}
+template <int Q>
+constexpr u64 prime_pow2(int e) {  // 2^e mod p
+  u64 r = 1;
+  for (int i = 0; i < e; i++) r = (u64)(((u128)r * 2) % Prime<Q>::p);
+  return r;
+}
+template <int Q>
 __device__ __forceinline__ u64 addm_q(u64 a, u64 b) { return addm(a, b, Prime<Q>::p); }
 template <int Q>
 __device__ __forceinline__ u64 subm_q(u64 a, u64 b) { return subm(a, b, Prime<Q>::p); }
@@ -78,12 +90,37 @@ __device__ __forceinline__ u128 mulhi128(u128 x, u128 y) {
   return p11 + (p01 >> 64) + (p10 >> 64) + (mid >> 64);
 }
 
-// residues -> x in [0, Q) -> torus y = x + floor((x c + 2^127) / 2^128)
-__device__ __forceinline__ u128 lift_to_torus(u64 r1, u64 r2, const SnsConst& K) {
+// residues -> x in [0, Q) (Garner)
+__device__ __forceinline__ u128 crt_x(u64 r1, u64 r2, const SnsConst& K) {
   constexpr u64 p1 = Prime<0>::p, p2 = Prime<1>::p;
   const u64 r1m = r1 >= p2 ? r1 - p2 : r1;
   const u64 t = mont_q<1>(subm_q<1>(r2, r1m), K.p1inv_m);
-  const u128 x = (u128)r1 + (u128)p1 * t;
+  return (u128)r1 + (u128)p1 * t;
+}
+
+// signed v, |v| < 2^127 - 2^96 -> v mod p
+template <int Q>
+__device__ __forceinline__ u64 reduce_s128(__int128 v) {
+  constexpr u64 p = Prime<Q>::p;
+  const u128 u = (u128)(v + ((__int128)p << 63));
+  u64 hi = (u64)(u >> 64), lo = (u64)u;
+  if (hi >= p) hi -= p;
+  if (lo >= p) lo -= p;
+  return addm_q<Q>(lo, mont_q<Q>(hi, prime_r2<Q>()));
+}
+
+// the load-time key rounding (oracle: or_sns_bsk_round): x centred in (-Q/2, Q/2], rounded to the
+// nearest multiple of 2^SF_DROP; returns x' / 2^SF_DROP (a signed 112-bit integer)
+__device__ __forceinline__ __int128 round_key(u64 r1, u64 r2, const SnsConst& K) {
+  constexpr u128 Qv = (u128)Prime<0>::p * Prime<1>::p;
+  const u128 x = crt_x(r1, r2, K);
+  const __int128 xc = x > (Qv >> 1) ? (__int128)(x - Qv) : (__int128)x;
+  return (xc + ((__int128)1 << (snsf::SF_DROP - 1))) >> snsf::SF_DROP;
+}
+
+// residues -> x in [0, Q) -> torus y = x + floor((x c + 2^127) / 2^128)
+__device__ __forceinline__ u128 lift_to_torus(u64 r1, u64 r2, const SnsConst& K) {
+  const u128 x = crt_x(r1, r2, K);
   const u128 c = ((u128)K.conv_hi << 64) | K.conv_lo;
   const u128 lo = x * c;
   return x + mulhi128(x, c) + (u128)((lo >> 127) & 1);
@@ -214,7 +251,12 @@ __global__ void __launch_bounds__(ST) sns_bsk_to_ntt_kernel(const u64* __restric
   const size_t poly = blockIdx.x;
   const int q = (int)(poly & 1);  // [..][prime][N]
   const SnsConst& K = *Kc;
-  for (int x = threadIdx.x; x < SN; x += ST) a[x] = in[poly * SN + x];
+  // the load-time rounding (round_key) needs both residues of each coefficient: the pair's other poly
+  const u64* pr = in + (poly & ~(size_t)1) * SN;
+  for (int x = threadIdx.x; x < SN; x += ST) {
+    const __int128 v = round_key(pr[x], pr[SN + x], K) * ((__int128)1 << snsf::SF_DROP);
+    a[x] = q ? reduce_s128<1>(v) : reduce_s128<0>(v);
+  }
   __syncthreads();
   if (q) {
     ntt_fwd_lds<1>(a, K.psi_rev[1]);
@@ -263,9 +305,8 @@ __device__ __forceinline__ void step1_level(const int* dg, u64* buf, const SnsCo
 
 // step 1 of CMUX i for (ciphertext ct, component c): X^{a_i} acc_c - acc_c, CRT lift, torus map, 3 digit
 // levels, forward NTT of each in both primes -> D; shared scratch rot (2 x N u64), dig (3 x N int), buf (N u64)
-__device__ void step1_body(const u64* __restrict__ lwe, int n, int i, const u64* __restrict__ acc,
-                           u64* __restrict__ D, const SnsConst& K, int ct, int c, u64 (*rot)[SN], int (*dig)[SN],
-                           u64* buf) {
+__device__ void step1_digits(const u64* __restrict__ lwe, int n, int i, const u64* __restrict__ acc,
+                             const SnsConst& K, int ct, int c, u64 (*rot)[SN], int (*dig)[SN]) {
   const u32 ai = mod_switch_4096(lwe[(size_t)ct * (n + 1) + i]);
   const u64* a = acc + ((size_t)ct * (SK + 1) + c) * 2 * SN;
   for (int x = threadIdx.x; x < 2 * SN; x += ST) {
@@ -297,6 +338,12 @@ __device__ void step1_body(const u64* __restrict__ lwe, int n, int i, const u64*
     }
   }
   __syncthreads();
+}
+
+__device__ void step1_body(const u64* __restrict__ lwe, int n, int i, const u64* __restrict__ acc,
+                           u64* __restrict__ D, const SnsConst& K, int ct, int c, u64 (*rot)[SN], int (*dig)[SN],
+                           u64* buf) {
+  step1_digits(lwe, n, i, acc, K, ct, c, rot, dig);
   for (int l = 0; l < SL; l++) {
     step1_level<0>(dig[l], buf, K, D + (((size_t)ct * SR + c * SL + l) * 2 + 0) * SN);
     step1_level<1>(dig[l], buf, K, D + (((size_t)ct * SR + c * SL + l) * 2 + 1) * SN);
@@ -361,6 +408,245 @@ __global__ void __launch_bounds__(ST) sns_fused_kernel(const u64* __restrict__ l
       __syncthreads();
     }
   }
+}
+
+// ---- the f64 FFT external product (default; sns_fft.h) ------------------------------------------
+// Layouts: key spectra Kf[i][r][j][t][M] (r = c L + l, t = limb, scaled by 1/M), digit spectra
+// Df[ct][r][M], both in the DIF's digit-reversed order; tables in SnsFftConst.
+using snsf::cd;
+using snsf::SF_LIMBS;
+using snsf::SF_M;
+
+struct SnsFftConst {
+  cd T[SF_M];           // e^{2 pi i e / M}
+  cd P[SF_M];           // psi^m = e^{i pi m / N}
+  u64 W[2][SF_LIMBS];   // limb weights 2^(SF_DROP + 16 t) mod p1, p2
+};
+
+__device__ __forceinline__ void fft_fwd_lds(cd* buf, const cd* __restrict__ T) {
+#pragma unroll
+  for (int s = 0; s < 5; s++) {
+    snsf::dif_stage(buf, s, threadIdx.x, T);
+    __syncthreads();
+  }
+}
+__device__ __forceinline__ void fft_inv_lds(cd* buf, const cd* __restrict__ T) {
+#pragma unroll
+  for (int s = 4; s >= 0; s--) {
+    snsf::dit_stage(buf, s, threadIdx.x, T);
+    __syncthreads();
+  }
+}
+
+// BSK standard domain (residue pairs) -> rounded key, 7 balanced 16-bit limbs, spectra / M.
+// One workgroup per (i, r, j) polynomial pair.
+__global__ void __launch_bounds__(ST) sns_bsk_to_fft_kernel(const u64* __restrict__ in, cd* __restrict__ out,
+                                                            const SnsConst* __restrict__ Kc,
+                                                            const SnsFftConst* __restrict__ Fc) {
+  __shared__ cd buf[SF_M];
+  const size_t pair = blockIdx.x;
+  const SnsConst& K = *Kc;
+  const SnsFftConst& F = *Fc;
+  const u64* pr = in + pair * 2 * SN;
+  __int128 rr[8];  // coefficients m = tid + 256 u (u < 4) and m + 1024
+#pragma unroll
+  for (int u = 0; u < 4; u++)
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int x = threadIdx.x + 256 * u + SF_M * h;
+      rr[2 * u + h] = round_key(pr[x], pr[SN + x], K);
+    }
+  for (int t = 0; t < SF_LIMBS; t++) {
+    double lv[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      if (t == SF_LIMBS - 1) {
+        lv[e] = (double)(long long)rr[e];  // the top limb keeps the remainder (|.| <= 2^15)
+      } else {
+        const __int128 l = ((rr[e] + 0x8000) & 0xFFFF) - 0x8000;
+        rr[e] = (rr[e] - l) >> 16;
+        lv[e] = (double)(long long)l;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int m = threadIdx.x + 256 * u;
+      buf[m] = snsf::cmul(cd{lv[2 * u], lv[2 * u + 1]}, F.P[m]);
+    }
+    __syncthreads();
+    fft_fwd_lds(buf, F.T);
+    cd* o = out + (pair * SF_LIMBS + t) * SF_M;
+    constexpr double inv_m = 1.0 / SF_M;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int f = threadIdx.x + 256 * u;
+      o[f] = cd{buf[f].x * inv_m, buf[f].y * inv_m};
+    }
+    __syncthreads();
+  }
+}
+
+// step 1 (ciphertext, component c): rotation, CRT lift, torus map, 3 digit levels (as the NTT path),
+// then the folded, twisted forward FFT of each digit polynomial -> Df
+__global__ void __launch_bounds__(ST) sns_step1f_kernel(const u64* __restrict__ lwe, int n, int i,
+                                                        const u64* __restrict__ acc, cd* __restrict__ Df,
+                                                        const SnsConst* __restrict__ Kc,
+                                                        const SnsFftConst* __restrict__ Fc) {
+  __shared__ u64 rot[2][SN];
+  __shared__ int dig[SL][SN];
+  const int ct = blockIdx.x / (SK + 1), c = blockIdx.x % (SK + 1);
+  const SnsFftConst& F = *Fc;
+  step1_digits(lwe, n, i, acc, *Kc, ct, c, rot, dig);
+  cd* buf = reinterpret_cast<cd*>(&rot[0][0]);  // rot is dead once the digits are out
+  for (int l = 0; l < SL; l++) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int m = threadIdx.x + 256 * u;
+      buf[m] = snsf::cmul(cd{(double)dig[l][m], (double)dig[l][m + SF_M]}, F.P[m]);
+    }
+    __syncthreads();
+    fft_fwd_lds(buf, F.T);
+    cd* o = Df + ((size_t)ct * SR + c * SL + l) * SF_M;
+#pragma unroll
+    for (int u = 0; u < 4; u++) o[threadIdx.x + 256 * u] = buf[threadIdx.x + 256 * u];
+    __syncthreads();
+  }
+}
+
+// one limb of step 2: MAC over the 9 rows, inverse FFT, untwist, rint -> exact integers, weighted
+// into the per-prime int128 sums
+__device__ __forceinline__ void step2f_limb(const cd* __restrict__ d, const cd* __restrict__ kf, int j, int T,
+                                            cd* buf, const SnsFftConst& F, __int128 (&s0)[8], __int128 (&s1)[8]) {
+#pragma unroll 1
+  for (int u = 0; u < 4; u++) {
+    const int f = threadIdx.x + 256 * u;
+    cd o = {0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < SR; r++)
+      o = snsf::cmac(o, d[(size_t)r * SF_M + f], kf[(((size_t)r * (SK + 1) + j) * SF_LIMBS + T) * SF_M + f]);
+    buf[f] = o;
+  }
+  __syncthreads();
+  fft_inv_lds(buf, F.T);
+  const __int128 w0 = (__int128)F.W[0][T], w1 = (__int128)F.W[1][T];
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int m = threadIdx.x + 256 * u;
+    const cd y = snsf::cmulc(buf[m], F.P[m]);
+    const long long c0 = (long long)__builtin_rint(y.x), c1 = (long long)__builtin_rint(y.y);
+    s0[2 * u] += (__int128)c0 * w0;
+    s1[2 * u] += (__int128)c0 * w1;
+    s0[2 * u + 1] += (__int128)c1 * w0;
+    s1[2 * u + 1] += (__int128)c1 * w1;
+  }
+  __syncthreads();
+}
+
+// step 2 (ciphertext, output component j): all limbs of the external product, acc_j += (mod p1, p2)
+__global__ void __launch_bounds__(ST) sns_step2f_kernel(const cd* __restrict__ Df, const cd* __restrict__ kf_i,
+                                                        u64* __restrict__ acc, const SnsFftConst* __restrict__ Fc) {
+  __shared__ cd buf[SF_M];
+  const int j = blockIdx.x % (SK + 1), ct = blockIdx.x / (SK + 1);
+  const SnsFftConst& F = *Fc;
+  const cd* d = Df + (size_t)ct * SR * SF_M;
+  __int128 s0[8], s1[8];
+#pragma unroll
+  for (int e = 0; e < 8; e++) s0[e] = s1[e] = 0;
+#pragma unroll 1
+  for (int t = 0; t < SF_LIMBS; t++) step2f_limb(d, kf_i, j, t, buf, F, s0, s1);
+  u64* a0 = acc + ((size_t)ct * (SK + 1) + j) * 2 * SN;
+  u64* a1 = a0 + SN;
+#pragma unroll
+  for (int u = 0; u < 4; u++)
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int x = threadIdx.x + 256 * u + SF_M * h;
+      a0[x] = addm_q<0>(a0[x], reduce_s128<0>(s0[2 * u + h]));
+      a1[x] = addm_q<1>(a1[x], reduce_s128<1>(s1[2 * u + h]));
+    }
+}
+
+// Step 2 split for key reuse across ciphertexts (default): the MAC as a frequency-tiled kernel whose
+// workgroup holds the CMUX's key for 16 frequencies x all 21 (output, limb) columns in LDS (48 KB)
+// and streams 32 ciphertexts' digit spectra through it, writing the products O[ct][j*7+t][M] to
+// global memory; then one workgroup per (ciphertext, output) runs the 7 inverse FFTs, rint, the limb
+// weights and acc_j += (mod p1, p2).  The one-kernel form (sns_step2f_kernel, TFHE_HIP_SNS_FUSED2=1)
+// re-reads the ~1 MB per-output key slice for every ciphertext.
+constexpr int MAC_F = 16, MAC_CT = 32, MAC_JT = (SK + 1) * SF_LIMBS;  // 21 (output, limb) columns
+
+__global__ void __launch_bounds__(ST) sns_mac_kernel(const cd* __restrict__ Df, const cd* __restrict__ kf_i,
+                                                     cd* __restrict__ O, int B) {
+  __shared__ cd kt[SR * MAC_JT][MAC_F];  // [r * 21 + jt][f]
+  const int f0 = (blockIdx.x % (SF_M / MAC_F)) * MAC_F;
+  const int c0 = (blockIdx.x / (SF_M / MAC_F)) * MAC_CT;
+  // key tile: row (r, jt) of the CMUX's key = kf_i[(r * 21 + jt) * M + f0 .. + 16]
+  for (int x = threadIdx.x; x < SR * MAC_JT * MAC_F; x += ST) {
+    const int row = x / MAC_F, f = x % MAC_F;
+    kt[row][f] = kf_i[(size_t)row * SF_M + f0 + f];
+  }
+  __syncthreads();
+  const int f = threadIdx.x % MAC_F, cl = threadIdx.x / MAC_F;  // 16 frequencies x 16 ciphertext lanes
+  const int ca = c0 + cl, cb = c0 + cl + 16;
+  const bool va = ca < B, vb = cb < B;
+  cd da[SR], db[SR];
+#pragma unroll
+  for (int r = 0; r < SR; r++) {
+    da[r] = va ? Df[((size_t)ca * SR + r) * SF_M + f0 + f] : cd{0.0, 0.0};
+    db[r] = vb ? Df[((size_t)cb * SR + r) * SF_M + f0 + f] : cd{0.0, 0.0};
+  }
+#pragma unroll 1
+  for (int jt = 0; jt < MAC_JT; jt++) {
+    cd oa = {0.0, 0.0}, ob = {0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < SR; r++) {
+      const cd k = kt[r * MAC_JT + jt][f];
+      oa = snsf::cmac(oa, da[r], k);
+      ob = snsf::cmac(ob, db[r], k);
+    }
+    if (va) O[((size_t)ca * MAC_JT + jt) * SF_M + f0 + f] = oa;
+    if (vb) O[((size_t)cb * MAC_JT + jt) * SF_M + f0 + f] = ob;
+  }
+}
+
+// the 7 inverse FFTs of (ciphertext, output j), rint, limb weights, acc_j += (mod p1, p2)
+__global__ void __launch_bounds__(ST) sns_inv_kernel(const cd* __restrict__ O, u64* __restrict__ acc,
+                                                     const SnsFftConst* __restrict__ Fc) {
+  __shared__ cd buf[SF_M];
+  const int j = blockIdx.x % (SK + 1), ct = blockIdx.x / (SK + 1);
+  const SnsFftConst& F = *Fc;
+  __int128 s0[8], s1[8];
+#pragma unroll
+  for (int e = 0; e < 8; e++) s0[e] = s1[e] = 0;
+#pragma unroll 1
+  for (int t = 0; t < SF_LIMBS; t++) {
+    const cd* o = O + ((size_t)ct * MAC_JT + j * SF_LIMBS + t) * SF_M;
+#pragma unroll
+    for (int u = 0; u < 4; u++) buf[threadIdx.x + 256 * u] = o[threadIdx.x + 256 * u];
+    __syncthreads();
+    fft_inv_lds(buf, F.T);
+    const __int128 w0 = (__int128)F.W[0][t], w1 = (__int128)F.W[1][t];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int m = threadIdx.x + 256 * u;
+      const cd y = snsf::cmulc(buf[m], F.P[m]);
+      const long long c0 = (long long)__builtin_rint(y.x), c1 = (long long)__builtin_rint(y.y);
+      s0[2 * u] += (__int128)c0 * w0;
+      s1[2 * u] += (__int128)c0 * w1;
+      s0[2 * u + 1] += (__int128)c1 * w0;
+      s1[2 * u + 1] += (__int128)c1 * w1;
+    }
+    __syncthreads();
+  }
+  u64* a0 = acc + ((size_t)ct * (SK + 1) + j) * 2 * SN;
+  u64* a1 = a0 + SN;
+#pragma unroll
+  for (int u = 0; u < 4; u++)
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int x = threadIdx.x + 256 * u + SF_M * h;
+      a0[x] = addm_q<0>(a0[x], reduce_s128<0>(s0[2 * u + h]));
+      a1[x] = addm_q<1>(a1[x], reduce_s128<1>(s1[2 * u + h]));
+    }
 }
 
 // acc -> LWE over Z_2^128 (dim k N, + body), (lo, hi) pairs
@@ -474,6 +760,59 @@ hipError_t launch_sns_blind_rotate(const u64* lwe, size_t B, int n, const u64* l
   for (int i = 0; i < n; i++) {
     sns_step1_kernel<<<(unsigned)(B * (SK + 1)), ST, 0, s>>>(lwe, n, i, acc, D, K);
     sns_step2_kernel<<<(unsigned)(B * (SK + 1) * 2), ST, 0, s>>>(D, bsk_ntt + bsk_i * i, acc, K);
+  }
+  return hipGetLastError();
+}
+
+size_t sns_fft_const_bytes() { return sizeof(SnsFftConst); }
+
+void make_sns_fft_const(void* out) {
+  SnsFftConst& F = *(SnsFftConst*)out;
+  const long double pi = 3.141592653589793238462643383279502884L;
+  for (int e = 0; e < SF_M; e++) {
+    F.T[e] = cd{(double)cosl(2 * pi * e / SF_M), (double)sinl(2 * pi * e / SF_M)};
+    F.P[e] = cd{(double)cosl(pi * e / SN), (double)sinl(pi * e / SN)};
+  }
+  for (int t = 0; t < SF_LIMBS; t++) {
+    F.W[0][t] = prime_pow2<0>(snsf::SF_DROP + snsf::SF_LIMB_BITS * t);
+    F.W[1][t] = prime_pow2<1>(snsf::SF_DROP + snsf::SF_LIMB_BITS * t);
+  }
+}
+
+size_t sns_fft_key_len(size_t n) { return n * SR * (SK + 1) * SF_LIMBS * SF_M; }  // in cd (16 B)
+
+// `pairs` (i, r, j) polynomial pairs of the standard-domain key -> spectra
+hipError_t launch_sns_bsk_to_fft(const u64* bsk_std, void* bsk_fft, size_t pairs, const void* d_const,
+                                 const void* d_fconst, hipStream_t s) {
+  sns_bsk_to_fft_kernel<<<(unsigned)pairs, ST, 0, s>>>(bsk_std, (cd*)bsk_fft, (const SnsConst*)d_const,
+                                                        (const SnsFftConst*)d_fconst);
+  return hipGetLastError();
+}
+
+// one squash pass over B ciphertexts on the f64 FFT path (acc B x 3 x 2 x N u64, D B x 9 x M cd)
+size_t sns_fft_prod_len(size_t B) { return B * MAC_JT * SF_M; }  // O workspace, in cd
+
+hipError_t launch_sns_blind_rotate_fft(const u64* lwe, size_t B, int n, const u64* lut, const void* bsk_fft, u64* acc,
+                                       void* D, void* Oprod, const void* d_const, const void* d_fconst,
+                                       hipStream_t s) {
+  const SnsConst* K = (const SnsConst*)d_const;
+  const SnsFftConst* F = (const SnsFftConst*)d_fconst;
+  sns_init_kernel<<<(unsigned)B, 256, 0, s>>>(lwe, n, lut, acc, K);
+  const size_t per_i = (size_t)SR * (SK + 1) * SF_LIMBS * SF_M;
+  static const bool fused2 = [] {
+    const char* e = getenv("TFHE_HIP_SNS_FUSED2");
+    return e && e[0] == '1';
+  }();
+  const unsigned mac_grid = (unsigned)((SF_M / MAC_F) * ((B + MAC_CT - 1) / MAC_CT));
+  for (int i = 0; i < n; i++) {
+    const cd* kf_i = (const cd*)bsk_fft + per_i * i;
+    sns_step1f_kernel<<<(unsigned)(B * (SK + 1)), ST, 0, s>>>(lwe, n, i, acc, (cd*)D, K, F);
+    if (fused2 || !Oprod) {
+      sns_step2f_kernel<<<(unsigned)(B * (SK + 1)), ST, 0, s>>>((const cd*)D, kf_i, acc, F);
+    } else {
+      sns_mac_kernel<<<mac_grid, ST, 0, s>>>((const cd*)D, kf_i, (cd*)Oprod, (int)B);
+      sns_inv_kernel<<<(unsigned)(B * (SK + 1)), ST, 0, s>>>((const cd*)Oprod, acc, F);
+    }
   }
   return hipGetLastError();
 }

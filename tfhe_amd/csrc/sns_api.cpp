@@ -3,6 +3,7 @@
 #include <hip/hip_runtime_api.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -63,10 +64,14 @@ struct tfhe_sns_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   void* d_const = nullptr;
-  u64* d_bsk = nullptr;
+  void* d_fconst = nullptr;
+  bool ntt = false;        // TFHE_HIP_SNS_NTT=1 at create: the Z_p NTT external product instead of the f64 FFT
+  u64* d_bsk = nullptr;    // NTT path: key in the NTT domain (n x 9 x 3 x 2 x N u64)
+  void* d_bskf = nullptr;  // FFT path: key limb spectra (n x 9 x 3 x 7 x 1024 complex f64)
   bool key = false;
   u64* d_acc = nullptr;
   u64* d_D = nullptr;
+  void* d_O = nullptr;  // FFT path: MAC products (chunk x 21 x 1024 complex)
   u64* d_lut = nullptr;
   uint32_t lut_mm = 0;
   size_t ws_cap = 0;
@@ -81,11 +86,14 @@ int ensure_ws(tfhe_sns_ctx* c, size_t B) {
   if (c->ws_cap >= B) return 0;
   (void)hipFree(c->d_acc);
   (void)hipFree(c->d_D);
+  (void)hipFree(c->d_O);
   c->d_acc = c->d_D = nullptr;
+  c->d_O = nullptr;
   c->ws_cap = 0;
   const size_t poly = 2 * (size_t)c->sp.N;
   SNS_TRY(hipMalloc(&c->d_acc, B * (c->sp.k + 1) * poly * 8));
   SNS_TRY(hipMalloc(&c->d_D, B * (c->sp.k + 1) * c->sp.level * poly * 8));
+  if (!c->ntt) SNS_TRY(hipMalloc(&c->d_O, tfhe::sns_fft_prod_len(B) * 16));
   c->ws_cap = B;
   return 0;
 }
@@ -109,8 +117,12 @@ int run_device(tfhe_sns_ctx* c, const u64* d_in, size_t B, u64* d_out, u64* d_ac
   const size_t acc_len = (size_t)(c->sp.k + 1) * 2 * c->sp.N;
   for (size_t f = 0; f < B; f += chunk) {
     const size_t nb = std::min(chunk, B - f);
-    SNS_TRY(tfhe::launch_sns_blind_rotate(d_in + f * in_dim, nb, (int)c->sp.n, c->d_lut, c->d_bsk, c->d_acc, c->d_D,
-                                          c->d_const, s));
+    if (c->ntt)
+      SNS_TRY(tfhe::launch_sns_blind_rotate(d_in + f * in_dim, nb, (int)c->sp.n, c->d_lut, c->d_bsk, c->d_acc,
+                                            c->d_D, c->d_const, s));
+    else
+      SNS_TRY(tfhe::launch_sns_blind_rotate_fft(d_in + f * in_dim, nb, (int)c->sp.n, c->d_lut, c->d_bskf, c->d_acc,
+                                                c->d_D, c->d_O, c->d_const, c->d_fconst, s));
     if (d_out) SNS_TRY(tfhe::launch_sns_extract(c->d_acc, nb, d_out + f * out_dim, c->d_const, s));
     if (d_acc_out)
       SNS_TRY(hipMemcpyAsync(d_acc_out + f * acc_len, c->d_acc, nb * acc_len * 8, hipMemcpyDeviceToDevice, s));
@@ -181,11 +193,16 @@ int tfhe_hip_sns_create(const tfhe_sns_params* sp, int device, tfhe_sns_ctx** ou
   tfhe_sns_ctx* c = new tfhe_sns_ctx();
   c->sp = *sp;
   c->device = device;
-  std::vector<unsigned char> K(tfhe::sns_const_bytes());
+  const char* e = getenv("TFHE_HIP_SNS_NTT");
+  c->ntt = e && e[0] == '1';
+  std::vector<unsigned char> K(tfhe::sns_const_bytes()), F(tfhe::sns_fft_const_bytes());
   tfhe::make_sns_const(K.data());
+  tfhe::make_sns_fft_const(F.data());
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->d_const, K.size()) != hipSuccess ||
-      hipMemcpy(c->d_const, K.data(), K.size(), hipMemcpyHostToDevice) != hipSuccess) {
+      hipMemcpy(c->d_const, K.data(), K.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMalloc(&c->d_fconst, F.size()) != hipSuccess ||
+      hipMemcpy(c->d_fconst, F.data(), F.size(), hipMemcpyHostToDevice) != hipSuccess) {
     tfhe_hip_sns_destroy(c);
     return fail(TFHE_HIP_EDEVICE, "sns_create: device setup failed");
   }
@@ -198,7 +215,8 @@ void tfhe_hip_sns_destroy(tfhe_sns_ctx* c) {
   {
     DevGuard g(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (void* p : {(void*)c->d_const, (void*)c->d_bsk, (void*)c->d_acc, (void*)c->d_D, (void*)c->d_lut, (void*)c->d_io})
+    for (void* p : {(void*)c->d_const, c->d_fconst, (void*)c->d_bsk, c->d_bskf, (void*)c->d_acc, (void*)c->d_D,
+                    c->d_O, (void*)c->d_lut, (void*)c->d_io})
       (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
   }
@@ -212,7 +230,8 @@ int tfhe_hip_sns_load_key(tfhe_sns_ctx* c, const uint64_t* bsk, size_t len) {
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
   c->key = false;
-  if (!c->d_bsk) SNS_TRY(hipMalloc(&c->d_bsk, len * 8));
+  if (c->ntt && !c->d_bsk) SNS_TRY(hipMalloc(&c->d_bsk, len * 8));
+  if (!c->ntt && !c->d_bskf) SNS_TRY(hipMalloc(&c->d_bskf, tfhe::sns_fft_key_len(c->sp.n) * 16));
   // stage the standard-domain key in chunks through the io buffer, convert in place
   const size_t polys = len / c->sp.N, per = 4096;
   const size_t bytes = per * c->sp.N * 8;
@@ -226,7 +245,11 @@ int tfhe_hip_sns_load_key(tfhe_sns_ctx* c, const uint64_t* bsk, size_t len) {
   for (size_t f = 0; f < polys; f += per) {
     const size_t np = std::min(per, polys - f);
     SNS_TRY(hipMemcpyAsync(c->d_io, bsk + f * c->sp.N, np * c->sp.N * 8, hipMemcpyHostToDevice, c->stream));
-    SNS_TRY(tfhe::launch_sns_bsk_to_ntt(c->d_io, c->d_bsk + f * c->sp.N, np, c->d_const, c->stream));
+    if (c->ntt)
+      SNS_TRY(tfhe::launch_sns_bsk_to_ntt(c->d_io, c->d_bsk + f * c->sp.N, np, c->d_const, c->stream));
+    else  // np is even (pairs of primes never straddle a chunk): 7 limb spectra per pair
+      SNS_TRY(tfhe::launch_sns_bsk_to_fft(c->d_io, (char*)c->d_bskf + (f / 2) * tfhe::SNS_FFT_PAIR_BYTES, np / 2,
+                                          c->d_const, c->d_fconst, c->stream));
   }
   SNS_TRY(hipStreamSynchronize(c->stream));
   c->key = true;
