@@ -273,6 +273,11 @@ int tfhe_hip_sns_keygen(const tfhe_sns_params* sp, uint64_t seed, const uint64_t
 typedef struct tfhe_sns_ctx tfhe_sns_ctx;
 int tfhe_hip_sns_create(const tfhe_sns_params* sp, int device, tfhe_sns_ctx** out);
 void tfhe_hip_sns_destroy(tfhe_sns_ctx* ctx);
+/* Loading rounds every key coefficient (centred mod Q) to the nearest multiple of 2^16 (oracle:
+ * or_sns_bsk_round; ~2^20 of extra phase noise beside the key's 2^30).  The default external product
+ * splits the rounded key into seven 16-bit limbs and computes each digit x limb convolution as an
+ * exact f64 FFT product (5.7 KB of key spectra per coefficient row: n x 9 x 3 x 7 x 1024 complex, 2.8 GB
+ * at n = 918); TFHE_HIP_SNS_NTT=1 at create selects the Z_p NTT product instead (same results). */
 int tfhe_hip_sns_load_key(tfhe_sns_ctx* ctx, const uint64_t* bsk, size_t len);
 /* B small-key ciphertexts (B x (n+1)) -> B x (k*N+1) x 2 u64; identity LUT over msg_modulus values */
 int tfhe_hip_sns_squash(tfhe_sns_ctx* ctx, const uint64_t* lwe_small, size_t B, uint32_t msg_modulus, uint64_t* out);

@@ -64,3 +64,16 @@ def test_ntt_path_agrees_with_fft_path(sns_setup, fhevm_engine, fhevm_keys, monk
         assert np.array_equal(key.decrypt(sq_ntt.squash(small)), msgs)
     finally:
         sq_ntt.close()
+
+
+@pytest.mark.parametrize("switch", ["TFHE_HIP_SNS_FUSED2", "TFHE_HIP_SNS_INVW"])
+def test_fft_variants_agree(sns_setup, fhevm_engine, fhevm_keys, monkeypatch, switch):
+    """The measured alternatives of the FFT path (one-kernel step 2; one wave per limb inverse) give the
+    default path's accumulators bit for bit."""
+    sp, osp, key, okey, sq = sns_setup
+    ck, _ = fhevm_keys
+    msgs = np.array([2, 11], dtype=np.uint64)
+    small, _ = fhevm_engine.ms_reduce(fhevm_engine.keyswitch(ck.encrypt(msgs, 16, seed=0xC0FFEE74)))
+    ref = sq.blind_rotate(small)
+    monkeypatch.setenv(switch, "1")
+    assert np.array_equal(sq.blind_rotate(small), ref)

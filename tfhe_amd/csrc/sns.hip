@@ -421,6 +421,7 @@ struct SnsFftConst {
   cd T[SF_M];           // e^{2 pi i e / M}
   cd P[SF_M];           // psi^m = e^{i pi m / N}
   u64 W[2][SF_LIMBS];   // limb weights 2^(SF_DROP + 16 t) mod p1, p2
+  u64 WM[2][SF_LIMBS];  // the same in Montgomery form (x R mod p): mont(c, WM) = c 2^(SF_DROP + 16 t) mod p
 };
 
 __device__ __forceinline__ void fft_fwd_lds(cd* buf, const cd* __restrict__ T) {
@@ -431,7 +432,7 @@ __device__ __forceinline__ void fft_fwd_lds(cd* buf, const cd* __restrict__ T) {
   }
 }
 __device__ __forceinline__ void fft_inv_lds(cd* buf, const cd* __restrict__ T) {
-#pragma unroll
+#pragma unroll  // unrolled: the twiddle loads of later stages are issued early (measured faster rolled-up too)
   for (int s = 4; s >= 0; s--) {
     snsf::dit_stage(buf, s, threadIdx.x, T);
     __syncthreads();
@@ -486,30 +487,58 @@ __global__ void __launch_bounds__(ST) sns_bsk_to_fft_kernel(const u64* __restric
   }
 }
 
+// LDS visibility of a wave's own writes to its other lanes (DS ops of a wave complete in order)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // step 1 (ciphertext, component c): rotation, CRT lift, torus map, 3 digit levels (as the NTT path),
-// then the folded, twisted forward FFT of each digit polynomial -> Df
+// then the folded, twisted forward FFT of each digit polynomial -> Df; wave l transforms level l in
+// registers (sns_fft.h passes), its padded exchange buffer aliasing the dead rotation / digit arrays
 __global__ void __launch_bounds__(ST) sns_step1f_kernel(const u64* __restrict__ lwe, int n, int i,
                                                         const u64* __restrict__ acc, cd* __restrict__ Df,
                                                         const SnsConst* __restrict__ Kc,
                                                         const SnsFftConst* __restrict__ Fc) {
   __shared__ u64 rot[2][SN];
   __shared__ int dig[SL][SN];
+  static_assert(sizeof(rot) + sizeof(dig) >= SL * snsf::SF_PADDED * sizeof(cd), "exchange buffers alias rot + dig");
   const int ct = blockIdx.x / (SK + 1), c = blockIdx.x % (SK + 1);
   const SnsFftConst& F = *Fc;
   step1_digits(lwe, n, i, acc, *Kc, ct, c, rot, dig);
-  cd* buf = reinterpret_cast<cd*>(&rot[0][0]);  // rot is dead once the digits are out
-  for (int l = 0; l < SL; l++) {
+  const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+  cd x[16];
+  if (w < SL) {
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int m = threadIdx.x + 256 * u;
-      buf[m] = snsf::cmul(cd{(double)dig[l][m], (double)dig[l][m + SF_M]}, F.P[m]);
+    for (int r = 0; r < 16; r++) {
+      const int m = snsf::pt01(t, r);
+      x[r] = snsf::cmul(cd{(double)dig[w][m], (double)dig[w][m + SF_M]}, F.P[m]);
     }
-    __syncthreads();
-    fft_fwd_lds(buf, F.T);
-    cd* o = Df + ((size_t)ct * SR + c * SL + l) * SF_M;
+    snsf::dif_pass01(x, t, F.T);
+  }
+  __syncthreads();  // every digit read is done before the exchange buffers overwrite rot / dig
+  if (w < SL) {
+    cd* buf = reinterpret_cast<cd*>(&rot[0][0]) + w * snsf::SF_PADDED;
 #pragma unroll
-    for (int u = 0; u < 4; u++) o[threadIdx.x + 256 * u] = buf[threadIdx.x + 256 * u];
-    __syncthreads();
+    for (int r = 0; r < 16; r++) buf[snsf::pad(snsf::pt01(t, r))] = x[r];
+    wave_sync();
+#pragma unroll
+    for (int r = 0; r < 16; r++) x[r] = buf[snsf::pad(snsf::pt23(t, r))];
+    snsf::dif_pass23(x, t, F.T);
+#pragma unroll
+    for (int r = 0; r < 16; r++) buf[snsf::pad(snsf::pt23(t, r))] = x[r];
+    wave_sync();
+#pragma unroll
+    for (int r = 0; r < 16; r++) x[r] = buf[snsf::pad(snsf::pt4(t, r))];
+    snsf::dif_pass4(x, F.T);
+    wave_sync();  // every lane has read its pass-4 inputs before the buffer takes the outputs
+#pragma unroll
+    for (int r = 0; r < 16; r++) buf[snsf::pad(snsf::pt4(t, r))] = x[r];
+    wave_sync();
+    cd* o = Df + ((size_t)ct * SR + c * SL + w) * SF_M;  // spectra in DIF position order, stored contiguously
+#pragma unroll
+    for (int r = 0; r < 16; r++) o[64 * r + t] = buf[snsf::pad(64 * r + t)];
   }
 }
 
@@ -608,7 +637,79 @@ __global__ void __launch_bounds__(ST) sns_mac_kernel(const cd* __restrict__ Df, 
   }
 }
 
-// the 7 inverse FFTs of (ciphertext, output j), rint, limb weights, acc_j += (mod p1, p2)
+// (TFHE_HIP_SNS_INVW=1, measured slower: 2 waves/SIMD at 256 VGPRs) the 7 inverse FFTs of (ciphertext, output j) — one per wave, two rounds (limbs 0-3, 4-6) — each
+// untwisted and rounded to exact int64 coefficients in the wave's buffer; every thread then folds its 8
+// coefficients' limb values into two exact int128 partial sums (A = sum_{t<4} c_t 2^16t, B = sum_{t>=4}
+// c_t 2^16(t-4); |A| < 2^102, |B| < 2^86), and the product 2^16 (A + 2^64 B) reduces once per prime:
+// acc_j += (mod p1, p2)
+__global__ void __launch_bounds__(ST, 2) sns_inv_wave_kernel(const cd* __restrict__ O, u64* __restrict__ acc,
+                                                        const SnsFftConst* __restrict__ Fc) {
+  __shared__ cd bufs[4][snsf::SF_PADDED];
+  const int j = blockIdx.x % (SK + 1), ct = blockIdx.x / (SK + 1);
+  const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const SnsFftConst& F = *Fc;
+  cd* buf = bufs[w];
+  long long* ci = reinterpret_cast<long long*>(buf);
+  __int128 ab[2][8];
+#pragma unroll 1
+  for (int round = 0; round < 2; round++) {
+    const int lim = round * 4 + w, nw = round ? SF_LIMBS - 4 : 4;
+    if (lim < SF_LIMBS) {
+      const cd* o = O + ((size_t)ct * MAC_JT + j * SF_LIMBS + lim) * SF_M;
+      cd x[16];
+#pragma unroll
+      for (int r = 0; r < 16; r++) x[r] = o[snsf::pt4(t, r)];
+      snsf::dit_pass4(x, F.T);
+#pragma unroll
+      for (int r = 0; r < 16; r++) buf[snsf::pad(snsf::pt4(t, r))] = x[r];
+      wave_sync();
+#pragma unroll
+      for (int r = 0; r < 16; r++) x[r] = buf[snsf::pad(snsf::pt23(t, r))];
+      snsf::dit_pass32(x, t, F.T);
+#pragma unroll
+      for (int r = 0; r < 16; r++) buf[snsf::pad(snsf::pt23(t, r))] = x[r];
+      wave_sync();
+#pragma unroll
+      for (int r = 0; r < 16; r++) x[r] = buf[snsf::pad(snsf::pt01(t, r))];
+      snsf::dit_pass10(x, t, F.T);
+      wave_sync();  // all lanes' reads are done before the integer coefficients overwrite the buffer
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int m = snsf::pt01(t, r);
+        const cd y = snsf::cmulc(x[r], F.P[m]);
+        ci[m] = (long long)__builtin_rint(y.x);
+        ci[m + SF_M] = (long long)__builtin_rint(y.y);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      __int128 acc128 = (__int128)reinterpret_cast<const long long*>(bufs[0])[threadIdx.x + 256 * u];
+      for (int q = 1; q < nw; q++)
+        acc128 += (__int128)reinterpret_cast<const long long*>(bufs[q])[threadIdx.x + 256 * u] << (16 * q);
+      ab[round][u] = acc128;
+    }
+    __syncthreads();
+  }
+  u64* a0 = acc + ((size_t)ct * (SK + 1) + j) * 2 * SN;
+  u64* a1 = a0 + SN;
+#pragma unroll
+  for (int u = 0; u < 8; u++) {
+    const int x = threadIdx.x + 256 * u;
+    const __int128 A = ab[0][u] << snsf::SF_DROP, Bv = ab[1][u] << snsf::SF_DROP;  // x 2^16: < 2^118, < 2^102
+    const u64 r0 = addm_q<0>(reduce_s128<0>(A), mont_q<0>(reduce_s128<0>(Bv), prime_r2<0>()));  // + 2^64 B
+    const u64 r1 = addm_q<1>(reduce_s128<1>(A), mont_q<1>(reduce_s128<1>(Bv), prime_r2<1>()));
+    a0[x] = addm_q<0>(a0[x], r0);
+    a1[x] = addm_q<1>(a1[x], r1);
+  }
+}
+
+// the 7 inverse FFTs of (ciphertext, output j), one after another by all 256 threads (stage form, 16 KB
+// LDS); each thread weights the rounded limb values (|c| < 2^53) of its 8 coefficients by 2^(16 + 16 t)
+// mod p into int128 sums per prime (|sum| < 2^120), reduced once: acc_j += (mod p1, p2).  Measured
+// alternatives, all slower: residue sums with a Montgomery product per limb (92 VGPRs, 5 waves/SIMD,
+// rolled stages), exact int128 shift-adds of the limbs (runtime 128-bit shifts, or a per-limb switch
+// of compile-time shifts: 60 spills), spectra stored in the pass-4 register order (gathered loads).
 __global__ void __launch_bounds__(ST) sns_inv_kernel(const cd* __restrict__ O, u64* __restrict__ acc,
                                                      const SnsFftConst* __restrict__ Fc) {
   __shared__ cd buf[SF_M];
@@ -776,6 +877,8 @@ void make_sns_fft_const(void* out) {
   for (int t = 0; t < SF_LIMBS; t++) {
     F.W[0][t] = prime_pow2<0>(snsf::SF_DROP + snsf::SF_LIMB_BITS * t);
     F.W[1][t] = prime_pow2<1>(snsf::SF_DROP + snsf::SF_LIMB_BITS * t);
+    F.WM[0][t] = hmul(F.W[0][t], (u64)0 - Prime<0>::p, Prime<0>::p);  // x (2^64 mod p)
+    F.WM[1][t] = hmul(F.W[1][t], (u64)0 - Prime<1>::p, Prime<1>::p);
   }
 }
 
@@ -799,10 +902,11 @@ hipError_t launch_sns_blind_rotate_fft(const u64* lwe, size_t B, int n, const u6
   const SnsFftConst* F = (const SnsFftConst*)d_fconst;
   sns_init_kernel<<<(unsigned)B, 256, 0, s>>>(lwe, n, lut, acc, K);
   const size_t per_i = (size_t)SR * (SK + 1) * SF_LIMBS * SF_M;
-  static const bool fused2 = [] {
-    const char* e = getenv("TFHE_HIP_SNS_FUSED2");
-    return e && e[0] == '1';
-  }();
+  // measured variants (read per call, so one process can check them all): the one-kernel step 2 and the
+  // one-wave-per-limb inverse
+  const char* e2 = getenv("TFHE_HIP_SNS_FUSED2");
+  const char* ew = getenv("TFHE_HIP_SNS_INVW");
+  const bool fused2 = e2 && e2[0] == '1', invw = ew && ew[0] == '1';
   const unsigned mac_grid = (unsigned)((SF_M / MAC_F) * ((B + MAC_CT - 1) / MAC_CT));
   for (int i = 0; i < n; i++) {
     const cd* kf_i = (const cd*)bsk_fft + per_i * i;
@@ -811,7 +915,10 @@ hipError_t launch_sns_blind_rotate_fft(const u64* lwe, size_t B, int n, const u6
       sns_step2f_kernel<<<(unsigned)(B * (SK + 1)), ST, 0, s>>>((const cd*)D, kf_i, acc, F);
     } else {
       sns_mac_kernel<<<mac_grid, ST, 0, s>>>((const cd*)D, kf_i, (cd*)Oprod, (int)B);
-      sns_inv_kernel<<<(unsigned)(B * (SK + 1)), ST, 0, s>>>((const cd*)Oprod, acc, F);
+      if (invw)
+        sns_inv_wave_kernel<<<(unsigned)(B * (SK + 1)), ST, 0, s>>>((const cd*)Oprod, acc, F);
+      else
+        sns_inv_kernel<<<(unsigned)(B * (SK + 1)), ST, 0, s>>>((const cd*)Oprod, acc, F);
     }
   }
   return hipGetLastError();

@@ -55,7 +55,16 @@ struct DevGuard {
   }
 };
 
-constexpr size_t SNS_CHUNK = 1024;  // ciphertexts per pass (acc 96 KB + digit spectra 288 KB each)
+// ciphertexts per pass (acc 96 KB + digit spectra 147-288 KB + FFT products 344 KB each);
+// TFHE_HIP_SNS_CHUNK overrides (the FFT path's per-CMUX working set is ~0.5 MB per ciphertext)
+size_t sns_chunk() {
+  static const size_t v = [] {
+    const char* e = getenv("TFHE_HIP_SNS_CHUNK");
+    const long x = e ? atol(e) : 0;
+    return x > 0 ? (size_t)x : (size_t)1024;
+  }();
+  return v;
+}
 
 }  // namespace
 
@@ -110,7 +119,7 @@ int ensure_lut(tfhe_sns_ctx* c, uint32_t mm) {
 
 // squash (out != null) or blind rotate only (acc_out != null) of B device ciphertexts
 int run_device(tfhe_sns_ctx* c, const u64* d_in, size_t B, u64* d_out, u64* d_acc_out, hipStream_t s) {
-  const size_t chunk = std::min(B, SNS_CHUNK);
+  const size_t chunk = std::min(B, sns_chunk());
   int rc = ensure_ws(c, chunk);
   if (rc) return rc;
   const size_t in_dim = c->sp.n + 1, out_dim = 2 * ((size_t)c->sp.k * c->sp.N + 1);

@@ -39,33 +39,90 @@ SF_HD cd cmul(cd a, cd b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x
 SF_HD cd cmulc(cd a, cd b) { return {a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y}; }  // a * conj(b)
 SF_HD cd cmac(cd acc, cd a, cd b) { return {acc.x + a.x * b.x - a.y * b.y, acc.y + a.x * b.y + a.y * b.x}; }
 
+// Radix-4 DIF butterfly with output twiddles T[e k] (e = j * 4^s), and its DIT inverse (conjugate
+// input twiddles, then the butterfly with -i): dit(dif(x)) = 4 x.
+SF_HD void r4_dif(cd& x0, cd& x1, cd& x2, cd& x3, int e, const cd* T) {
+  const cd a0 = cadd(x0, x2), a1 = csub(x0, x2), a2 = cadd(x1, x3), d = csub(x1, x3);
+  const cd a3 = {-d.y, d.x};  // i (x1 - x3)
+  x0 = cadd(a0, a2);
+  x1 = cmul(cadd(a1, a3), T[e]);  // T[0] = 1 exactly: e = 0 needs no branch
+  x2 = cmul(csub(a0, a2), T[2 * e]);
+  x3 = cmul(csub(a1, a3), T[3 * e]);
+}
+SF_HD void r4_dif0(cd& x0, cd& x1, cd& x2, cd& x3) {  // e = 0
+  const cd a0 = cadd(x0, x2), a1 = csub(x0, x2), a2 = cadd(x1, x3), d = csub(x1, x3);
+  const cd a3 = {-d.y, d.x};
+  x0 = cadd(a0, a2);
+  x1 = cadd(a1, a3);
+  x2 = csub(a0, a2);
+  x3 = csub(a1, a3);
+}
+SF_HD void r4_dit(cd& y0, cd& y1, cd& y2, cd& y3, int e, const cd* T) {
+  if (e >= 0) {  // e < 0: no twiddles (r4_dit0)
+    y1 = cmulc(y1, T[e]);
+    y2 = cmulc(y2, T[2 * e]);
+    y3 = cmulc(y3, T[3 * e]);
+  }
+  const cd b0 = cadd(y0, y2), b1 = csub(y0, y2), b2 = cadd(y1, y3), d = csub(y1, y3);
+  const cd b3 = {d.y, -d.x};  // -i (y1 - y3)
+  y0 = cadd(b0, b2);
+  y1 = cadd(b1, b3);
+  y2 = csub(b0, b2);
+  y3 = csub(b1, b3);
+}
+
 // One radix-4 DIF butterfly of stage s (span L = M / 4^s) for thread t < 256; T[e] = e^{2 pi i e / M}.
 SF_HD void dif_stage(cd* a, int s, int t, const cd* T) {
   const int lq = 8 - 2 * s;  // log2(L / 4)
   const int q = 1 << lq, j = t & (q - 1), base = ((t >> lq) << (lq + 2)) + j;
-  const cd x0 = a[base], x1 = a[base + q], x2 = a[base + 2 * q], x3 = a[base + 3 * q];
-  const cd a0 = cadd(x0, x2), a1 = csub(x0, x2), a2 = cadd(x1, x3), d = csub(x1, x3);
-  const cd a3 = {-d.y, d.x};  // i (x1 - x3)
-  const int e = j << (2 * s);  // j * M / L
-  a[base] = cadd(a0, a2);
-  a[base + q] = cmul(cadd(a1, a3), T[e]);
-  a[base + 2 * q] = cmul(csub(a0, a2), T[2 * e]);
-  a[base + 3 * q] = cmul(csub(a1, a3), T[3 * e]);
+  r4_dif(a[base], a[base + q], a[base + 2 * q], a[base + 3 * q], j << (2 * s), T);
 }
-
-// The inverse butterfly of stage s: conjugate twiddles first, then the radix-4 DFT with -i.
+// The inverse butterfly of stage s.
 SF_HD void dit_stage(cd* a, int s, int t, const cd* T) {
   const int lq = 8 - 2 * s;
   const int q = 1 << lq, j = t & (q - 1), base = ((t >> lq) << (lq + 2)) + j;
-  const int e = j << (2 * s);
-  const cd y0 = a[base], y1 = cmulc(a[base + q], T[e]), y2 = cmulc(a[base + 2 * q], T[2 * e]),
-           y3 = cmulc(a[base + 3 * q], T[3 * e]);
-  const cd b0 = cadd(y0, y2), b1 = csub(y0, y2), b2 = cadd(y1, y3), d = csub(y1, y3);
-  const cd b3 = {d.y, -d.x};  // -i (y1 - y3)
-  a[base] = cadd(b0, b2);
-  a[base + q] = cadd(b1, b3);
-  a[base + 2 * q] = csub(b0, b2);
-  a[base + 3 * q] = csub(b1, b3);
+  r4_dit(a[base], a[base + q], a[base + 2 * q], a[base + 3 * q], j << (2 * s), T);
+}
+
+// ---- one transform per wave (64 lanes x 16 points): the same 5 stages grouped as passes (0,1),
+// (2,3), (4) in registers, two wave-private LDS exchanges.  Lane t's registers x[4 k1 + k2]:
+//   pass 01: point t + 64 k2 + 256 k1   (stage 0 over k1 at j = t + 64 k2, stage 1 over k2 at j = t)
+//   pass 23: point 64 b + j + 16 k1 + 4 k2, t = 4 b + j   (stage 2 over k1 at j + 4 k2, stage 3 over k2 at j)
+//   pass 4 : point 4 (t + 64 k1) + k2   (stage 4 over k2, no twiddles)
+// The exchange buffer is padded by one complex per 16 (pad(p) = p + p/16, 1088 entries): each of the
+// three access patterns then covers 16 distinct 16-byte slots per 16 lanes (no bank conflicts).
+constexpr int SF_PADDED = SF_M + SF_M / 16;
+SF_HD int pad(int p) { return p + (p >> 4); }
+SF_HD int pt01(int t, int r) { return t + 64 * (r & 3) + 256 * (r >> 2); }
+SF_HD int pt23(int t, int r) { return 64 * (t >> 2) + (t & 3) + 16 * (r >> 2) + 4 * (r & 3); }
+SF_HD int pt4(int t, int r) { return 4 * (t + 64 * (r >> 2)) + (r & 3); }
+// Spectra live in global memory in DIF position order (a one-wave transform stores them through its
+// exchange buffer, contiguously); storing them in the pass-4 register order instead made the 256-thread
+// inverse's loads gathers (measured slower).
+
+SF_HD void dif_pass01(cd (&x)[16], int t, const cd* T) {
+  for (int k2 = 0; k2 < 4; k2++) r4_dif(x[k2], x[4 + k2], x[8 + k2], x[12 + k2], t + 64 * k2, T);
+  for (int k1 = 0; k1 < 4; k1++) r4_dif(x[4 * k1], x[4 * k1 + 1], x[4 * k1 + 2], x[4 * k1 + 3], 4 * t, T);
+}
+SF_HD void dif_pass23(cd (&x)[16], int t, const cd* T) {
+  const int j = t & 3;
+  for (int k2 = 0; k2 < 4; k2++) r4_dif(x[k2], x[4 + k2], x[8 + k2], x[12 + k2], 16 * (j + 4 * k2), T);
+  for (int k1 = 0; k1 < 4; k1++) r4_dif(x[4 * k1], x[4 * k1 + 1], x[4 * k1 + 2], x[4 * k1 + 3], 64 * j, T);
+}
+SF_HD void dif_pass4(cd (&x)[16], const cd* T) {
+  for (int k1 = 0; k1 < 4; k1++) r4_dif0(x[4 * k1], x[4 * k1 + 1], x[4 * k1 + 2], x[4 * k1 + 3]);
+}
+SF_HD void dit_pass4(cd (&x)[16], const cd* T) {
+  for (int k1 = 0; k1 < 4; k1++) r4_dit(x[4 * k1], x[4 * k1 + 1], x[4 * k1 + 2], x[4 * k1 + 3], -1, T);
+}
+SF_HD void dit_pass32(cd (&x)[16], int t, const cd* T) {
+  const int j = t & 3;
+  for (int k1 = 0; k1 < 4; k1++) r4_dit(x[4 * k1], x[4 * k1 + 1], x[4 * k1 + 2], x[4 * k1 + 3], 64 * j, T);
+  for (int k2 = 0; k2 < 4; k2++) r4_dit(x[k2], x[4 + k2], x[8 + k2], x[12 + k2], 16 * (j + 4 * k2), T);
+}
+SF_HD void dit_pass10(cd (&x)[16], int t, const cd* T) {
+  for (int k1 = 0; k1 < 4; k1++) r4_dit(x[4 * k1], x[4 * k1 + 1], x[4 * k1 + 2], x[4 * k1 + 3], 4 * t, T);
+  for (int k2 = 0; k2 < 4; k2++) r4_dit(x[k2], x[4 + k2], x[8 + k2], x[12 + k2], t + 64 * k2, T);
 }
 
 }  // namespace snsf

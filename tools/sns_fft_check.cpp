@@ -26,15 +26,59 @@ static void tables() {
   }
 }
 
+static bool g_wave = false;  // the one-wave pass form instead of the 256-thread stages
+
+// 64 simulated lanes: registers -> padded buffer -> registers between passes
+static void wave_fwd(cd* z) {
+  static cd x[64][16], buf[SF_PADDED];
+  for (int t = 0; t < 64; t++) {
+    for (int r = 0; r < 16; r++) x[t][r] = z[pt01(t, r)];
+    dif_pass01(x[t], t, T);
+    for (int r = 0; r < 16; r++) buf[pad(pt01(t, r))] = x[t][r];
+  }
+  for (int t = 0; t < 64; t++) {
+    for (int r = 0; r < 16; r++) x[t][r] = buf[pad(pt23(t, r))];
+    dif_pass23(x[t], t, T);
+    for (int r = 0; r < 16; r++) buf[pad(pt23(t, r))] = x[t][r];
+  }
+  for (int t = 0; t < 64; t++) {
+    for (int r = 0; r < 16; r++) x[t][r] = buf[pad(pt4(t, r))];
+    dif_pass4(x[t], T);
+    for (int r = 0; r < 16; r++) z[pt4(t, r)] = x[t][r];
+  }
+}
+static void wave_inv(cd* z) {
+  static cd x[64][16], buf[SF_PADDED];
+  for (int t = 0; t < 64; t++) {
+    for (int r = 0; r < 16; r++) x[t][r] = z[pt4(t, r)];
+    dit_pass4(x[t], T);
+    for (int r = 0; r < 16; r++) buf[pad(pt4(t, r))] = x[t][r];
+  }
+  for (int t = 0; t < 64; t++) {
+    for (int r = 0; r < 16; r++) x[t][r] = buf[pad(pt23(t, r))];
+    dit_pass32(x[t], t, T);
+    for (int r = 0; r < 16; r++) buf[pad(pt23(t, r))] = x[t][r];
+  }
+  for (int t = 0; t < 64; t++) {
+    for (int r = 0; r < 16; r++) x[t][r] = buf[pad(pt01(t, r))];
+    dit_pass10(x[t], t, T);
+    for (int r = 0; r < 16; r++) z[pt01(t, r)] = x[t][r];
+  }
+}
+
 static void fwd(const int64_t* a, cd* z) {
   for (int m = 0; m < SF_M; m++) z[m] = cmul(cd{(double)a[m], (double)a[m + SF_M]}, P[m]);
+  if (g_wave) return wave_fwd(z);
   for (int s = 0; s < 5; s++)
     for (int t = 0; t < SF_NT; t++) dif_stage(z, s, t, T);
 }
 
 static void inv(cd* z, double* out) {
-  for (int s = 4; s >= 0; s--)
-    for (int t = 0; t < SF_NT; t++) dit_stage(z, s, t, T);
+  if (g_wave)
+    wave_inv(z);
+  else
+    for (int s = 4; s >= 0; s--)
+      for (int t = 0; t < SF_NT; t++) dit_stage(z, s, t, T);
   for (int m = 0; m < SF_M; m++) {
     const cd y = cmulc(z[m], P[m]);
     out[m] = y.x;
@@ -45,6 +89,23 @@ static void inv(cd* z, double* out) {
 int main(int argc, char** argv) {
   tables();
   const int trials = argc > 1 ? atoi(argv[1]) : 6;
+  g_wave = argc > 2 && argv[2][0] == 'w';
+  {  // the wave form computes the same spectrum positions as the stage form
+    std::mt19937_64 g0(7);
+    std::vector<int64_t> a(SF_N);
+    for (auto& v : a) v = (int64_t)(g0() % (1u << 24)) - (1 << 23);
+    std::vector<cd> z1(SF_M), z2(SF_M);
+    const bool w = g_wave;
+    g_wave = false;
+    fwd(a.data(), z1.data());
+    g_wave = true;
+    fwd(a.data(), z2.data());
+    g_wave = w;
+    double d = 0;
+    for (int f = 0; f < SF_M; f++) d = fmax(d, fmax(fabs(z1[f].x - z2[f].x), fabs(z1[f].y - z2[f].y)));
+    printf("stage form vs wave form spectra: max |diff| = %.3e\n", d);
+    if (d > 1e-3) return 1;
+  }
   std::mt19937_64 g(12345);
   double worst = 0;
   for (int tr = 0; tr < trials; tr++) {
