@@ -597,7 +597,8 @@ __global__ void __launch_bounds__(ST) sns_step2f_kernel(const cd* __restrict__ D
 
 // Step 2 split for key reuse across ciphertexts (default): the MAC as a frequency-tiled kernel whose
 // workgroup holds the CMUX's key for 16 frequencies x all 21 (output, limb) columns in LDS (48 KB)
-// and streams 32 ciphertexts' digit spectra through it, writing the products O[ct][j*7+t][M] to
+// and streams 32 ciphertexts' digit spectra through it (8 frequencies x 64 ciphertexts, 24 KB, 4
+// workgroups per CU: 108 us instead of 96, the 128-byte runs cost more than the occupancy gains), writing the products O[ct][j*7+t][M] to
 // global memory; then one workgroup per (ciphertext, output) runs the 7 inverse FFTs, rint, the limb
 // weights and acc_j += (mod p1, p2).  The one-kernel form (sns_step2f_kernel, TFHE_HIP_SNS_FUSED2=1)
 // re-reads the ~1 MB per-output key slice for every ciphertext.
@@ -614,8 +615,9 @@ __global__ void __launch_bounds__(ST) sns_mac_kernel(const cd* __restrict__ Df, 
     kt[row][f] = kf_i[(size_t)row * SF_M + f0 + f];
   }
   __syncthreads();
-  const int f = threadIdx.x % MAC_F, cl = threadIdx.x / MAC_F;  // 16 frequencies x 16 ciphertext lanes
-  const int ca = c0 + cl, cb = c0 + cl + 16;
+  const int f = threadIdx.x % MAC_F, cl = threadIdx.x / MAC_F;  // MAC_F frequencies x (256 / MAC_F) ciphertext lanes
+  static_assert(MAC_CT == 2 * (ST / MAC_F), "two ciphertexts per thread");
+  const int ca = c0 + cl, cb = c0 + cl + ST / MAC_F;
   const bool va = ca < B, vb = cb < B;
   cd da[SR], db[SR];
 #pragma unroll
@@ -705,36 +707,42 @@ __global__ void __launch_bounds__(ST, 2) sns_inv_wave_kernel(const cd* __restric
 }
 
 // the 7 inverse FFTs of (ciphertext, output j), one after another by all 256 threads (stage form, 16 KB
-// LDS); each thread weights the rounded limb values (|c| < 2^53) of its 8 coefficients by 2^(16 + 16 t)
-// mod p into int128 sums per prime (|sum| < 2^120), reduced once: acc_j += (mod p1, p2).  Measured
-// alternatives, all slower: residue sums with a Montgomery product per limb (92 VGPRs, 5 waves/SIMD,
-// rolled stages), exact int128 shift-adds of the limbs (runtime 128-bit shifts, or a per-limb switch
-// of compile-time shifts: 60 spills), spectra stored in the pass-4 register order (gathered loads).
-__global__ void __launch_bounds__(ST) sns_inv_kernel(const cd* __restrict__ O, u64* __restrict__ acc,
+// LDS), limbs from the top: each thread folds the rounded limb values (|c| < 2^53) of its 8 coefficients
+// into exact int128 Horner sums with a constant shift, B = ((c6 2^16) + c5) 2^16 + c4 (< 2^86), then
+// A = c3 2^48 + ... + c0 (< 2^102), and reduces 2^16 (A + 2^64 B) once per prime: acc_j += (mod p1,
+// p2).  Measured alternatives, all slower: weighting every limb value by 2^(16+16t) mod p into int128
+// sums (two 64 x 64 products per coefficient and limb: 160 us), residue sums with a Montgomery product
+// per limb (206-219 us), runtime-amount int128 shifts (227 us), a per-limb switch of compile-time shifts
+// (60 spills, 387 us), spectra stored in the pass-4 register order (gathered loads, 264 us).
+__global__ void __launch_bounds__(ST, 3) sns_inv_kernel(const cd* __restrict__ O, u64* __restrict__ acc,
                                                      const SnsFftConst* __restrict__ Fc) {
   __shared__ cd buf[SF_M];
   const int j = blockIdx.x % (SK + 1), ct = blockIdx.x / (SK + 1);
   const SnsFftConst& F = *Fc;
-  __int128 s0[8], s1[8];
+  __int128 h[8], Bv[8];
 #pragma unroll
-  for (int e = 0; e < 8; e++) s0[e] = s1[e] = 0;
+  for (int e = 0; e < 8; e++) h[e] = Bv[e] = 0;
+  static_assert(SF_LIMBS == 7, "B = limbs 6..4, A = limbs 3..0");
 #pragma unroll 1
-  for (int t = 0; t < SF_LIMBS; t++) {
+  for (int t = SF_LIMBS - 1; t >= 0; t--) {
+    if (t == 3) {  // uniform: B complete, start A
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        Bv[e] = h[e];
+        h[e] = 0;
+      }
+    }
     const cd* o = O + ((size_t)ct * MAC_JT + j * SF_LIMBS + t) * SF_M;
 #pragma unroll
     for (int u = 0; u < 4; u++) buf[threadIdx.x + 256 * u] = o[threadIdx.x + 256 * u];
     __syncthreads();
     fft_inv_lds(buf, F.T);
-    const __int128 w0 = (__int128)F.W[0][t], w1 = (__int128)F.W[1][t];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const int m = threadIdx.x + 256 * u;
       const cd y = snsf::cmulc(buf[m], F.P[m]);
-      const long long c0 = (long long)__builtin_rint(y.x), c1 = (long long)__builtin_rint(y.y);
-      s0[2 * u] += (__int128)c0 * w0;
-      s1[2 * u] += (__int128)c0 * w1;
-      s0[2 * u + 1] += (__int128)c1 * w0;
-      s1[2 * u + 1] += (__int128)c1 * w1;
+      h[2 * u] = (h[2 * u] << 16) + (__int128)(long long)__builtin_rint(y.x);
+      h[2 * u + 1] = (h[2 * u + 1] << 16) + (__int128)(long long)__builtin_rint(y.y);
     }
     __syncthreads();
   }
@@ -743,10 +751,13 @@ __global__ void __launch_bounds__(ST) sns_inv_kernel(const cd* __restrict__ O, u
 #pragma unroll
   for (int u = 0; u < 4; u++)
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int x = threadIdx.x + 256 * u + SF_M * h;
-      a0[x] = addm_q<0>(a0[x], reduce_s128<0>(s0[2 * u + h]));
-      a1[x] = addm_q<1>(a1[x], reduce_s128<1>(s1[2 * u + h]));
+    for (int hh = 0; hh < 2; hh++) {
+      const int x = threadIdx.x + 256 * u + SF_M * hh;
+      const __int128 a = h[2 * u + hh] << snsf::SF_DROP, b = Bv[2 * u + hh] << snsf::SF_DROP;  // < 2^118, 2^102
+      const u64 r0 = addm_q<0>(reduce_s128<0>(a), mont_q<0>(reduce_s128<0>(b), prime_r2<0>()));  // + 2^64 b
+      const u64 r1 = addm_q<1>(reduce_s128<1>(a), mont_q<1>(reduce_s128<1>(b), prime_r2<1>()));
+      a0[x] = addm_q<0>(a0[x], r0);
+      a1[x] = addm_q<1>(a1[x], r1);
     }
 }
 
