@@ -105,8 +105,10 @@ def test_fft_limb_product_exactness(tmp_path):
     exe = tmp_path / "sns_fft_check"
     subprocess.run(["g++", "-O2", "-std=c++17", "-I", f"{root}/tfhe_amd/csrc", f"{root}/tools/sns_fft_check.cpp",
                     "-o", str(exe)], check=True)
-    out = subprocess.run([str(exe), "6"], capture_output=True, text=True).stdout
-    errs = [(int(l.split()[3].rstrip(":")), float(l.split("=")[1].split(",")[0])) for l in out.splitlines()
-            if l.startswith("trial")]
-    assert len(errs) == 6
-    assert all(e < 0.07 for mode, e in errs if mode != 2)
+    for form in ("s", "w"):  # the 256-thread stage form (inverse, key conversion) and the one-wave form (step 1)
+        out = subprocess.run([str(exe), "6", form], capture_output=True, text=True).stdout
+        assert "stage form vs wave form spectra: max |diff| = 0.000e+00" in out
+        errs = [(int(l.split()[3].rstrip(":")), float(l.split("=")[1].split(",")[0])) for l in out.splitlines()
+                if l.startswith("trial")]
+        assert len(errs) == 6
+        assert all(e < 0.07 for mode, e in errs if mode != 2)
