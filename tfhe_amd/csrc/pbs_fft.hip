@@ -162,7 +162,7 @@ constexpr int CHUNK_GLDS = CHUNK_C64 * 16 / 1024;  // 1 KB wave-instructions per
 #ifndef FFT_STAMPS
 #define FFT_STAMPS 0
 #endif
-constexpr int FS_NPH = 8;  // rotate, level barrier, digits + twist, forward DFT, MAC, inverse 0, inverse 1, top
+[[maybe_unused]] constexpr int FS_NPH = 8;  // rotate, level barrier, digits + twist, forward DFT, MAC, inverse 0, inverse 1, top
 #if FFT_STAMPS
 __device__ unsigned long long fft_stamps[16][FB_WAVES][FS_NPH];
 #define FS_STAMP(k)                                                                              \
