@@ -77,3 +77,32 @@ def test_fft_variants_agree(sns_setup, fhevm_engine, fhevm_keys, monkeypatch, sw
     ref = sq.blind_rotate(small)
     monkeypatch.setenv(switch, "1")
     assert np.array_equal(sq.blind_rotate(small), ref)
+
+
+@pytest.mark.parametrize("slots", ["1", "3"])
+def test_mac_slot_walk_agrees(sns_setup, fhevm_engine, fhevm_keys, monkeypatch, slots):
+    """The MAC grid with fewer ciphertext-group slots than groups (each workgroup stages its key tile
+    once and walks groups g, g + G, ...; 100 ciphertexts = 3 full groups of 32 + a ragged one) gives
+    the one-group-per-workgroup accumulators bit for bit."""
+    sp, osp, key, okey, sq = sns_setup
+    ck, _ = fhevm_keys
+    msgs = (np.arange(100) % 16).astype(np.uint64)
+    small, _ = fhevm_engine.ms_reduce(fhevm_engine.keyswitch(ck.encrypt(msgs, 16, seed=0xC0FFEE75)))
+    monkeypatch.setenv("TFHE_HIP_SNS_MACG", "0")
+    ref = sq.blind_rotate(small)
+    monkeypatch.setenv("TFHE_HIP_SNS_MACG", slots)
+    assert np.array_equal(sq.blind_rotate(small), ref)
+    assert np.array_equal(key.decrypt(sq.squash(small)), msgs)
+
+
+@pytest.mark.parametrize("occ", ["4", "5"])
+def test_inverse_occupancy_variants_agree(sns_setup, fhevm_engine, fhevm_keys, monkeypatch, occ):
+    """The inverse kernel's measured forms (rolled stages at 4 and 5 waves/SIMD) give the default
+    (unrolled stages, 3 waves/SIMD) accumulators bit for bit."""
+    sp, osp, key, okey, sq = sns_setup
+    ck, _ = fhevm_keys
+    msgs = np.array([5, 14, 1], dtype=np.uint64)
+    small, _ = fhevm_engine.ms_reduce(fhevm_engine.keyswitch(ck.encrypt(msgs, 16, seed=0xC0FFEE76)))
+    ref = sq.blind_rotate(small)
+    monkeypatch.setenv("TFHE_HIP_SNS_INVOCC", occ)
+    assert np.array_equal(sq.blind_rotate(small), ref)

@@ -431,11 +431,23 @@ __device__ __forceinline__ void fft_fwd_lds(cd* buf, const cd* __restrict__ T) {
     __syncthreads();
   }
 }
+// ROLLED = false: unrolled, the twiddle loads of later stages are issued early (168 VGPRs, 3 waves per
+// SIMD: 159 us per CMUX launch at B = 1024); rolled, the stage loop fits 4 waves per SIMD without spills
+// but waits on every stage's twiddle loads (199 us; 5 waves spill 48 VGPRs: slower still)
+template <bool ROLLED = false>
 __device__ __forceinline__ void fft_inv_lds(cd* buf, const cd* __restrict__ T) {
-#pragma unroll  // unrolled: the twiddle loads of later stages are issued early (measured faster rolled-up too)
-  for (int s = 4; s >= 0; s--) {
-    snsf::dit_stage(buf, s, threadIdx.x, T);
-    __syncthreads();
+  if (ROLLED) {
+#pragma unroll 1
+    for (int s = 4; s >= 0; s--) {
+      snsf::dit_stage(buf, s, threadIdx.x, T);
+      __syncthreads();
+    }
+  } else {
+#pragma unroll
+    for (int s = 4; s >= 0; s--) {
+      snsf::dit_stage(buf, s, threadIdx.x, T);
+      __syncthreads();
+    }
   }
 }
 
@@ -496,17 +508,47 @@ __device__ __forceinline__ void wave_sync() {
 
 // step 1 (ciphertext, component c): rotation, CRT lift, torus map, 3 digit levels (as the NTT path),
 // then the folded, twisted forward FFT of each digit polynomial -> Df; wave l transforms level l in
-// registers (sns_fft.h passes), its padded exchange buffer aliasing the dead rotation / digit arrays
+// registers (sns_fft.h passes), its padded exchange buffer aliasing the dead digit arrays
+// The rotation is read straight from global memory (coefficient t of X^{a_i} acc is +-acc[(t - a_i) mod
+// 2N]), so the LDS holds only the digits, aliased by the three exchange buffers: 52 KB, 3 workgroups
+// per CU (an LDS copy of the rotated residues, 56 KB, allowed 2).
+__device__ __forceinline__ void step1_digits_g(const u64* __restrict__ lwe, int n, int i, const u64* __restrict__ acc,
+                                               const SnsConst& K, int ct, int c, int (*dig)[SN]) {
+  const u32 ai = mod_switch_4096(lwe[(size_t)ct * (n + 1) + i]);
+  const u64* a = acc + ((size_t)ct * (SK + 1) + c) * 2 * SN;
+  for (int t = threadIdx.x; t < SN; t += ST) {
+    const u32 t1 = ((u32)t - ai) & 4095u;
+    const bool neg = t1 >= (u32)SN;
+    const int src = (int)(t1 & (u32)(SN - 1));
+    const u64 v0 = a[src], v1 = a[SN + src];
+    const u64 x0 = (neg && v0) ? Prime<0>::p - v0 : v0, x1 = (neg && v1) ? Prime<1>::p - v1 : v1;
+    const u64 r1 = subm_q<0>(x0, a[t]);
+    const u64 r2 = subm_q<1>(x1, a[SN + t]);
+    // signed decomposition of the torus image: 72 bits, 3 digits of 24 (tfhe-rs SignedDecomposer)
+    const u128 y = lift_to_torus(r1, r2, K);
+    u128 state = ((y >> 55) + 1) >> 1;
+    state &= ((u128)1 << 72) - 1;
+    for (int l = SL - 1; l >= 0; l--) {
+      const u64 res = (u64)state & 0xFFFFFFull;
+      state >>= 24;
+      const u64 carry = ((((res - 1) | (u64)state) & res) >> 23) & 1;
+      state += carry;
+      dig[l][t] = (int)((long long)res - (long long)(carry << 24));
+    }
+  }
+  __syncthreads();
+}
+
 __global__ void __launch_bounds__(ST) sns_step1f_kernel(const u64* __restrict__ lwe, int n, int i,
                                                         const u64* __restrict__ acc, cd* __restrict__ Df,
                                                         const SnsConst* __restrict__ Kc,
                                                         const SnsFftConst* __restrict__ Fc) {
-  __shared__ u64 rot[2][SN];
-  __shared__ int dig[SL][SN];
-  static_assert(sizeof(rot) + sizeof(dig) >= SL * snsf::SF_PADDED * sizeof(cd), "exchange buffers alias rot + dig");
+  __shared__ cd xbuf[SL * snsf::SF_PADDED];  // the digits, then the waves' exchange buffers
+  int (*dig)[SN] = reinterpret_cast<int (*)[SN]>(&xbuf[0]);
+  static_assert(SL * SN * sizeof(int) <= sizeof(xbuf), "digits fit the exchange buffers");
   const int ct = blockIdx.x / (SK + 1), c = blockIdx.x % (SK + 1);
   const SnsFftConst& F = *Fc;
-  step1_digits(lwe, n, i, acc, *Kc, ct, c, rot, dig);
+  step1_digits_g(lwe, n, i, acc, *Kc, ct, c, dig);
   const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
   cd x[16];
   if (w < SL) {
@@ -517,9 +559,9 @@ __global__ void __launch_bounds__(ST) sns_step1f_kernel(const u64* __restrict__ 
     }
     snsf::dif_pass01(x, t, F.T);
   }
-  __syncthreads();  // every digit read is done before the exchange buffers overwrite rot / dig
+  __syncthreads();  // every digit read is done before the exchange buffers overwrite the digits
   if (w < SL) {
-    cd* buf = reinterpret_cast<cd*>(&rot[0][0]) + w * snsf::SF_PADDED;
+    cd* buf = xbuf + w * snsf::SF_PADDED;
 #pragma unroll
     for (int r = 0; r < 16; r++) buf[snsf::pad(snsf::pt01(t, r))] = x[r];
     wave_sync();
@@ -604,38 +646,55 @@ __global__ void __launch_bounds__(ST) sns_step2f_kernel(const cd* __restrict__ D
 // re-reads the ~1 MB per-output key slice for every ciphertext.
 constexpr int MAC_F = 16, MAC_CT = 32, MAC_JT = (SK + 1) * SF_LIMBS;  // 21 (output, limb) columns
 
-__global__ void __launch_bounds__(ST) sns_mac_kernel(const cd* __restrict__ Df, const cd* __restrict__ kf_i,
-                                                     cd* __restrict__ O, int B) {
-  __shared__ cd kt[SR * MAC_JT][MAC_F];  // [r * 21 + jt][f]
-  const int f0 = (blockIdx.x % (SF_M / MAC_F)) * MAC_F;
-  const int c0 = (blockIdx.x / (SF_M / MAC_F)) * MAC_CT;
-  // key tile: row (r, jt) of the CMUX's key = kf_i[(r * 21 + jt) * M + f0 .. + 16]
-  for (int x = threadIdx.x; x < SR * MAC_JT * MAC_F; x += ST) {
-    const int row = x / MAC_F, f = x % MAC_F;
-    kt[row][f] = kf_i[(size_t)row * SF_M + f0 + f];
-  }
-  __syncthreads();
-  const int f = threadIdx.x % MAC_F, cl = threadIdx.x / MAC_F;  // MAC_F frequencies x (256 / MAC_F) ciphertext lanes
-  static_assert(MAC_CT == 2 * (ST / MAC_F), "two ciphertexts per thread");
+// Grid: (M / 16) frequency tiles x G ciphertext-group slots; slot g walks the groups g, g + G, ...
+// (G = all groups: one group per workgroup), so a slot stages its key tile once for all its groups.
+// The first group's digit spectra are requested before the key tile is staged, so those loads overlap
+// the LDS fill (a register prefetch of the next group as well costs 100 spilled VGPRs at 3 waves/SIMD);
+// the arithmetic per output is the same in every form.
+__device__ __forceinline__ void mac_load(const cd* __restrict__ Df, int c0, int B, int f0, int f, int cl,
+                                         cd (&da)[SR], cd (&db)[SR]) {
   const int ca = c0 + cl, cb = c0 + cl + ST / MAC_F;
-  const bool va = ca < B, vb = cb < B;
-  cd da[SR], db[SR];
 #pragma unroll
   for (int r = 0; r < SR; r++) {
-    da[r] = va ? Df[((size_t)ca * SR + r) * SF_M + f0 + f] : cd{0.0, 0.0};
-    db[r] = vb ? Df[((size_t)cb * SR + r) * SF_M + f0 + f] : cd{0.0, 0.0};
+    da[r] = ca < B ? Df[((size_t)ca * SR + r) * SF_M + f0 + f] : cd{0.0, 0.0};
+    db[r] = cb < B ? Df[((size_t)cb * SR + r) * SF_M + f0 + f] : cd{0.0, 0.0};
   }
+}
+
+__global__ void __launch_bounds__(ST, 3) sns_mac_kernel(const cd* __restrict__ Df, const cd* __restrict__ kf_i,
+                                                     cd* __restrict__ O, int B) {
+  __shared__ cd kt[SR * MAC_JT][MAC_F];  // [r * 21 + jt][f]
+  constexpr int FT = SF_M / MAC_F;
+  const int f0 = (blockIdx.x % FT) * MAC_F;
+  const int slots = gridDim.x / FT, groups = (B + MAC_CT - 1) / MAC_CT;
+  const int f = threadIdx.x % MAC_F, cl = threadIdx.x / MAC_F;  // MAC_F frequencies x (256 / MAC_F) ciphertext lanes
+  static_assert(MAC_CT == 2 * (ST / MAC_F), "two ciphertexts per thread");
+  int g = blockIdx.x / FT;
+  cd da[SR], db[SR];
+  mac_load(Df, g * MAC_CT, B, f0, f, cl, da, db);
+  // key tile: row (r, jt) of the CMUX's key = kf_i[(r * 21 + jt) * M + f0 .. + 16]
+  for (int x = threadIdx.x; x < SR * MAC_JT * MAC_F; x += ST) {
+    const int row = x / MAC_F, fx = x % MAC_F;
+    kt[row][fx] = kf_i[(size_t)row * SF_M + f0 + fx];
+  }
+  __syncthreads();
 #pragma unroll 1
-  for (int jt = 0; jt < MAC_JT; jt++) {
-    cd oa = {0.0, 0.0}, ob = {0.0, 0.0};
+  for (; g < groups; g += slots) {
+    const int ca = g * MAC_CT + cl, cb = ca + ST / MAC_F;
+    const bool va = ca < B, vb = cb < B;
+    if (g != (int)(blockIdx.x / FT)) mac_load(Df, g * MAC_CT, B, f0, f, cl, da, db);  // later groups
+#pragma unroll 1
+    for (int jt = 0; jt < MAC_JT; jt++) {
+      cd oa = {0.0, 0.0}, ob = {0.0, 0.0};
 #pragma unroll
-    for (int r = 0; r < SR; r++) {
-      const cd k = kt[r * MAC_JT + jt][f];
-      oa = snsf::cmac(oa, da[r], k);
-      ob = snsf::cmac(ob, db[r], k);
+      for (int r = 0; r < SR; r++) {
+        const cd k = kt[r * MAC_JT + jt][f];
+        oa = snsf::cmac(oa, da[r], k);
+        ob = snsf::cmac(ob, db[r], k);
+      }
+      if (va) O[((size_t)ca * MAC_JT + jt) * SF_M + f0 + f] = oa;
+      if (vb) O[((size_t)cb * MAC_JT + jt) * SF_M + f0 + f] = ob;
     }
-    if (va) O[((size_t)ca * MAC_JT + jt) * SF_M + f0 + f] = oa;
-    if (vb) O[((size_t)cb * MAC_JT + jt) * SF_M + f0 + f] = ob;
   }
 }
 
@@ -714,8 +773,9 @@ __global__ void __launch_bounds__(ST, 2) sns_inv_wave_kernel(const cd* __restric
 // sums (two 64 x 64 products per coefficient and limb: 160 us), residue sums with a Montgomery product
 // per limb (206-219 us), runtime-amount int128 shifts (227 us), a per-limb switch of compile-time shifts
 // (60 spills, 387 us), spectra stored in the pass-4 register order (gathered loads, 264 us).
-__global__ void __launch_bounds__(ST, 3) sns_inv_kernel(const cd* __restrict__ O, u64* __restrict__ acc,
-                                                     const SnsFftConst* __restrict__ Fc) {
+template <int OCC>  // waves per SIMD: 3 = unrolled stages (168 VGPRs, default), 4 / 5 = rolled stages
+__global__ void __launch_bounds__(ST, OCC) sns_inv_kernel(const cd* __restrict__ O, u64* __restrict__ acc,
+                                                          const SnsFftConst* __restrict__ Fc) {
   __shared__ cd buf[SF_M];
   const int j = blockIdx.x % (SK + 1), ct = blockIdx.x / (SK + 1);
   const SnsFftConst& F = *Fc;
@@ -736,7 +796,7 @@ __global__ void __launch_bounds__(ST, 3) sns_inv_kernel(const cd* __restrict__ O
 #pragma unroll
     for (int u = 0; u < 4; u++) buf[threadIdx.x + 256 * u] = o[threadIdx.x + 256 * u];
     __syncthreads();
-    fft_inv_lds(buf, F.T);
+    fft_inv_lds<(OCC > 3)>(buf, F.T);
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const int m = threadIdx.x + 256 * u;
@@ -918,7 +978,12 @@ hipError_t launch_sns_blind_rotate_fft(const u64* lwe, size_t B, int n, const u6
   const char* e2 = getenv("TFHE_HIP_SNS_FUSED2");
   const char* ew = getenv("TFHE_HIP_SNS_INVW");
   const bool fused2 = e2 && e2[0] == '1', invw = ew && ew[0] == '1';
-  const unsigned mac_grid = (unsigned)((SF_M / MAC_F) * ((B + MAC_CT - 1) / MAC_CT));
+  const char* eo = getenv("TFHE_HIP_SNS_INVOCC");  // waves per SIMD of sns_inv_kernel (3 default, 4, 5)
+  const int inv_occ = eo ? atoi(eo) : 3;
+  // TFHE_HIP_SNS_MACG = ciphertext-group slots of the MAC grid (default 8; 0: one group per workgroup)
+  const char* eg = getenv("TFHE_HIP_SNS_MACG");
+  const size_t groups = (B + MAC_CT - 1) / MAC_CT, mg = eg ? (size_t)atoi(eg) : 8;
+  const unsigned mac_grid = (unsigned)((SF_M / MAC_F) * (mg > 0 && mg < groups ? mg : groups));
   for (int i = 0; i < n; i++) {
     const cd* kf_i = (const cd*)bsk_fft + per_i * i;
     sns_step1f_kernel<<<(unsigned)(B * (SK + 1)), ST, 0, s>>>(lwe, n, i, acc, (cd*)D, K, F);
@@ -926,10 +991,15 @@ hipError_t launch_sns_blind_rotate_fft(const u64* lwe, size_t B, int n, const u6
       sns_step2f_kernel<<<(unsigned)(B * (SK + 1)), ST, 0, s>>>((const cd*)D, kf_i, acc, F);
     } else {
       sns_mac_kernel<<<mac_grid, ST, 0, s>>>((const cd*)D, kf_i, (cd*)Oprod, (int)B);
+      const unsigned ig = (unsigned)(B * (SK + 1));
       if (invw)
-        sns_inv_wave_kernel<<<(unsigned)(B * (SK + 1)), ST, 0, s>>>((const cd*)Oprod, acc, F);
+        sns_inv_wave_kernel<<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
+      else if (inv_occ == 4)
+        sns_inv_kernel<4><<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
+      else if (inv_occ == 5)
+        sns_inv_kernel<5><<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
       else
-        sns_inv_kernel<<<(unsigned)(B * (SK + 1)), ST, 0, s>>>((const cd*)Oprod, acc, F);
+        sns_inv_kernel<3><<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
     }
   }
   return hipGetLastError();
