@@ -773,12 +773,42 @@ __global__ void __launch_bounds__(ST, 2) sns_inv_wave_kernel(const cd* __restric
 // sums (two 64 x 64 products per coefficient and limb: 160 us), residue sums with a Montgomery product
 // per limb (206-219 us), runtime-amount int128 shifts (227 us), a per-limb switch of compile-time shifts
 // (60 spills, 387 us), spectra stored in the pass-4 register order (gathered loads, 264 us).
-template <int OCC>  // waves per SIMD: 3 = unrolled stages (168 VGPRs, default), 4 / 5 = rolled stages
+// Inverse twiddles from LDS (TWL): a per-stage table, stage s at TL_OFF[s], rows k = 1..3 of q_s = 4^(4-s)
+// entries, tl[off + (k-1) q + j] = T[k (j << 2s)] (the values the global-table form reads: same products)
+constexpr int TL_LEN = 3 * (256 + 64 + 16 + 4 + 1);  // 1023
+__device__ __forceinline__ int tl_off(int s) { return s == 0 ? 0 : s == 1 ? 768 : s == 2 ? 960 : s == 3 ? 1008 : 1020; }
+__device__ __forceinline__ void fill_tl(cd* tl, const cd* __restrict__ T) {
+  for (int x = threadIdx.x; x < TL_LEN; x += ST) {
+    const int s = x < 768 ? 0 : x < 960 ? 1 : x < 1008 ? 2 : x < 1020 ? 3 : 4;
+    const int q = 1 << (8 - 2 * s), r = x - tl_off(s), k = r / q + 1, jj = r % q;
+    tl[x] = T[k * (jj << (2 * s))];
+  }
+}
+__device__ __forceinline__ void fft_inv_lds_tl(cd* a, const cd* tl) {
+#pragma unroll
+  for (int s = 4; s >= 0; s--) {
+    const int lq = 8 - 2 * s, q = 1 << lq, t = threadIdx.x;
+    const int jj = t & (q - 1), base = ((t >> lq) << (lq + 2)) + jj;
+    const cd* w = tl + tl_off(s) + jj;
+    cd y0 = a[base], y1 = snsf::cmulc(a[base + q], w[0]), y2 = snsf::cmulc(a[base + 2 * q], w[q]),
+       y3 = snsf::cmulc(a[base + 3 * q], w[2 * q]);
+    snsf::r4_dit(y0, y1, y2, y3, -1, tl);
+    a[base] = y0;
+    a[base + q] = y1;
+    a[base + 2 * q] = y2;
+    a[base + 3 * q] = y3;
+    __syncthreads();
+  }
+}
+
+template <int OCC, bool TWL>  // waves per SIMD: 3 = unrolled stages (168 VGPRs, default), 4 / 5 = rolled stages
 __global__ void __launch_bounds__(ST, OCC) sns_inv_kernel(const cd* __restrict__ O, u64* __restrict__ acc,
                                                           const SnsFftConst* __restrict__ Fc) {
   __shared__ cd buf[SF_M];
+  __shared__ cd tl[TWL ? TL_LEN : 1];
   const int j = blockIdx.x % (SK + 1), ct = blockIdx.x / (SK + 1);
   const SnsFftConst& F = *Fc;
+  if (TWL) fill_tl(tl, F.T);  // ordered before its first use by the limb loop's first barrier
   __int128 h[8], Bv[8];
 #pragma unroll
   for (int e = 0; e < 8; e++) h[e] = Bv[e] = 0;
@@ -796,7 +826,10 @@ __global__ void __launch_bounds__(ST, OCC) sns_inv_kernel(const cd* __restrict__
 #pragma unroll
     for (int u = 0; u < 4; u++) buf[threadIdx.x + 256 * u] = o[threadIdx.x + 256 * u];
     __syncthreads();
-    fft_inv_lds<(OCC > 3)>(buf, F.T);
+    if (TWL)
+      fft_inv_lds_tl(buf, tl);
+    else
+      fft_inv_lds<(OCC > 3)>(buf, F.T);
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const int m = threadIdx.x + 256 * u;
@@ -978,7 +1011,8 @@ hipError_t launch_sns_blind_rotate_fft(const u64* lwe, size_t B, int n, const u6
   const char* e2 = getenv("TFHE_HIP_SNS_FUSED2");
   const char* ew = getenv("TFHE_HIP_SNS_INVW");
   const bool fused2 = e2 && e2[0] == '1', invw = ew && ew[0] == '1';
-  const char* eo = getenv("TFHE_HIP_SNS_INVOCC");  // waves per SIMD of sns_inv_kernel (3 default, 4, 5)
+  // waves per SIMD of sns_inv_kernel (3 default, 4, 5); 13 / 14: 3 / 4 with the LDS twiddle table
+  const char* eo = getenv("TFHE_HIP_SNS_INVOCC");
   const int inv_occ = eo ? atoi(eo) : 3;
   // TFHE_HIP_SNS_MACG = ciphertext-group slots of the MAC grid (default 8; 0: one group per workgroup)
   const char* eg = getenv("TFHE_HIP_SNS_MACG");
@@ -995,11 +1029,15 @@ hipError_t launch_sns_blind_rotate_fft(const u64* lwe, size_t B, int n, const u6
       if (invw)
         sns_inv_wave_kernel<<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
       else if (inv_occ == 4)
-        sns_inv_kernel<4><<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
+        sns_inv_kernel<4, false><<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
       else if (inv_occ == 5)
-        sns_inv_kernel<5><<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
+        sns_inv_kernel<5, false><<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
+      else if (inv_occ == 13)
+        sns_inv_kernel<3, true><<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
+      else if (inv_occ == 14)
+        sns_inv_kernel<4, true><<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
       else
-        sns_inv_kernel<3><<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
+        sns_inv_kernel<3, false><<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
     }
   }
   return hipGetLastError();
