@@ -95,10 +95,11 @@ def test_mac_slot_walk_agrees(sns_setup, fhevm_engine, fhevm_keys, monkeypatch, 
     assert np.array_equal(key.decrypt(sq.squash(small)), msgs)
 
 
-@pytest.mark.parametrize("occ", ["4", "5", "13", "14"])
+@pytest.mark.parametrize("occ", ["3", "4", "5", "13", "14"])
 def test_inverse_occupancy_variants_agree(sns_setup, fhevm_engine, fhevm_keys, monkeypatch, occ):
-    """The inverse kernel's measured forms (rolled stages at 4 and 5 waves/SIMD; twiddles from an LDS
-    table at 3 and 4 waves/SIMD) give the default accumulators bit for bit."""
+    """The inverse kernel's measured forms (all five stages through LDS, unrolled at 3 waves/SIMD or
+    rolled at 4 and 5; twiddles from an LDS table at 3 and 4) give the default (register-ended stages)
+    accumulators bit for bit."""
     sp, osp, key, okey, sq = sns_setup
     ck, _ = fhevm_keys
     msgs = np.array([5, 14, 1], dtype=np.uint64)

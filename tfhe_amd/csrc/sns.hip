@@ -801,7 +801,32 @@ __device__ __forceinline__ void fft_inv_lds_tl(cd* a, const cd* tl) {
   }
 }
 
-template <int OCC, bool TWL>  // waves per SIMD: 3 = unrolled stages (168 VGPRs, default), 4 / 5 = rolled stages
+// The register-ended inverse (REG, default): stage 4's butterflies (q = 1, unit twiddles) each take 4
+// consecutive points, so thread t loads points 4t..4t+3 straight from global memory and transforms them
+// before the first LDS write; stage 0's butterfly of thread t yields points t + 256 k, exactly the
+// coefficients the thread untwists and rounds, so they stay in registers.  Same butterflies, same
+// values; two LDS passes and two barriers fewer per limb (store + 5 stages + read -> 4 stages).
+__device__ __forceinline__ void fft_inv_reg(const cd* __restrict__ o, cd* buf, const cd* __restrict__ T, cd (&y)[4]) {
+  const int t = threadIdx.x;
+  y[0] = o[4 * t];
+  y[1] = o[4 * t + 1];
+  y[2] = o[4 * t + 2];
+  y[3] = o[4 * t + 3];
+  snsf::r4_dit(y[0], y[1], y[2], y[3], 0, T);  // dit_stage(s = 4): base 4t, e = 0
+#pragma unroll
+  for (int k = 0; k < 4; k++) buf[4 * t + k] = y[k];
+  __syncthreads();
+#pragma unroll
+  for (int s = 3; s >= 1; s--) {
+    snsf::dit_stage(buf, s, t, T);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) y[k] = buf[t + 256 * k];
+  snsf::r4_dit(y[0], y[1], y[2], y[3], t, T);  // dit_stage(s = 0): base t, q 256, e = t
+}
+
+template <int OCC, bool TWL, bool REG = false>  // waves per SIMD: 3 = unrolled stages (168 VGPRs), 4 / 5 = rolled
 __global__ void __launch_bounds__(ST, OCC) sns_inv_kernel(const cd* __restrict__ O, u64* __restrict__ acc,
                                                           const SnsFftConst* __restrict__ Fc) {
   __shared__ cd buf[SF_M];
@@ -823,17 +848,24 @@ __global__ void __launch_bounds__(ST, OCC) sns_inv_kernel(const cd* __restrict__
       }
     }
     const cd* o = O + ((size_t)ct * MAC_JT + j * SF_LIMBS + t) * SF_M;
+    cd yr[4];
+    if (REG) {
+      fft_inv_reg(o, buf, F.T, yr);
+    } else {
 #pragma unroll
-    for (int u = 0; u < 4; u++) buf[threadIdx.x + 256 * u] = o[threadIdx.x + 256 * u];
-    __syncthreads();
-    if (TWL)
-      fft_inv_lds_tl(buf, tl);
-    else
-      fft_inv_lds<(OCC > 3)>(buf, F.T);
+      for (int u = 0; u < 4; u++) buf[threadIdx.x + 256 * u] = o[threadIdx.x + 256 * u];
+      __syncthreads();
+      if (TWL)
+        fft_inv_lds_tl(buf, tl);
+      else
+        fft_inv_lds<(OCC > 3)>(buf, F.T);
+#pragma unroll
+      for (int u = 0; u < 4; u++) yr[u] = buf[threadIdx.x + 256 * u];
+    }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const int m = threadIdx.x + 256 * u;
-      const cd y = snsf::cmulc(buf[m], F.P[m]);
+      const cd y = snsf::cmulc(yr[u], F.P[m]);
       h[2 * u] = (h[2 * u] << 16) + (__int128)(long long)__builtin_rint(y.x);
       h[2 * u + 1] = (h[2 * u + 1] << 16) + (__int128)(long long)__builtin_rint(y.y);
     }
@@ -1011,9 +1043,10 @@ hipError_t launch_sns_blind_rotate_fft(const u64* lwe, size_t B, int n, const u6
   const char* e2 = getenv("TFHE_HIP_SNS_FUSED2");
   const char* ew = getenv("TFHE_HIP_SNS_INVW");
   const bool fused2 = e2 && e2[0] == '1', invw = ew && ew[0] == '1';
-  // waves per SIMD of sns_inv_kernel (3 default, 4, 5); 13 / 14: 3 / 4 with the LDS twiddle table
+  // sns_inv_kernel form: 0 (default) register-ended stages at 3 waves/SIMD; 3 / 4 / 5: all five stages
+  // through LDS at that many waves/SIMD; 13 / 14: 3 / 4 with the LDS twiddle table
   const char* eo = getenv("TFHE_HIP_SNS_INVOCC");
-  const int inv_occ = eo ? atoi(eo) : 3;
+  const int inv_occ = eo ? atoi(eo) : 0;
   // TFHE_HIP_SNS_MACG = ciphertext-group slots of the MAC grid (default 8; 0: one group per workgroup)
   const char* eg = getenv("TFHE_HIP_SNS_MACG");
   const size_t groups = (B + MAC_CT - 1) / MAC_CT, mg = eg ? (size_t)atoi(eg) : 8;
@@ -1028,6 +1061,8 @@ hipError_t launch_sns_blind_rotate_fft(const u64* lwe, size_t B, int n, const u6
       const unsigned ig = (unsigned)(B * (SK + 1));
       if (invw)
         sns_inv_wave_kernel<<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
+      else if (inv_occ == 0)
+        sns_inv_kernel<3, false, true><<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
       else if (inv_occ == 4)
         sns_inv_kernel<4, false><<<ig, ST, 0, s>>>((const cd*)Oprod, acc, F);
       else if (inv_occ == 5)
