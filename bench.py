@@ -20,10 +20,10 @@ rank; C4 = 65,536 -> 8,192 per GPU at N = 8); value = G x steps / max-over-ranks
 
 The roofline figure is for the dominant kernel (blind rotation + fused sample extract), timed by HIP
 events recorded by libtfhe_hip.so on the launch stream around every launch in the timed region.  Its
-bound is VALU issue (see roofline()): achieved = SQ_INSTS_VALU per launch from the counter profile of
-THIS build (profiles/*_roofline.json with a matching tfhe_amd.source_id()) over the live kernel time;
-without one, the FFT64 kernels report algorithmic f64 FLOP/s against the 78.6 TFLOP/s FP64 peak.  The
-SURVEY §8d key-streaming byte model (61,952,960 B per PBS at r = 1) is reported as a labelled model only.
+bound is the f64 VALU (see roofline()): frac = algorithmic f64 FLOP per PBS x batch / live kernel time /
+78.6 TFLOP/s.  The VALU issue rate and the HBM traffic (and its ratio to the BSK + ciphertext floor) come
+from the counter profile of THIS build (profiles/*_roofline.json with a matching tfhe_amd.source_id()).
+The SURVEY §8d key-streaming byte model (61,952,960 B per PBS at r = 1) is reported as a labelled model only.
 
 --preset fhevm runs the same protocol on the production fhEVM parameter set (P-FHEVM: n=918, k=1,
 N=2048, PBS 2^23 x 1, KS 2^4 x 4, KS -> PBS; shortint messages m < 16, identity LUT) as a secondary
@@ -94,46 +94,52 @@ def profile_for(kernel: str, B: int):
     return None
 
 
-def roofline(preset: str, kernel: str, B: int, kernel_ms: float, br_bytes: int) -> dict:
-    """The dominant kernel's roofline.  The blind rotation is bound by VALU issue, not HBM: each BSK chunk
-    is streamed once per workgroup into LDS and shared by its ciphertexts (and by resident workgroups
-    through L2), so the measured HBM traffic is ~1 GB per 4096-PBS launch, not the 254 GB a key-streaming
-    model (r = 1) would charge.  Primary figure: VALU issue = SQ_INSTS_VALU per launch (same-build counter
-    profile) x 4 cycles over 1024 SIMDs x 2.4 GHz x the live kernel time.  Without a same-build profile
-    the FFT64 kernels fall back to the f64 FLOP figure (algorithmic FLOP / live kernel time vs the
-    78.6 TFLOP/s FP64 vector peak); `traffic` is then null."""
+def roofline(preset: str, kernel: str, B: int, kernel_ms: float, br_bytes: int, floor_bytes: int) -> dict:
+    """The dominant kernel's roofline: ALGORITHMIC f64 work against the FP64 vector peak.
+
+    The blind rotation is bound by the f64 VALU, not by HBM: each BSK chunk is streamed once per workgroup into
+    LDS and shared by its ciphertexts (and by resident workgroups through L2), so the measured HBM traffic is ~1 GB
+    per 4096-PBS launch, not the 254 GB a key-streaming model (r = 1) would charge.  So
+      frac = FLOP_PER_PBS x B / live kernel time / 78.6 TFLOP/s
+    with FLOP_PER_PBS counted from the transforms' and MAC's operation sequence (fma = 2 FLOP) -- useful work only,
+    independent of how many integer / move / conversion instructions the kernel spends around it.
+    Reported beside it (same-build counter profile, profiles/*_roofline.json with this tree's source_id):
+      valu_issue          SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x 2.4 GHz x kernel time) -- an issue rate, not work
+      traffic             HBM bytes per launch (FETCH_SIZE + WRITE_SIZE passes, gfx950-corrected)
+      traffic_over_floor  traffic / (BSK + B x ciphertext bytes in and out): re-reads of the key per XCD and round
+    Without a same-build profile those three are null."""
     prof = profile_for(kernel, B)
     s = kernel_ms * 1e-3
-    out = {"kernel": kernel + " (+fused sample extract)", "kernel_ms": round(kernel_ms, 3)}
     flops = FLOP_PER_PBS.get(preset)
-    f64 = None
+    out = {"kernel": kernel + " (+fused sample extract)", "kernel_ms": round(kernel_ms, 3)}
     if flops:
         tf = B * flops / s / 1e12
-        f64 = {"flop_per_pbs": flops, "achieved": round(tf, 2), "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s",
-               "frac": round(tf / F64_PEAK_TFLOPS, 4),
-               "model": "algorithmic f64 FLOP of the transforms + MAC (bench.py FLOP_PER_PBS), fma = 2"}
-    traffic = None
-    if prof and prof.get("hbm_bytes"):
-        traffic = int(prof["hbm_bytes"])
-    if prof and prof.get("SQ_INSTS_VALU"):
-        ginst = prof["SQ_INSTS_VALU"] / s / 1e9
-        out.update({"bound": "valu", "achieved": round(ginst, 1), "peak": VALU_PEAK_GINST,
-                    "unit": "G wave64-VALU-instr/s", "frac": round(ginst / VALU_PEAK_GINST, 4),
-                    "valu_insts_per_launch": int(prof["SQ_INSTS_VALU"])})
-    elif f64:
-        out.update({"bound": "valu", "achieved": f64["achieved"], "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": f64["frac"]})
-    else:
+        out.update({"bound": "valu", "achieved": round(tf, 2), "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(tf / F64_PEAK_TFLOPS, 4), "flop_per_pbs": flops,
+                    "model": "algorithmic f64 FLOP of the transforms + MAC per PBS (bench.py FLOP_PER_PBS, fma = 2) "
+                             "x batch / live kernel time; peak = FP64 vector 256 CUs x 4 SIMDs x 16 lanes x 2 x 2.4 GHz"})
+    else:  # the Goldilocks NTT engine: integer work, the VALU-issue figure is its roofline
         out.update({"bound": "valu", "achieved": None, "peak": VALU_PEAK_GINST, "unit": "G wave64-VALU-instr/s",
                     "frac": None})
+    traffic = int(prof["hbm_bytes"]) if prof and prof.get("hbm_bytes") else None
     out["traffic"] = traffic
+    out["traffic_floor_bytes"] = floor_bytes
+    out["traffic_over_floor"] = round(traffic / floor_bytes, 2) if traffic else None
+    if prof and prof.get("SQ_INSTS_VALU"):
+        ginst = prof["SQ_INSTS_VALU"] / s / 1e9
+        out["valu_issue"] = round(ginst / VALU_PEAK_GINST, 4)
+        out["valu_insts_per_launch"] = int(prof["SQ_INSTS_VALU"])
+        if not flops:
+            out.update({"achieved": round(ginst, 1), "frac": out["valu_issue"]})
+    else:
+        out["valu_issue"] = None
     if traffic:
         gbs = traffic / s / 1e9
         out["hbm"] = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                       "traffic_per_pbs": round(traffic / B)}
-    out["f64"] = f64
     out["counters"] = ({"source": prof["source"], "source_id": prof["source_id"],
-                        **{k: prof[k] for k in ("avg_ms", "SQ_WAIT_ANY_per_wave_cycle", "SQ_WAIT_INST_LDS_per_wave_cycle")
+                        **{k: prof[k] for k in ("avg_ms", "SQ_WAIT_ANY_per_wave_cycle", "SQ_WAIT_INST_LDS_per_wave_cycle",
+                                                "f64_share")
                            if k in prof}} if prof else
                        {"source": None, "note": f"no profiles/*_roofline.json for source_id {tfhe_amd.source_id()}"})
     # SURVEY 8(d)'s key-streaming model (r = 1: every PBS charged the whole BSK) -- a model, not a measurement
@@ -365,7 +371,9 @@ def main() -> int:
                 "params": params.as_dict(),
                 "parallelism": f"batch-sharded x{world}, BSK/KSK RCCL broadcast once",
             },
-            "roofline": dict(roofline(args.preset, br_kernel, B, br_avg, br_bytes),
+            # the blind rotation's own floor: the BSK once + small LWEs in + extracted big LWEs out
+            "roofline": dict(roofline(args.preset, br_kernel, B, br_avg, br_bytes,
+                                      bsk_bytes + B * 8 * ((pd["n"] + 1) + (pd["k"] * pd["N"] + 1))),
                              # the reuse the kernel implements and the true minimum traffic
                              bsk_reuse=(f"each BSK level-step chunk is streamed once per workgroup into LDS and shared "
                                         f"by its {8 if not (fhevm and fft) else 4} ciphertexts; resident workgroups "

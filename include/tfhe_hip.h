@@ -140,6 +140,14 @@ int tfhe_hip_ndev(const tfhe_ctx* ctx);            /* number of shards */
 int tfhe_hip_device_at(const tfhe_ctx* ctx, int i); /* device of shard i, -1 if out of range */
 /* How the last key load reached shards 1..ndev-1: 0 = single shard, 1 = device copies, 2 = RCCL. */
 int tfhe_hip_key_bcast_mode(const tfhe_ctx* ctx);
+/* The key-load broadcast planner behind tfhe_hip_load_keys (host logic only, no device is touched), so the
+ * N-rank call structure is testable without N GPUs.  policy: "rccl", "copy" or NULL / "" = auto (RCCL when
+ * the ordinals are distinct and librccl is available, device / peer copies otherwise).  *mode as
+ * tfhe_hip_key_bcast_mode.  mode 2: calls[i] = the rank issuing the i-th ncclBroadcast inside one
+ * ncclGroupStart / ncclGroupEnd (root 0 first); mode 1: calls[i] = destination shard of the i-th copy from
+ * shard 0.  Returns the number of calls (<= max_calls) or a negative error code. */
+int tfhe_hip_bcast_plan(const int* devices, int ndev, const char* policy, int rccl_available, int* mode, int* calls,
+                        int max_calls);
 
 /* Upload standard-domain BSK and KSK from host memory through a pinned staging ring to shard 0,
  * broadcast them to every other shard, and convert them on each device (BSK to the transform domain,
@@ -239,6 +247,10 @@ size_t tfhe_hip_pksk_len(const tfhe_pks_params* pp); /* in_dim * level * (out_k+
 /* output GLWE key (out_k*out_N bits, ChaCha stream 4) and PKSK [j][l][(k+1)N] (stream 0x300000+j) */
 int tfhe_hip_pks_keygen(const tfhe_pks_params* pp, uint64_t seed, const uint64_t* in_key, uint64_t* out_key,
                         uint64_t* pksk /* nullable */);
+/* the same from a 192-bit rng key (tfhe_hip_rng_key_entropy for production keys; the seeded form above
+ * is tfhe_hip_rng_key_from_seed(seed) and exists for reproducible tests) */
+int tfhe_hip_pks_keygen_k(const tfhe_pks_params* pp, const tfhe_rng_key* rk, const uint64_t* in_key,
+                          uint64_t* out_key, uint64_t* pksk /* nullable */);
 typedef struct tfhe_pks_ctx tfhe_pks_ctx;
 int tfhe_hip_pks_create(const tfhe_pks_params* pp, int device, tfhe_pks_ctx** out);
 void tfhe_hip_pks_destroy(tfhe_pks_ctx* ctx);
@@ -270,6 +282,9 @@ size_t tfhe_hip_sns_bsk_len(const tfhe_sns_params* sp); /* n*(k+1)L*(k+1)*2*N: [
 /* 128-bit GLWE key (k*N bits, ChaCha stream 5) and BSK (stream 0x400000 + i) for the small LWE key */
 int tfhe_hip_sns_keygen(const tfhe_sns_params* sp, uint64_t seed, const uint64_t* lwe_key, uint64_t* glwe_key,
                         uint64_t* bsk /* nullable */);
+/* the same from a 192-bit rng key (OS entropy for production keys) */
+int tfhe_hip_sns_keygen_k(const tfhe_sns_params* sp, const tfhe_rng_key* rk, const uint64_t* lwe_key,
+                          uint64_t* glwe_key, uint64_t* bsk /* nullable */);
 typedef struct tfhe_sns_ctx tfhe_sns_ctx;
 int tfhe_hip_sns_create(const tfhe_sns_params* sp, int device, tfhe_sns_ctx** out);
 void tfhe_hip_sns_destroy(tfhe_sns_ctx* ctx);

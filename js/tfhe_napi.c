@@ -507,14 +507,37 @@ static napi_value queue_job(napi_env env, ctx_box* b, napi_value engine, job_t* 
   j->box = b;
   j->ctx = b->ctx;
   j->out = outp;
+  j->work = NULL;
   napi_create_reference(env, out, 1, &j->out_ref);
   napi_create_reference(env, engine, 1, &j->refs[j->nrefs++]);
   for (int i = 0; i < nkeep; i++) napi_create_reference(env, keep[i], 1, &j->refs[j->nrefs++]);
+  /* b->pending counts only jobs that were queued: on any failure below the references and the job are
+   * released here and the engine stays destroyable / reloadable */
+  napi_status st = napi_create_promise(env, &j->deferred, &promise);
+  const int have_promise = st == napi_ok;
+  if (st == napi_ok) {
+    napi_create_string_utf8(env, "tfhe_hip", NAPI_AUTO_LENGTH, &name);
+    st = napi_create_async_work(env, NULL, name, job_execute, job_complete, j, &j->work);
+  }
+  if (st == napi_ok) st = napi_queue_async_work(env, j->work);
+  if (st != napi_ok) {
+    if (j->work) napi_delete_async_work(env, j->work);
+    for (int i = 0; i < j->nrefs; i++) napi_delete_reference(env, j->refs[i]);
+    napi_delete_reference(env, j->out_ref);
+    if (have_promise) { /* settle the promise rather than leak its deferred */
+      napi_value err, code, msg;
+      napi_create_string_utf8(env, "EDEVICE", NAPI_AUTO_LENGTH, &code);
+      napi_create_string_utf8(env, "could not queue the async work", NAPI_AUTO_LENGTH, &msg);
+      napi_create_error(env, code, msg, &err);
+      napi_reject_deferred(env, j->deferred, err);
+      free(j);
+      return promise;
+    }
+    free(j);
+    napi_throw_error(env, "EDEVICE", "could not queue the async work");
+    return NULL;
+  }
   b->pending++;
-  NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
-  napi_create_string_utf8(env, "tfhe_hip", NAPI_AUTO_LENGTH, &name);
-  NAPI_CALL(env, napi_create_async_work(env, NULL, name, job_execute, job_complete, j, &j->work));
-  NAPI_CALL(env, napi_queue_async_work(env, j->work));
   return promise;
 }
 

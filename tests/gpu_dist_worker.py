@@ -10,7 +10,10 @@ node) in a torch.distributed group:
   3. (P-GATE) the C5 auction tree (256 FheUint32 bids, 8 levels) with every level sharded over the
      ranks and the winners all_gathered between levels.
 
-  RANK=r WORLD_SIZE=w MASTER_ADDR=127.0.0.1 MASTER_PORT=p python tests/gpu_dist_worker.py PRESET OUT_JSON
+  RANK=r WORLD_SIZE=w MASTER_ADDR=127.0.0.1 MASTER_PORT=p python tests/gpu_dist_worker.py PRESET OUT_JSON [G]
+
+G (default 1024, C2) sets the global batch of step 2; G = 65536 is C4's global batch (BASELINE.json configs[3]),
+checked at both sides of the rank boundary; step 3 (C5) runs only at the default G.
 """
 import json
 import os
@@ -30,7 +33,7 @@ from tfhe_amd.dist import broadcast_keys, sharded_map  # noqa: E402
 KEY_SEED = 0x7F4E0001
 
 
-def main(preset_name: str, out_path: str) -> int:
+def main(preset_name: str, out_path: str, G: int = 1024) -> int:
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", rank=rank, world_size=world)
     res = {"rank": rank, "world": world, "preset": preset_name}
@@ -63,8 +66,7 @@ def main(preset_name: str, out_path: str) -> int:
         if fhevm:
             eng.load_ms_key(zeros.numpy().view(np.uint64))
 
-        # 2. one global C2 batch, sharded over the ranks and gathered
-        G = 1024
+        # 2. one global batch (C2 by default, C4 at G = 65536), sharded over the ranks and gathered
         rng = np.random.default_rng(0xC0FFEE02)
         if fhevm:
             msgs = rng.integers(0, 16, G).astype(np.uint64)
@@ -89,12 +91,14 @@ def main(preset_name: str, out_path: str) -> int:
             from oracle import oracle as O
             prm = O.params(preset)
             keys = O.Keys(prm, KEY_SEED)
-            sel = np.array([0, 1, G // 2 - 1, G // 2, G // 2 + 1, G - 1])   # both sides of the shard boundary
+            bounds = [G * r // world for r in range(1, world)]
+            sel = np.array(sorted({0, 1, G - 1} | {b + d for b in bounds for d in (-1, 0, 1)}))  # both sides of each boundary
             ref = O.pbs_batch(prm, keys, cts[sel], lut[None])   # P-FHEVM: with the same MS zeros (seeded)
+            res["oracle_sample"] = sel.tolist()
             res["oracle_sample_ok"] = bool(np.array_equal(out[sel], ref))
 
         # 3. C5 auction tree, every level sharded over the ranks
-        if not fhevm:
+        if not fhevm and G == 1024:
             from tfhe_amd import integer as I
             from tfhe_amd.auction import max_tree
             v = np.random.default_rng(5).integers(0, 2**32, 256, dtype=np.uint64)
@@ -115,4 +119,4 @@ def main(preset_name: str, out_path: str) -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main(sys.argv[1], sys.argv[2]))
+    sys.exit(main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 1024))

@@ -62,3 +62,17 @@ def test_erc20_lockstep_transfers(backend):
     single0 = tok.c.launches
     tok.transfer(users[0], users[1], _amount(tok, 1))
     assert depth == tok.c.launches - single0       # four transfers cost the launches of one
+
+
+@pytest.mark.parametrize("backend", ["gate", "radix"])
+def test_erc20_self_transfer_keeps_balance(backend):
+    """EncryptedERC20.sol:211-216 writes balances[to] first and computes balances[from] from the stored
+    value: a transfer (or transferFrom) to oneself moves nothing and creates no tokens."""
+    tok, ck = _token(backend)
+    tok.mint(5000)
+    tok.transfer("alice", "alice", _amount(tok, 1200))
+    assert tok.balance_of(ck, "alice") == 5000
+    tok.approve("alice", "bob", _amount(tok, 700))
+    tok.transfer_from("bob", "alice", "alice", _amount(tok, 700))
+    assert tok.balance_of(ck, "alice") == 5000
+    assert tok.allowance(ck, "alice", "bob") == 0

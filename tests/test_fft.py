@@ -176,3 +176,36 @@ def test_decomp_23x1_high_word_restatement(oracle_mod):
             st = ((hi + 256) % 2**32) >> 9
             d = ((st + 0x3FFFFF) & 0x7FFFFF) - 0x3FFFFF
             assert [d] == oracle_mod.decompose(x, 23, 1), (hi, lo)
+
+
+def _fast_f64_to_torus(x: float) -> int:
+    """pbs_fft.hip's f64_to_torus (fft512.h), restated: rint, h = floor(t / 2^32), l = t - h 2^32, and the low
+    word of h taken from the mantissa of h + 1.5 * 2^52 -- exact only while |h| < 2^51, i.e. |x| < 2^83."""
+    import struct
+    t = float(np.rint(x))
+    h = math.floor(t * 2.0 ** -32)
+    l = t - h * 2.0 ** 32
+    hm = struct.unpack("<Q", struct.pack("<d", float(h) + 1.5 * 2.0 ** 52))[0] & 0xFFFFFFFF
+    return (hm << 32) | int(l)
+
+
+def test_pgate_inverse_output_bound_fast_torus_path(oracle_mod):
+    """P-GATE's inverse-transform outputs stay inside the fast f64_to_torus range by linearity:
+    |sum over (k+1)l = 6 rows of d (*) BSK| <= 6 * N * 2^6 * 2^63 = 2^81.58 < 2^83.  Adversarial case: every BSK
+    coefficient -2^63, digits +-64 signed so one output coefficient reaches the bound exactly; the fast form
+    equals the oracle's exact two-split form on every output."""
+    bound = 6 * N * 64 * 2 ** 63
+    assert math.log2(bound) < 81.6 and bound < 2 ** 83
+    bsk_poly = np.full(N, -2.0 ** 63)
+    K = oracle_mod.fft_fwd(bsk_poly)[0] / M          # or_bsk_to_fourier: x 2^-9
+    for k_peak in (0, 511, N - 1):
+        O = np.zeros(M, dtype=np.complex128)
+        for r in range(6):
+            d = np.where(np.arange(N) <= k_peak, 64.0, -64.0)   # coefficient k_peak sums every term with one sign
+            D = oracle_mod.fft_fwd(d)[0]
+            O = O + D * K
+        x = oracle_mod.fft_inv(O)[0]
+        assert np.max(np.abs(x)) < 2.0 ** 83
+        assert abs(abs(x[k_peak]) - bound) <= 2.0 ** 40   # the peak coefficient reaches the linear bound
+        for v in x[:: 37].tolist() + [x[k_peak]]:
+            assert _fast_f64_to_torus(v) == oracle_mod.f64_to_torus(v)

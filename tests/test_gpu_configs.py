@@ -19,8 +19,16 @@ pytestmark = pytest.mark.gpu
 P = 0xFFFFFFFF00000001
 
 
-def test_c3_fheuint8_lut_eval_4096(engine, product_keys, oracle_mod, gate_params, oracle_keys):
-    ck, _ = product_keys
+@pytest.mark.parametrize("transform", ["ntt", "fft64"])
+def test_c3_fheuint8_lut_eval_4096(request, transform, oracle_mod):
+    """C3 on both engines: the FFT64 engine is the default of the bench and of the JS binding."""
+    engine = request.getfixturevalue("engine" if transform == "ntt" else "gate_fft_engine")
+    ck, _ = request.getfixturevalue("product_keys" if transform == "ntt" else "gate_fft_keys")
+    if transform == "ntt":
+        gate_params, oracle_keys = request.getfixturevalue("gate_params"), request.getfixturevalue("oracle_keys")
+    else:
+        gate_params = oracle_mod.params(tfhe_amd.PRESET_GATE_FFT)
+        oracle_keys = oracle_mod.Keys(gate_params, 0x7F4E0001)
     B = 4096
     rng = np.random.default_rng(3)
     vals = rng.integers(0, 256, B).astype(np.uint64)

@@ -27,14 +27,15 @@ def _free_port() -> int:
     return port
 
 
-def _run_world(preset: str, tmp_path, world: int = 2):
+def _run_world(preset: str, tmp_path, world: int = 2, G: int = 1024):
     port = _free_port()
     procs, outs = [], []
     for r in range(world):
         out = str(tmp_path / f"rank{r}.json")
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "gpu_dist_worker.py"), preset, out],
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "gpu_dist_worker.py"), preset, out,
+                                       str(G)],
                                       cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
         outs.append(out)
     logs = []
@@ -63,3 +64,13 @@ def test_world2_engines_shard_gather_bitexact(preset, tmp_path):
         # the tree's comparisons really were split: each rank ran a share of the PBS
         assert all(r["c5_pbs_this_rank"] > 0 for r in res)
     print({r["rank"]: {k: r[k] for k in r if k.endswith("_s") or k.endswith("_ms")} for r in res})
+
+
+def test_world2_c4_global_batch_65536(tmp_path):
+    """C4's global batch (65,536 PBS, BASELINE.json configs[3]) through the world-2 engine path: 32,768 PBS per
+    rank, gathered, equal to a single-rank run of all 65,536, decrypted, oracle-exact across the rank boundary."""
+    res = _run_world("gate_fft", tmp_path, G=65536)
+    r0 = res[0]
+    assert r0["equal_single_rank"] and r0["decrypt_ok"] and r0["oracle_sample_ok"], r0
+    assert 32767 in r0["oracle_sample"] and 32768 in r0["oracle_sample"]
+    print({r["rank"]: r["sharded_s"] for r in res})

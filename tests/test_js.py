@@ -72,7 +72,7 @@ def test_js_integer_kats_cpu():
 
 
 def test_js_radix_kats_cpu():
-    """js/radix.js replays the 912 radix-layer fhEVM KATs with the same launch and PBS counts as
+    """js/radix.js replays all 2,394 radix-layer fhEVM KATs (ebool .. euint256) with the same launch and PBS counts as
     tfhe_amd/radix.py (tests/test_radix.py) — the two layers build identical circuits."""
     import sys
     sys.path.insert(0, os.path.dirname(__file__))

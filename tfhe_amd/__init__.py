@@ -103,10 +103,10 @@ ABI_SYMBOLS = (
     "tfhe_hip_sample_extract", "tfhe_hip_keyswitch", "tfhe_hip_ntt_fwd", "tfhe_hip_ntt_inv", "tfhe_hip_nand",
     "tfhe_hip_sync", "tfhe_hip_timing_enable", "tfhe_hip_timing_reset", "tfhe_hip_timing_stats",
     "tfhe_hip_server_keygen", "tfhe_hip_set_latency_batch", "tfhe_hip_ms_zeros_keygen", "tfhe_hip_load_ms_key",
-    "tfhe_hip_ms_reduce", "tfhe_hip_pks_params_preset", "tfhe_hip_pksk_len", "tfhe_hip_pks_keygen",
+    "tfhe_hip_ms_reduce", "tfhe_hip_pks_params_preset", "tfhe_hip_pksk_len", "tfhe_hip_pks_keygen", "tfhe_hip_pks_keygen_k", "tfhe_hip_bcast_plan",
     "tfhe_hip_pks_create", "tfhe_hip_pks_destroy", "tfhe_hip_pks_load_key", "tfhe_hip_pks_pack",
     "tfhe_hip_pks_pack_async", "tfhe_hip_pks_packed_words", "tfhe_hip_pks_compress", "tfhe_hip_pks_extract",
-    "tfhe_hip_glwe_phase", "tfhe_hip_sns_params_preset", "tfhe_hip_sns_bsk_len", "tfhe_hip_sns_keygen",
+    "tfhe_hip_glwe_phase", "tfhe_hip_sns_params_preset", "tfhe_hip_sns_bsk_len", "tfhe_hip_sns_keygen", "tfhe_hip_sns_keygen_k",
     "tfhe_hip_sns_create", "tfhe_hip_sns_destroy", "tfhe_hip_sns_load_key", "tfhe_hip_sns_squash",
     "tfhe_hip_sns_squash_async", "tfhe_hip_sns_blind_rotate", "tfhe_hip_sns_phase", "tfhe_hip_fft_fwd",
     "tfhe_hip_fft_inv", "tfhe_hip_rng_key_entropy", "tfhe_hip_rng_key_from_seed", "tfhe_hip_keygen_k",

@@ -16,7 +16,7 @@ from typing import List, Optional
 
 import numpy as np
 
-from . import _c_u64, _check, _stream_handle, _u64, lib
+from . import RngKey, _c_u64, _check, _stream_handle, _u64, lib, rng_key
 
 PKS_PRESET_ML2048 = 0
 _U64P = ctypes.POINTER(ctypes.c_uint64)
@@ -50,6 +50,7 @@ def _lib():
         L.tfhe_hip_pksk_len.argtypes = [P]
         L.tfhe_hip_pksk_len.restype = ctypes.c_size_t
         L.tfhe_hip_pks_keygen.argtypes = [P, ctypes.c_uint64, _U64P, _U64P, _U64P]
+        L.tfhe_hip_pks_keygen_k.argtypes = [P, ctypes.POINTER(RngKey), _U64P, _U64P, _U64P]
         L.tfhe_hip_pks_create.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
         L.tfhe_hip_pks_destroy.argtypes = [ctypes.c_void_p]
         L.tfhe_hip_pks_load_key.argtypes = [ctypes.c_void_p, _U64P, ctypes.c_size_t]
@@ -69,13 +70,14 @@ class CompressionKey:
     """Packing keyswitching key from an input LWE key (e.g. a GLWE key read as an LWE key) to a fresh
     binary GLWE key (`post_packing_key`, held by the client for decryption)."""
 
-    def __init__(self, params: PksParams, seed: int, in_key: np.ndarray, with_key: bool = True):
+    def __init__(self, params: PksParams, seed: Optional[int], in_key: np.ndarray, with_key: bool = True):
         L = _lib()
         self.params, self.seed = params, seed
         self.in_key = _c_u64(in_key)
         self.post_packing_key = np.zeros(params.out_k * params.out_N, dtype=np.uint64)
         self.pksk = np.zeros(L.tfhe_hip_pksk_len(ctypes.byref(params)), dtype=np.uint64) if with_key else None
-        _check(L.tfhe_hip_pks_keygen(ctypes.byref(params), seed, _u64(self.in_key), _u64(self.post_packing_key),
+        rk = rng_key(seed)  # None: 192 bits of OS entropy (production); an int: the public test stream
+        _check(L.tfhe_hip_pks_keygen_k(ctypes.byref(params), ctypes.byref(rk), _u64(self.in_key), _u64(self.post_packing_key),
                                      _u64(self.pksk) if with_key else None))
 
 

@@ -373,37 +373,85 @@ bool devices_distinct(const tfhe_ctx* c) {
   return true;
 }
 
-// Broadcast `count` u64 from src (on shard 0's device) into dst[i] of every shard i >= 1.
+// Broadcast planner (tfhe_hip_bcast_plan): which replication the key load takes and the per-rank call list.
+//   policy "rccl": RCCL even for one device (the plumbing test); "copy": device / peer copies; NULL or "" = auto:
+//   RCCL when the ordinals are distinct and librccl loads, device / peer copies otherwise (a repeated ordinal, or
+//   no RCCL: hipMemcpyPeerAsync reaches every xGMI peer without it).
+//   mode 2: calls[i] = rank i's ncclBroadcast inside ONE ncclGroupStart / ncclGroupEnd, root 0 (sends in place)
+//   first, every rank on its own communicator member and stream; mode 1: calls[i - 1] = destination shard i of
+//   copy i from shard 0; mode 0: nothing to do.  Returns the call count or a negative error.
+int bcast_plan(const int* devices, int ndev, const char* policy, bool rccl_ok, int* mode, int* calls, int max_calls,
+               std::string* why) {
+  const bool forced = policy && strcmp(policy, "rccl") == 0;
+  const bool copy = policy && strcmp(policy, "copy") == 0;
+  if (policy && *policy && !forced && !copy) {
+    if (why) *why = std::string("unknown broadcast policy '") + policy + "' (rccl | copy)";
+    return TFHE_HIP_EINVAL;
+  }
+  bool distinct = true;
+  for (int i = 0; i < ndev; i++)
+    for (int j = i + 1; j < ndev; j++)
+      if (devices[i] == devices[j]) distinct = false;
+  *mode = 0;
+  if (ndev < 2 && !forced) return 0;
+  if (forced) {
+    if (!distinct) {
+      if (why) *why = "RCCL broadcast needs distinct device ordinals";
+      return TFHE_HIP_EINVAL;
+    }
+    if (!rccl_ok) {
+      if (why) *why = "RCCL forced but unavailable";
+      return TFHE_HIP_EDEVICE;
+    }
+  }
+  const bool use_rccl = forced || (!copy && distinct && rccl_ok);
+  const int n = use_rccl ? ndev : ndev - 1;
+  if (calls && n > max_calls) {
+    if (why) *why = "call list too small";
+    return TFHE_HIP_EINVAL;
+  }
+  for (int i = 0; calls && i < n; i++) calls[i] = use_rccl ? i : i + 1;
+  *mode = use_rccl ? 2 : 1;
+  return n;
+}
+
+// Broadcast `count` u64 from src (on shard 0's device) into dst[i] of every shard i >= 1, as planned above.
 int broadcast(tfhe_ctx* c, const u64* src, const std::vector<u64*>& dst, size_t count) {
   const int nd = (int)c->sh.size();
   const char* env = getenv("TFHE_HIP_BCAST");
-  const bool forced = env && strcmp(env, "rccl") == 0;  // also a 1-device communicator: the RCCL plumbing test
-  if (nd < 2 && !forced) return 0;
-  const bool want_rccl = env ? forced : devices_distinct(c);
-  if (want_rccl) {
-    if (!devices_distinct(c)) return fail(TFHE_HIP_EINVAL, "RCCL broadcast needs distinct device ordinals");
-    Rccl& R = rccl();
-    if (!R.ok) return fail(TFHE_HIP_EDEVICE, "RCCL unavailable: %s", R.why.c_str());
+  std::vector<int> devs(nd), calls(nd);
+  for (int i = 0; i < nd; i++) devs[i] = c->sh[i].device;
+  bool distinct = true;
+  for (int i = 0; i < nd; i++)
+    for (int j = i + 1; j < nd; j++) distinct = distinct && devs[i] != devs[j];
+  // librccl is only probed when the plan could use it
+  const bool want = (env && strcmp(env, "rccl") == 0) || (nd > 1 && distinct && !(env && strcmp(env, "copy") == 0));
+  Rccl* R = want ? &rccl() : nullptr;
+  int mode = 0;
+  std::string why;
+  const int ncalls = bcast_plan(devs.data(), nd, env, R && R->ok, &mode, calls.data(), nd, &why);
+  if (ncalls < 0)
+    return fail(ncalls, "key broadcast: %s%s%s", why.c_str(), R && !R->ok ? ": " : "", R && !R->ok ? R->why.c_str() : "");
+  if (mode == 2) {
     if (c->comms.empty()) {
-      std::vector<int> devs(nd);
-      for (int i = 0; i < nd; i++) devs[i] = c->sh[i].device;
       c->comms.assign(nd, nullptr);
-      const ncclResult_t r = R.comm_init_all(c->comms.data(), nd, devs.data());
+      const ncclResult_t r = R->comm_init_all(c->comms.data(), nd, devs.data());
       if (r != ncclSuccess) {
         c->comms.clear();
-        return fail(TFHE_HIP_EDEVICE, "ncclCommInitAll: %s", R.err(r));
+        return fail(TFHE_HIP_EDEVICE, "ncclCommInitAll: %s", R->err(r));
       }
     }
-    R.group_start();
+    R->group_start();
     ncclResult_t r = ncclSuccess;
-    for (int i = 0; i < nd && r == ncclSuccess; i++) {
+    for (int k = 0; k < ncalls && r == ncclSuccess; k++) {
+      const int i = calls[k];
       DeviceGuard g(c->sh[i].device);
-      r = R.bcast(i == 0 ? (const void*)src : (const void*)dst[i], i == 0 ? (void*)src : (void*)dst[i], count,
-                  ncclUint64, 0, c->comms[i], c->sh[i].stream);
+      r = R->bcast(i == 0 ? (const void*)src : (const void*)dst[i], i == 0 ? (void*)src : (void*)dst[i], count,
+                   ncclUint64, 0, c->comms[i], c->sh[i].stream);
     }
-    const ncclResult_t r2 = R.group_end();
+    const ncclResult_t r2 = R->group_end();
     if (r != ncclSuccess || r2 != ncclSuccess)
-      return fail(TFHE_HIP_EDEVICE, "ncclBroadcast: %s", R.err(r != ncclSuccess ? r : r2));
+      return fail(TFHE_HIP_EDEVICE, "ncclBroadcast: %s", R->err(r != ncclSuccess ? r : r2));
     for (int i = 0; i < nd; i++) {
       DeviceGuard g(c->sh[i].device);
       HIP_TRY(hipStreamSynchronize(c->sh[i].stream));
@@ -411,13 +459,14 @@ int broadcast(tfhe_ctx* c, const u64* src, const std::vector<u64*>& dst, size_t 
     c->bcast_mode = 2;
     return 0;
   }
-  for (int i = 1; i < nd; i++) {
-    shard& s = c->sh[i];
+  if (mode == 0) return 0;
+  for (int k = 0; k < ncalls; k++) {
+    shard& s = c->sh[calls[k]];
     DeviceGuard g(s.device);
     if (s.device == c->sh[0].device)
-      HIP_TRY(hipMemcpyAsync(dst[i], src, count * 8, hipMemcpyDeviceToDevice, s.stream));
+      HIP_TRY(hipMemcpyAsync(dst[calls[k]], src, count * 8, hipMemcpyDeviceToDevice, s.stream));
     else
-      HIP_TRY(hipMemcpyPeerAsync(dst[i], s.device, src, c->sh[0].device, count * 8, s.stream));
+      HIP_TRY(hipMemcpyPeerAsync(dst[calls[k]], s.device, src, c->sh[0].device, count * 8, s.stream));
     HIP_TRY(hipStreamSynchronize(s.stream));
   }
   c->bcast_mode = 1;
@@ -728,6 +777,15 @@ int tfhe_hip_device_at(const tfhe_ctx* c, int i) {
   return c && i >= 0 && i < (int)c->sh.size() ? c->sh[(size_t)i].device : -1;
 }
 int tfhe_hip_key_bcast_mode(const tfhe_ctx* c) { return c ? c->bcast_mode : -1; }
+
+int tfhe_hip_bcast_plan(const int* devices, int ndev, const char* policy, int rccl_available, int* mode, int* calls,
+                        int max_calls) {
+  if (!devices || ndev < 1 || !mode || (max_calls > 0 && !calls)) return fail(TFHE_HIP_EINVAL, "bcast_plan: bad arguments");
+  std::string why;
+  const int n = bcast_plan(devices, ndev, policy, rccl_available != 0, mode, max_calls > 0 ? calls : nullptr, max_calls,
+                           &why);
+  return n < 0 ? fail(n, "bcast_plan: %s", why.c_str()) : n;
+}
 
 static int load_keys_impl(tfhe_ctx* c, const uint64_t* bsk, size_t bsk_len, const uint64_t* ksk, size_t ksk_len,
                           bool from_host) {

@@ -140,13 +140,19 @@ int tfhe_hip_pks_params_preset(int preset, tfhe_pks_params* o) {
 
 size_t tfhe_hip_pksk_len(const tfhe_pks_params* pp) { return pp ? tfhe::client::pksk_len(*pp) : 0; }
 
-int tfhe_hip_pks_keygen(const tfhe_pks_params* pp, uint64_t seed, const uint64_t* in_key, uint64_t* out_key,
-                        uint64_t* pksk) {
-  if (!pks_valid(pp) || !in_key || !out_key) return fail(TFHE_HIP_EINVAL, "pks_keygen: bad arguments");
+int tfhe_hip_pks_keygen_k(const tfhe_pks_params* pp, const tfhe_rng_key* rk, const uint64_t* in_key,
+                          uint64_t* out_key, uint64_t* pksk) {
+  if (!pks_valid(pp) || !rk || !in_key || !out_key) return fail(TFHE_HIP_EINVAL, "pks_keygen: bad arguments");
   for (uint32_t j = 0; j < pp->in_dim; j++)
     if (in_key[j] > 1) return fail(TFHE_HIP_EINVAL, "pks_keygen: in_key[%u] is not binary", j);
-  tfhe::client::pks_keygen(*pp, tfhe::client::rng_key_from_seed(seed), in_key, out_key, pksk);
+  tfhe::client::pks_keygen(*pp, *rk, in_key, out_key, pksk);
   return 0;
+}
+
+int tfhe_hip_pks_keygen(const tfhe_pks_params* pp, uint64_t seed, const uint64_t* in_key, uint64_t* out_key,
+                        uint64_t* pksk) {
+  const tfhe_rng_key rk = tfhe::client::rng_key_from_seed(seed);
+  return tfhe_hip_pks_keygen_k(pp, &rk, in_key, out_key, pksk);
 }
 
 int tfhe_hip_pks_create(const tfhe_pks_params* pp, int device, tfhe_pks_ctx** out) {

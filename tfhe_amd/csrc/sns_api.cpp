@@ -181,13 +181,19 @@ int tfhe_hip_sns_params_preset(int preset, tfhe_sns_params* o) {
 
 size_t tfhe_hip_sns_bsk_len(const tfhe_sns_params* sp) { return sp ? tfhe::client::sns_bsk_len(*sp) : 0; }
 
-int tfhe_hip_sns_keygen(const tfhe_sns_params* sp, uint64_t seed, const uint64_t* lwe_key, uint64_t* glwe_key,
-                        uint64_t* bsk) {
-  if (!sns_valid(sp) || !lwe_key || !glwe_key) return fail(TFHE_HIP_EINVAL, "sns_keygen: bad arguments");
+int tfhe_hip_sns_keygen_k(const tfhe_sns_params* sp, const tfhe_rng_key* rk, const uint64_t* lwe_key,
+                          uint64_t* glwe_key, uint64_t* bsk) {
+  if (!sns_valid(sp) || !rk || !lwe_key || !glwe_key) return fail(TFHE_HIP_EINVAL, "sns_keygen: bad arguments");
   for (uint32_t i = 0; i < sp->n; i++)
     if (lwe_key[i] > 1) return fail(TFHE_HIP_EINVAL, "sns_keygen: lwe_key[%u] is not binary", i);
-  tfhe::client::sns_keygen(*sp, tfhe::client::rng_key_from_seed(seed), lwe_key, glwe_key, bsk);
+  tfhe::client::sns_keygen(*sp, *rk, lwe_key, glwe_key, bsk);
   return 0;
+}
+
+int tfhe_hip_sns_keygen(const tfhe_sns_params* sp, uint64_t seed, const uint64_t* lwe_key, uint64_t* glwe_key,
+                        uint64_t* bsk) {
+  const tfhe_rng_key rk = tfhe::client::rng_key_from_seed(seed);
+  return tfhe_hip_sns_keygen_k(sp, &rk, lwe_key, glwe_key, bsk);
 }
 
 int tfhe_hip_sns_create(const tfhe_sns_params* sp, int device, tfhe_sns_ctx** out) {

@@ -219,8 +219,28 @@ def casting_keys(ck, pke_key: np.ndarray, seed: Optional[int] = None):
     if pke_key.shape[0] != p.k * p.N:
         raise ValueError(f"compact-PKE key dimension {pke_key.shape[0]} != k*N = {p.k * p.N}")
     sk = tfhe_amd.server_keygen(ck, seed)
-    cast = tfhe_amd.server_keygen(tfhe_amd.ClientKey(p, seed, ck.lwe_key, np.asarray(pke_key, dtype=np.uint64)), seed)
-    return tfhe_amd.ServerKey(p, sk.bsk, cast.ksk, sk.ms_zeros)
+    return tfhe_amd.ServerKey(p, sk.bsk, casting_ksk(ck, pke_key, seed), sk.ms_zeros)
+
+
+# seeded test streams of the casting KSK are offset from the server key's seed, so the two KSKs never share
+# a mask or noise term (their row difference would otherwise expose glwe_key XOR pke_key)
+CAST_SEED_TAG = 0xCA57_1E5D_0000_0000
+
+
+def casting_ksk(ck, pke_key: np.ndarray, seed: Optional[int] = None) -> np.ndarray:
+    """The casting KSK alone (compact-PKE key -> small LWE key, P-FHEVM KS 2^4 x 4): no BSK is generated.
+    seed None: its own 192 bits of OS entropy; an int: a test stream independent of ``server_keygen(ck,
+    seed)``'s."""
+    import ctypes
+    import tfhe_amd
+    p = ck.params
+    L = tfhe_amd.lib()
+    ksk = np.zeros(L.tfhe_hip_ksk_len(ctypes.byref(p)), dtype=np.uint64)
+    rk = tfhe_amd.rng_key(None if seed is None else (int(seed) ^ CAST_SEED_TAG) & (2**64 - 1))
+    lwe, pke = tfhe_amd._c_u64(ck.lwe_key), tfhe_amd._c_u64(np.asarray(pke_key, dtype=np.uint64))
+    tfhe_amd._check(L.tfhe_hip_server_keygen_k(ctypes.byref(p), ctypes.byref(rk), tfhe_amd._u64(lwe),
+                                               tfhe_amd._u64(pke), None, tfhe_amd._u64(ksk)))
+    return ksk
 
 
 T_LO = tuple(v % 4 for v in range(PACKED_MM))

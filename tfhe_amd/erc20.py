@@ -102,14 +102,19 @@ class EncryptedERC20:
         return (yield from self._move(sender, to, amount, can))
 
     def _move(self, frm: str, to: str, amount, ok):
+        """_transfer (:208-219): balances[to] is written first and balances[from] is then computed from the
+        stored value, so a self-transfer (frm == to) leaves the balance unchanged.  Callers store new_to
+        first and new_from last, the contract's write order."""
         value = yield from self.b.select(ok, amount, self.b.trivial(0))
         new_to = yield from self.b.op("add", self._bal(to), value)
-        new_from = yield from self.b.op("sub", self._bal(frm), value)
+        from_bal = new_to if frm == to else self._bal(frm)
+        new_from = yield from self.b.op("sub", from_bal, value)
         return new_from, new_to
 
     def transfer(self, sender: str, to: str, amount) -> None:
         new_from, new_to = self.c.run(self.transfer_op(sender, to, amount))
-        self.balances[sender], self.balances[to] = new_from, new_to
+        self.balances[to] = new_to
+        self.balances[sender] = new_from
 
     # -- :120-126 ----------------------------------------------------------------------------------
     def approve(self, owner: str, spender: str, amount) -> None:
@@ -128,7 +133,9 @@ class EncryptedERC20:
 
     def transfer_from(self, spender: str, frm: str, to: str, amount) -> None:
         a, f, t = self.c.run(self.transfer_from_op(spender, frm, to, amount))
-        self.allowances[(frm, spender)], self.balances[frm], self.balances[to] = a, f, t
+        self.allowances[(frm, spender)] = a
+        self.balances[to] = t
+        self.balances[frm] = f
 
     def balance_of(self, ck, who: str) -> int:
         return self.b.decrypt(ck, self._bal(who))

@@ -13,7 +13,7 @@ from typing import Optional
 
 import numpy as np
 
-from . import _c_u64, _check, _stream_handle, _u64, lib
+from . import RngKey, _c_u64, _check, _stream_handle, _u64, lib, rng_key
 
 SNS_PRESET_FHEVM = 0
 _U64P = ctypes.POINTER(ctypes.c_uint64)
@@ -46,6 +46,7 @@ def _lib():
         L.tfhe_hip_sns_bsk_len.argtypes = [P]
         L.tfhe_hip_sns_bsk_len.restype = ctypes.c_size_t
         L.tfhe_hip_sns_keygen.argtypes = [P, ctypes.c_uint64, _U64P, _U64P, _U64P]
+        L.tfhe_hip_sns_keygen_k.argtypes = [P, ctypes.POINTER(RngKey), _U64P, _U64P, _U64P]
         L.tfhe_hip_sns_create.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
         L.tfhe_hip_sns_destroy.argtypes = [ctypes.c_void_p]
         L.tfhe_hip_sns_load_key.argtypes = [ctypes.c_void_p, _U64P, ctypes.c_size_t]
@@ -61,13 +62,14 @@ def _lib():
 class SquashedKey:
     """128-bit GLWE key (client side) and the squashing BSK (server side) for a small LWE key."""
 
-    def __init__(self, params: SnsParams, seed: int, lwe_key: np.ndarray, with_bsk: bool = True):
+    def __init__(self, params: SnsParams, seed: Optional[int], lwe_key: np.ndarray, with_bsk: bool = True):
         L = _lib()
         self.params, self.seed = params, seed
         self.lwe_key = _c_u64(lwe_key)
         self.glwe_key = np.zeros(params.k * params.N, dtype=np.uint64)
         self.bsk = np.zeros(L.tfhe_hip_sns_bsk_len(ctypes.byref(params)), dtype=np.uint64) if with_bsk else None
-        _check(L.tfhe_hip_sns_keygen(ctypes.byref(params), seed, _u64(self.lwe_key), _u64(self.glwe_key),
+        rk = rng_key(seed)  # None: 192 bits of OS entropy (production); an int: the public test stream
+        _check(L.tfhe_hip_sns_keygen_k(ctypes.byref(params), ctypes.byref(rk), _u64(self.lwe_key), _u64(self.glwe_key),
                                      _u64(self.bsk) if with_bsk else None))
 
     def phase(self, cts: np.ndarray) -> list:

@@ -60,6 +60,11 @@ def main(tag, stats_csv, sq_csv, fetch_csv, write_csv, *rest):
         d.update({n: v for n, v in mix.get(k, {}).items()})
         if "SQ_INSTS_VALU" in c and s["avg_ms"] > 0:
             d["valu_issue_frac"] = round(c["SQ_INSTS_VALU"] * 4 / (1024 * 2.4e9 * s["avg_ms"] * 1e-3), 4)
+        m = mix.get(k, {})
+        f64 = sum(m.get(n, 0.0) for n in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                          "SQ_INSTS_VALU_TRANS_F64"))
+        if f64 and c.get("SQ_INSTS_VALU"):
+            d["f64_share"] = round(f64 / c["SQ_INSTS_VALU"], 4)   # f64 share of the VALU instruction stream
         if "SQ_WAVE_CYCLES" in c:
             for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_ANY"):
                 if n in c:
