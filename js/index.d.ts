@@ -79,6 +79,26 @@ export class FheUint16 extends FheUintN { static encrypt(v: number | bigint | Ar
 export class FheUint32 extends FheUintN { static encrypt(v: number | bigint | Array<number | bigint>, ck: ClientKey, e: Engine, seed?: bigint, stream0?: bigint): FheUint32; }
 export class FheUint64 extends FheUintN { static encrypt(v: number | bigint | Array<number | bigint>, ck: ClientKey, e: Engine, seed?: bigint, stream0?: bigint): FheUint64; }
 
+/** ciphertext compression (compression.rs:222,276): LWE list -> GLWE packing keyswitch + 26-bit bit packing */
+export class Packer {
+  constructor(device?: number);
+  static keygen(inKey: BigUint64Array, seed?: bigint): { outKey: BigUint64Array; pksk: BigUint64Array };
+  loadKey(pksk: BigUint64Array): this;
+  packCompress(lwes: BigUint64Array): Promise<Array<{ glwe: BigUint64Array; packed: BigUint64Array; bodies: number }>>;
+  static extract(packed: BigUint64Array, bodies: number): BigUint64Array;
+  static glwePhase(key: BigUint64Array, glwe: BigUint64Array): BigUint64Array;
+  destroy(): void;
+}
+/** switch-and-squash (the fhEVM sns-worker): P-FHEVM ciphertexts -> 128-bit LWEs, (lo, hi) u64 pairs */
+export class Squasher {
+  constructor(device?: number);
+  static keygen(lweKey: BigUint64Array, seed?: bigint): { glweKey: BigUint64Array; bsk: BigUint64Array };
+  loadKey(bsk: BigUint64Array): this;
+  squash(engine: Engine, cts: BigUint64Array, msgModulus?: number): Promise<BigUint64Array>;
+  static decrypt(glweKey: BigUint64Array, cts: BigUint64Array, msgModulus?: number): number[];
+  destroy(): void;
+}
+
 /** ciphertext bytes: 'TFA1' | u8 kind | u8 0 | u16 width | u32 lwe_dim | u32 count | u64[] (LE) */
 /** kind: 0 ebool / 1 euint (P-GATE bits), 2 radix euint / 3 radix ebool (P-FHEVM blocks) */
 export function serializeCiphertext(kind: 0 | 1 | 2 | 3, width: number, lweDim: number, count: number, words: BigUint64Array): Uint8Array;

@@ -118,6 +118,63 @@ class Engine {
   nand(c1, c2) { return native.nand(this.handle, c1, c2); }
 }
 
+/**
+ * Ciphertext compression (ml/extensions/rust/src/compression.rs:222,276: LWE list -> GLWE packing keyswitch, then
+ * CompressedModulusSwitchedGlweCiphertext::compress) on the GPU.  PARAMS_8B_2048_NEW: LWE dim 2048 -> k = 1,
+ * N = 2048, 2 x 2^14, 2048 LWEs per GLWE, 26-bit storage.
+ */
+class Packer {
+  constructor(device = 0) { this.handle = native.createPacker(device); }
+  /** inKey: the LWE key of the inputs (BigUint64Array(2048) bits); seed undefined = OS entropy.
+   *  -> {outKey (client, decrypts the packed GLWEs), pksk (server)} */
+  static keygen(inKey, seed = undefined) { return native.pksKeygen(inKey, rngArg(seed)); }
+  loadKey(pksk) { native.loadAuxKey(this.handle, pksk); return this; }
+  /** lwes: count x 2049 -> Promise<[{glwe, packed, bodies}]> one entry per GLWE of up to 2048 LWEs */
+  async packCompress(lwes) {
+    const r = await native.packCompress(this.handle, lwes);
+    const glweLen = 2 * 2048, count = lwes.length / 2049, out = [];
+    let off = 0;
+    for (let g = 0; g * 2048 < count; g++) {
+      const bodies = Math.min(2048, count - g * 2048);
+      const words = Math.ceil((2048 + bodies) * 26 / 64);   // tfhe_hip_pks_packed_words: 26 bits per coefficient
+      out.push({ glwe: r.glwes.subarray(g * glweLen, (g + 1) * glweLen), packed: r.packed.subarray(off, off + words), bodies });
+      off += words;
+    }
+    if (off !== r.packed.length) throw new Error(`packCompress: ${off} packed words expected, ${r.packed.length} returned`);
+    return out;
+  }
+  /** the decompression of one compressed GLWE (host) */
+  static extract(packed, bodies) { return native.extractGlwe(packed, bodies); }
+  static glwePhase(key, glwe) { return native.glwePhase(key, glwe); }
+  destroy() { if (this.handle) { native.destroyAux(this.handle); this.handle = null; } }
+}
+
+/**
+ * Switch-and-squash noise squashing (the fhEVM sns-worker, tests/fhevm-suite/fhevm/docker-compose/
+ * coprocessor-docker-compose.yml:124-140): P-FHEVM ciphertexts -> 128-bit LWEs (k = 2, N = 2048 squashing key)
+ * with ~2^-63 noise for threshold decryption.
+ */
+class Squasher {
+  constructor(device = 0) { this.handle = native.createSquasher(device); }
+  /** lweKey: the P-FHEVM small LWE key (918 bits); -> {glweKey (client, 128-bit), bsk (server)} */
+  static keygen(lweKey, seed = undefined) { return native.snsKeygen(lweKey, rngArg(seed)); }
+  loadKey(bsk) { native.loadAuxKey(this.handle, bsk); return this; }
+  /** engine: the P-FHEVM Engine holding the server key (keyswitch + modulus-switch reduction);
+   *  cts: B x 2049 -> Promise<BigUint64Array> B x 4097 x 2 ((lo, hi) words of the 128-bit LWEs) */
+  squash(engine, cts, msgModulus = 16) { return native.squash(this.handle, engine.handle, cts, msgModulus); }
+  /** client side: decrypt squashed ciphertexts (one padding bit, msgModulus values) */
+  static decrypt(glweKey, cts, msgModulus = 16) {
+    const ph = native.snsPhase(glweKey, cts), out = [];
+    const delta = (1n << 127n) / BigInt(msgModulus);
+    for (let i = 0; i < ph.length; i += 2) {
+      const v = ph[i] | (ph[i + 1] << 64n);
+      out.push(Number(((v + delta / 2n) / delta) % BigInt(msgModulus)));
+    }
+    return out;
+  }
+  destroy() { if (this.handle) { native.destroyAux(this.handle); this.handle = null; } }
+}
+
 /* gate linear part (0, c) + k1*c1 + k2*c2 over Z_2^64, ciphertext-wise */
 function gateLin(c1, c2, k1, k2, c, ctLen) {
   const out = new BigUint64Array(c1.length);
@@ -397,6 +454,6 @@ class LuxFHELocalClient {
 
 module.exports = {
   native, integer, radix, KIND, PRESET_GATE, PRESET_FHEVM, PRESET_GATE_FFT, PRESET_FHEVM_FFT, MU, paramsPreset, genKeys, ClientKey, ServerKey, Engine,
-  FheBool, FheUint8, FheUint16, FheUint32, FheUint64, UINT_CLASSES, LuxFHELocalClient,
+  Packer, Squasher, FheBool, FheUint8, FheUint16, FheUint32, FheUint64, UINT_CLASSES, LuxFHELocalClient,
   serializeCiphertext, parseCiphertext,
 };

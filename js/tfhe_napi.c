@@ -285,7 +285,10 @@ static void finalize_ctx(napi_env env, void* data, void* hint) {
 /* An engine handle.  Every queued job holds a reference to the handle's JS external (so GC cannot
  * finalize it while the job runs) and counts in `pending`; destroyEngine with jobs in flight only marks
  * the box, and the last job's completion (main thread, like destroyEngine) destroys the ctx. */
+#define BOX_ENGINE 0x454E4731u /* first word of every external's payload: which handle it is */
+#define BOX_AUX 0x41555831u
 typedef struct {
+  uint32_t magic; /* BOX_ENGINE */
   tfhe_ctx* ctx;
   tfhe_params p;
   int pending;
@@ -302,7 +305,7 @@ static void finalize_box(napi_env env, void* data, void* hint) {
 
 static ctx_box* get_box(napi_env env, napi_value v) {
   void* d = NULL;
-  if (napi_get_value_external(env, v, &d) != napi_ok) return NULL;
+  if (napi_get_value_external(env, v, &d) != napi_ok || !d || *(uint32_t*)d != BOX_ENGINE) return NULL;
   return (ctx_box*)d;
 }
 
@@ -352,6 +355,11 @@ static napi_value js_create(napi_env env, napi_callback_info info) {
   int rc = tfhe_hip_create(&p, devs, ndev, &c);
   if (rc) return throw_tfhe(env, rc);
   ctx_box* b = (ctx_box*)calloc(1, sizeof(ctx_box));
+  if (!b) {
+    tfhe_hip_destroy(c);
+    return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  }
+  b->magic = BOX_ENGINE;
   b->ctx = c;
   b->p = p;
   napi_value ext;
@@ -438,23 +446,80 @@ static napi_value js_load_keys(napi_env env, napi_callback_info info) {
 }
 
 /* ---- async work: pbs / nand / keyswitch / blindRotate ------------------------------------ */
-enum { JOB_PBS = 0, JOB_NAND = 1, JOB_KEYSWITCH = 2, JOB_BLIND_ROTATE = 3 };
+enum { JOB_PBS = 0, JOB_NAND = 1, JOB_KEYSWITCH = 2, JOB_BLIND_ROTATE = 3, JOB_PACK = 4, JOB_SQUASH = 5 };
+
+/* A packing-keyswitch (tfhe_pks_ctx) or noise-squashing (tfhe_sns_ctx) context: the adjacent kernels of the
+ * fhEVM coprocessor.  Same lifetime rules as an engine (pending jobs defer the teardown). */
+enum { AUX_PKS = 1, AUX_SNS = 2 };
+typedef struct {
+  uint32_t magic; /* BOX_AUX */
+  int kind;
+  void* ctx;
+  tfhe_pks_params pp;
+  tfhe_sns_params sp;
+  int pending;
+  int destroy_requested;
+} aux_box;
+
+static void aux_destroy(aux_box* a) {
+  if (!a->ctx) return;
+  if (a->kind == AUX_PKS) tfhe_hip_pks_destroy((tfhe_pks_ctx*)a->ctx);
+  else tfhe_hip_sns_destroy((tfhe_sns_ctx*)a->ctx);
+  a->ctx = NULL;
+}
+
 typedef struct {
   napi_async_work work;
   napi_deferred deferred;
   napi_ref refs[5];
   int nrefs;
-  ctx_box* box;
+  ctx_box* box;  /* NULL for packing jobs */
   tfhe_ctx* ctx;
+  aux_box* abox; /* packing / squashing jobs */
   int kind;
   const uint64_t *in, *in2, *luts;
   const uint32_t* lut_index;
   size_t B, n_lut;
+  uint32_t msg_modulus;
   uint64_t* out;
   napi_ref out_ref;
+  uint64_t* out2; /* JOB_PACK: the compressed words of every GLWE, concatenated */
+  napi_ref out2_ref;
   int rc;
   char err[256];
 } job_t;
+
+/* JOB_PACK: pack on the device, then modulus-switch + bit-pack every GLWE on the host (compression.rs:246-291) */
+static int run_pack(job_t* j) {
+  const tfhe_pks_params* pp = &j->abox->pp;
+  const size_t glwe_len = (size_t)(pp->out_k + 1) * pp->out_N;
+  int rc = tfhe_hip_pks_pack((tfhe_pks_ctx*)j->abox->ctx, j->in, j->B, j->out);
+  uint64_t* dst = j->out2;
+  for (size_t g = 0; !rc && g * pp->lwe_per_glwe < j->B; g++) {
+    const size_t left = j->B - g * pp->lwe_per_glwe;
+    const uint32_t bodies = (uint32_t)(left < pp->lwe_per_glwe ? left : pp->lwe_per_glwe);
+    rc = tfhe_hip_pks_compress(pp, j->out + g * glwe_len, bodies, dst);
+    dst += tfhe_hip_pks_packed_words(pp, bodies);
+  }
+  return rc;
+}
+
+/* JOB_SQUASH: the sns-worker path of one batch of P-FHEVM big-key ciphertexts: keyswitch + modulus-switch noise
+ * reduction on the engine, then the 128-bit bootstrap on the squasher */
+static int run_squash(job_t* j) {
+  const size_t small = (size_t)j->box->p.n + 1;
+  uint64_t* ks = (uint64_t*)malloc(j->B * small * 8);
+  uint64_t* ms = (uint64_t*)malloc(j->B * small * 8);
+  int32_t* picks = (int32_t*)malloc(j->B * sizeof(int32_t) + 1);
+  int rc = ks && ms && picks ? 0 : TFHE_HIP_ENOMEM;
+  if (!rc) rc = tfhe_hip_keyswitch(j->ctx, j->in, j->B, ks);
+  if (!rc) rc = tfhe_hip_ms_reduce(j->ctx, ks, j->B, ms, picks);
+  if (!rc) rc = tfhe_hip_sns_squash((tfhe_sns_ctx*)j->abox->ctx, ms, j->B, j->msg_modulus, j->out);
+  free(ks);
+  free(ms);
+  free(picks);
+  return rc;
+}
 
 static void job_execute(napi_env env, void* data) {
   (void)env;
@@ -462,7 +527,10 @@ static void job_execute(napi_env env, void* data) {
   if (j->kind == JOB_PBS) j->rc = tfhe_hip_pbs(j->ctx, j->in, j->B, j->luts, j->n_lut, j->lut_index, j->out);
   else if (j->kind == JOB_NAND) j->rc = tfhe_hip_nand(j->ctx, j->in, j->in2, j->B, j->out);
   else if (j->kind == JOB_KEYSWITCH) j->rc = tfhe_hip_keyswitch(j->ctx, j->in, j->B, j->out);
-  else j->rc = tfhe_hip_blind_rotate(j->ctx, j->in, j->B, j->luts, j->n_lut, j->lut_index, j->out);
+  else if (j->kind == JOB_BLIND_ROTATE)
+    j->rc = tfhe_hip_blind_rotate(j->ctx, j->in, j->B, j->luts, j->n_lut, j->lut_index, j->out);
+  else if (j->kind == JOB_PACK) j->rc = run_pack(j);
+  else j->rc = run_squash(j);
   if (j->rc) snprintf(j->err, sizeof(j->err), "%s", tfhe_hip_last_error());
 }
 
@@ -471,6 +539,14 @@ static void job_complete(napi_env env, napi_status status, void* data) {
   napi_value out;
   napi_get_reference_value(env, j->out_ref, &out);
   if (status == napi_ok && j->rc == 0) {
+    if (j->kind == JOB_PACK) { /* {glwes, packed} */
+      napi_value o, packed;
+      napi_get_reference_value(env, j->out2_ref, &packed);
+      napi_create_object(env, &o);
+      napi_set_named_property(env, o, "glwes", out);
+      napi_set_named_property(env, o, "packed", packed);
+      out = o;
+    }
     napi_resolve_deferred(env, j->deferred, out);
   } else {
     napi_value err, msg, code, num;
@@ -485,12 +561,15 @@ static void job_complete(napi_env env, napi_status status, void* data) {
   }
   for (int i = 0; i < j->nrefs; i++) napi_delete_reference(env, j->refs[i]);
   napi_delete_reference(env, j->out_ref);
+  if (j->out2_ref) napi_delete_reference(env, j->out2_ref);
   napi_delete_async_work(env, j->work);
   ctx_box* b = j->box;
-  if (--b->pending == 0 && b->destroy_requested && b->ctx) {
+  if (b && --b->pending == 0 && b->destroy_requested && b->ctx) {
     tfhe_hip_destroy(b->ctx);
     b->ctx = NULL;
   }
+  aux_box* a = j->abox;
+  if (a && --a->pending == 0 && a->destroy_requested) aux_destroy(a);
   free(j);
 }
 
@@ -505,7 +584,7 @@ static napi_value queue_job(napi_env env, ctx_box* b, napi_value engine, job_t* 
     return throw_tfhe(env, TFHE_HIP_ENOMEM);
   }
   j->box = b;
-  j->ctx = b->ctx;
+  j->ctx = b ? b->ctx : NULL;
   j->out = outp;
   j->work = NULL;
   napi_create_reference(env, out, 1, &j->out_ref);
@@ -524,6 +603,7 @@ static napi_value queue_job(napi_env env, ctx_box* b, napi_value engine, job_t* 
     if (j->work) napi_delete_async_work(env, j->work);
     for (int i = 0; i < j->nrefs; i++) napi_delete_reference(env, j->refs[i]);
     napi_delete_reference(env, j->out_ref);
+    if (j->out2_ref) napi_delete_reference(env, j->out2_ref);
     if (have_promise) { /* settle the promise rather than leak its deferred */
       napi_value err, code, msg;
       napi_create_string_utf8(env, "EDEVICE", NAPI_AUTO_LENGTH, &code);
@@ -537,7 +617,8 @@ static napi_value queue_job(napi_env env, ctx_box* b, napi_value engine, job_t* 
     napi_throw_error(env, "EDEVICE", "could not queue the async work");
     return NULL;
   }
-  b->pending++;
+  if (b) b->pending++;
+  if (j->abox) j->abox->pending++;
   return promise;
 }
 
@@ -654,6 +735,325 @@ static napi_value js_nand(napi_env env, napi_callback_info info) {
   return queue_job(env, b, argv[0], j, keep, 2, n1);
 }
 
+/* ---- adjacent kernels: packing keyswitch + compression, noise squashing ------------------
+ * The reference's consumers: ciphertext compression (ml/extensions/rust/src/compression.rs:222,276) and the
+ * fhEVM sns-worker (tests/fhevm-suite/fhevm/docker-compose/coprocessor-docker-compose.yml:124-140). */
+static void finalize_aux(napi_env env, void* data, void* hint) {
+  (void)env; (void)hint;
+  aux_box* a = (aux_box*)data;
+  if (a) {
+    aux_destroy(a); /* unreachable with jobs pending: they reference the external */
+    free(a);
+  }
+}
+
+static aux_box* get_aux(napi_env env, napi_value v, int kind) {
+  void* d = NULL;
+  if (napi_get_value_external(env, v, &d) != napi_ok || !d || *(uint32_t*)d != BOX_AUX) return NULL;
+  aux_box* a = (aux_box*)d;
+  return a->kind == kind && a->ctx && !a->destroy_requested ? a : NULL;
+}
+
+static int opt_device(napi_env env, size_t argc, napi_value* argv, size_t i, int* dev) {
+  *dev = 0;
+  if (argc <= i) return 1;
+  napi_valuetype t;
+  napi_typeof(env, argv[i], &t);
+  if (t == napi_undefined || t == napi_null) return 1;
+  return t == napi_number && napi_get_value_int32(env, argv[i], dev) == napi_ok;
+}
+
+/* createPacker([device = 0]) -> external (PARAMS_8B_2048_NEW packing keyswitch, the only preset) */
+static napi_value js_create_packer(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  int dev;
+  if (!opt_device(env, argc, argv, 0, &dev)) {
+    napi_throw_type_error(env, "EINVAL", "createPacker([device])");
+    return NULL;
+  }
+  aux_box* a = (aux_box*)calloc(1, sizeof(aux_box));
+  if (!a) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  a->magic = BOX_AUX;
+  a->kind = AUX_PKS;
+  int rc = tfhe_hip_pks_params_preset(TFHE_HIP_PKS_PRESET_ML2048, &a->pp);
+  tfhe_pks_ctx* c = NULL;
+  if (!rc) rc = tfhe_hip_pks_create(&a->pp, dev, &c);
+  if (rc) {
+    free(a);
+    return throw_tfhe(env, rc);
+  }
+  a->ctx = c;
+  napi_value ext;
+  NAPI_CALL(env, napi_create_external(env, a, finalize_aux, NULL, &ext));
+  return ext;
+}
+
+/* createSquasher([device = 0]) -> external (k = 2, N = 2048, 2^24 x 3 squashing PBS, TFHE_HIP_SNS_PRESET_FHEVM) */
+static napi_value js_create_squasher(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  int dev;
+  if (!opt_device(env, argc, argv, 0, &dev)) {
+    napi_throw_type_error(env, "EINVAL", "createSquasher([device])");
+    return NULL;
+  }
+  aux_box* a = (aux_box*)calloc(1, sizeof(aux_box));
+  if (!a) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  a->magic = BOX_AUX;
+  a->kind = AUX_SNS;
+  int rc = tfhe_hip_sns_params_preset(TFHE_HIP_SNS_PRESET_FHEVM, &a->sp);
+  tfhe_sns_ctx* c = NULL;
+  if (!rc) rc = tfhe_hip_sns_create(&a->sp, dev, &c);
+  if (rc) {
+    free(a);
+    return throw_tfhe(env, rc);
+  }
+  a->ctx = c;
+  napi_value ext;
+  NAPI_CALL(env, napi_create_external(env, a, finalize_aux, NULL, &ext));
+  return ext;
+}
+
+/* destroyAux(handle): deferred to the last pending job like destroyEngine */
+static napi_value js_destroy_aux(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  void* d = NULL;
+  if (argc && napi_get_value_external(env, argv[0], &d) == napi_ok && d && *(uint32_t*)d == BOX_AUX) {
+    aux_box* a = (aux_box*)d;
+    if (a->pending) a->destroy_requested = 1;
+    else aux_destroy(a);
+  }
+  return NULL;
+}
+
+/* pksKeygen(inKey[, rng]) -> {outKey, pksk}: the post-packing GLWE key (client) and the packing KSK (server) */
+static napi_value js_pks_keygen(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  tfhe_pks_params pp;
+  tfhe_rng_key rk;
+  uint64_t *in_key, *ok, *pk;
+  size_t n;
+  if (tfhe_hip_pks_params_preset(TFHE_HIP_PKS_PRESET_ML2048, &pp) || argc < 1 ||
+      !get_typed(env, argv[0], napi_biguint64_array, (void**)&in_key, &n) || n != pp.in_dim ||
+      !get_rng(env, argc > 1 ? argv[1] : NULL, &rk)) {
+    napi_throw_type_error(env, "EINVAL", "pksKeygen(inKey: BigUint64Array(2048)[, rng])");
+    return NULL;
+  }
+  napi_value o, a, b;
+  a = new_u64_array(env, (size_t)pp.out_k * pp.out_N, &ok);
+  b = new_u64_array(env, tfhe_hip_pksk_len(&pp), &pk);
+  if (!a || !b) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  int rc = tfhe_hip_pks_keygen_k(&pp, &rk, in_key, ok, pk);
+  if (rc) return throw_tfhe(env, rc);
+  napi_create_object(env, &o);
+  napi_set_named_property(env, o, "outKey", a);
+  napi_set_named_property(env, o, "pksk", b);
+  return o;
+}
+
+/* snsKeygen(lweKey[, rng]) -> {glweKey, bsk}: the 128-bit GLWE key (client) and the squashing BSK (server) */
+static napi_value js_sns_keygen(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  tfhe_sns_params sp;
+  tfhe_rng_key rk;
+  uint64_t *lwe_key, *gk, *bk;
+  size_t n;
+  if (tfhe_hip_sns_params_preset(TFHE_HIP_SNS_PRESET_FHEVM, &sp) || argc < 1 ||
+      !get_typed(env, argv[0], napi_biguint64_array, (void**)&lwe_key, &n) || n != sp.n ||
+      !get_rng(env, argc > 1 ? argv[1] : NULL, &rk)) {
+    napi_throw_type_error(env, "EINVAL", "snsKeygen(lweKey: BigUint64Array(918)[, rng])");
+    return NULL;
+  }
+  napi_value o, a, b;
+  a = new_u64_array(env, (size_t)sp.k * sp.N, &gk);
+  b = new_u64_array(env, tfhe_hip_sns_bsk_len(&sp), &bk);
+  if (!a || !b) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  int rc = tfhe_hip_sns_keygen_k(&sp, &rk, lwe_key, gk, bk);
+  if (rc) return throw_tfhe(env, rc);
+  napi_create_object(env, &o);
+  napi_set_named_property(env, o, "glweKey", a);
+  napi_set_named_property(env, o, "bsk", b);
+  return o;
+}
+
+/* loadAuxKey(handle, key): the packing KSK of a packer or the squashing BSK of a squasher */
+static napi_value js_load_aux_key(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  void* d = NULL;
+  uint64_t* key;
+  size_t n;
+  if (argc < 2 || napi_get_value_external(env, argv[0], &d) != napi_ok || !d || *(uint32_t*)d != BOX_AUX ||
+      !get_typed(env, argv[1], napi_biguint64_array, (void**)&key, &n)) {
+    napi_throw_type_error(env, "EINVAL", "loadAuxKey(packer | squasher, key)");
+    return NULL;
+  }
+  aux_box* a = (aux_box*)d;
+  if (!a->ctx || a->destroy_requested || a->pending) {
+    napi_throw_type_error(env, "EINVAL", "loadAuxKey: destroyed or busy handle");
+    return NULL;
+  }
+  const int rc = a->kind == AUX_PKS ? tfhe_hip_pks_load_key((tfhe_pks_ctx*)a->ctx, key, n)
+                                    : tfhe_hip_sns_load_key((tfhe_sns_ctx*)a->ctx, key, n);
+  if (rc) return throw_tfhe(env, rc);
+  return NULL;
+}
+
+/* packCompress(packer, lwes: count x 2049) -> Promise<{glwes, packed}>: LWE -> GLWE packing keyswitch on the
+ * device (chunks of 2048 LWEs per GLWE), then each GLWE modulus-switched and bit-packed (26 bits per word);
+ * `packed` concatenates the GLWEs' words (tfhe_hip_pks_packed_words(bodies) each, last one ragged) */
+static napi_value js_pack_compress(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  aux_box* a = argc ? get_aux(env, argv[0], AUX_PKS) : NULL;
+  uint64_t* in;
+  size_t n_in;
+  if (!a || argc < 2 || !get_typed(env, argv[1], napi_biguint64_array, (void**)&in, &n_in)) {
+    napi_throw_type_error(env, "EINVAL", "packCompress(packer, lwes)");
+    return NULL;
+  }
+  const tfhe_pks_params* pp = &a->pp;
+  const size_t dim = (size_t)pp->in_dim + 1;
+  if (!n_in || n_in % dim) {
+    napi_throw_range_error(env, "EINVAL", "packCompress: length is not a positive multiple of in_dim + 1");
+    return NULL;
+  }
+  const size_t count = n_in / dim, groups = (count + pp->lwe_per_glwe - 1) / pp->lwe_per_glwe;
+  size_t words = 0;
+  for (size_t g = 0; g < groups; g++) {
+    const size_t left = count - g * pp->lwe_per_glwe;
+    words += tfhe_hip_pks_packed_words(pp, (uint32_t)(left < pp->lwe_per_glwe ? left : pp->lwe_per_glwe));
+  }
+  job_t* j = (job_t*)calloc(1, sizeof(job_t));
+  if (!j) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  napi_value packed = new_u64_array(env, words, &j->out2);
+  if (!packed) {
+    free(j);
+    return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  }
+  napi_create_reference(env, packed, 1, &j->out2_ref);
+  j->kind = JOB_PACK;
+  j->abox = a;
+  j->in = in;
+  j->B = count;
+  napi_value keep[1] = {argv[1]};
+  return queue_job(env, NULL, argv[0], j, keep, 1, groups * (size_t)(pp->out_k + 1) * pp->out_N);
+}
+
+/* squash(squasher, engine, cts: B x 2049[, msgModulus = 16]) -> Promise<BigUint64Array> of B x (k N + 1) x 2
+ * ((lo, hi) u64 per 128-bit word): keyswitch + modulus-switch noise reduction on the P-FHEVM engine, then the
+ * squashing bootstrap */
+static napi_value js_squash(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  aux_box* a = argc ? get_aux(env, argv[0], AUX_SNS) : NULL;
+  ctx_box* b = argc > 1 ? get_box(env, argv[1]) : NULL;
+  uint64_t* in;
+  size_t n_in;
+  uint32_t mm = 16;
+  if (!a || !b || !b->ctx || b->destroy_requested || argc < 3 ||
+      !get_typed(env, argv[2], napi_biguint64_array, (void**)&in, &n_in) ||
+      (argc > 3 && napi_get_value_uint32(env, argv[3], &mm) != napi_ok)) {
+    napi_throw_type_error(env, "EINVAL", "squash(squasher, engine, cts[, msgModulus])");
+    return NULL;
+  }
+  if (b->p.order != 1 || b->p.n != a->sp.n) {
+    napi_throw_type_error(env, "EINVAL", "squash: the engine must run the P-FHEVM (KS -> PBS) parameter set");
+    return NULL;
+  }
+  const size_t big = (size_t)b->p.k * b->p.N + 1;
+  if (!n_in || n_in % big) {
+    napi_throw_range_error(env, "EINVAL", "squash: length is not a positive multiple of k*N + 1");
+    return NULL;
+  }
+  job_t* j = (job_t*)calloc(1, sizeof(job_t));
+  if (!j) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  j->kind = JOB_SQUASH;
+  j->abox = a;
+  j->in = in;
+  j->B = n_in / big;
+  j->msg_modulus = mm;
+  napi_value keep[2] = {argv[0], argv[2]};  /* the squasher handle too: the engine is argv[1] */
+  return queue_job(env, b, argv[1], j, keep, 2, j->B * ((size_t)a->sp.k * a->sp.N + 1) * 2);
+}
+
+/* extractGlwe(packed, bodies) -> BigUint64Array((k+1) N): the decompression of one compressed GLWE (host) */
+static napi_value js_extract_glwe(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  tfhe_pks_params pp;
+  uint64_t *packed, *out;
+  size_t n;
+  uint32_t bodies;
+  if (tfhe_hip_pks_params_preset(TFHE_HIP_PKS_PRESET_ML2048, &pp) || argc < 2 ||
+      !get_typed(env, argv[0], napi_biguint64_array, (void**)&packed, &n) ||
+      napi_get_value_uint32(env, argv[1], &bodies) != napi_ok || !bodies || bodies > pp.lwe_per_glwe ||
+      n != tfhe_hip_pks_packed_words(&pp, bodies)) {
+    napi_throw_type_error(env, "EINVAL", "extractGlwe(packed, bodies)");
+    return NULL;
+  }
+  napi_value res = new_u64_array(env, (size_t)(pp.out_k + 1) * pp.out_N, &out);
+  if (!res) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  int rc = tfhe_hip_pks_extract(&pp, packed, bodies, out);
+  if (rc) return throw_tfhe(env, rc);
+  return res;
+}
+
+/* glwePhase(key, glwe) -> BigUint64Array(N): client-side phase of a native GLWE (k = key.length / N) */
+static napi_value js_glwe_phase(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  uint64_t *key, *g, *out;
+  size_t nk, ng;
+  if (argc < 2 || !get_typed(env, argv[0], napi_biguint64_array, (void**)&key, &nk) ||
+      !get_typed(env, argv[1], napi_biguint64_array, (void**)&g, &ng) || ng <= nk || ng % (ng - nk)) {
+    napi_throw_type_error(env, "EINVAL", "glwePhase(key, glwe)");
+    return NULL;
+  }
+  const size_t N = ng - nk, k = nk / N;
+  napi_value res = new_u64_array(env, N, &out);
+  if (!res) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  int rc = tfhe_hip_glwe_phase((uint32_t)k, (uint32_t)N, key, g, out);
+  if (rc) return throw_tfhe(env, rc);
+  return res;
+}
+
+/* snsPhase(glweKey, cts) -> BigUint64Array of (lo, hi) phase pairs of squashed ciphertexts (client side) */
+static napi_value js_sns_phase(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  tfhe_sns_params sp;
+  uint64_t *key, *c, *out;
+  size_t nk, nc;
+  if (tfhe_hip_sns_params_preset(TFHE_HIP_SNS_PRESET_FHEVM, &sp) || argc < 2 ||
+      !get_typed(env, argv[0], napi_biguint64_array, (void**)&key, &nk) || nk != (size_t)sp.k * sp.N ||
+      !get_typed(env, argv[1], napi_biguint64_array, (void**)&c, &nc) || nc % (2 * (nk + 1))) {
+    napi_throw_type_error(env, "EINVAL", "snsPhase(glweKey, cts)");
+    return NULL;
+  }
+  const size_t count = nc / (2 * (nk + 1));
+  napi_value res = new_u64_array(env, 2 * count, &out);
+  if (!res) return throw_tfhe(env, TFHE_HIP_ENOMEM);
+  int rc = tfhe_hip_sns_phase(&sp, key, c, count, out);
+  if (rc) return throw_tfhe(env, rc);
+  return res;
+}
+
 static napi_value js_last_error(napi_env env, napi_callback_info info) {
   (void)info;
   napi_value s;
@@ -678,6 +1078,17 @@ static napi_value init(napi_env env, napi_value exports) {
       {"blindRotate", 0, js_blind_rotate, 0, 0, 0, napi_enumerable, 0},
       {"engineInfo", 0, js_engine_info, 0, 0, 0, napi_enumerable, 0},
       {"lastError", 0, js_last_error, 0, 0, 0, napi_enumerable, 0},
+      {"createPacker", 0, js_create_packer, 0, 0, 0, napi_enumerable, 0},
+      {"createSquasher", 0, js_create_squasher, 0, 0, 0, napi_enumerable, 0},
+      {"destroyAux", 0, js_destroy_aux, 0, 0, 0, napi_enumerable, 0},
+      {"pksKeygen", 0, js_pks_keygen, 0, 0, 0, napi_enumerable, 0},
+      {"snsKeygen", 0, js_sns_keygen, 0, 0, 0, napi_enumerable, 0},
+      {"loadAuxKey", 0, js_load_aux_key, 0, 0, 0, napi_enumerable, 0},
+      {"packCompress", 0, js_pack_compress, 0, 0, 0, napi_enumerable, 0},
+      {"squash", 0, js_squash, 0, 0, 0, napi_enumerable, 0},
+      {"extractGlwe", 0, js_extract_glwe, 0, 0, 0, napi_enumerable, 0},
+      {"glwePhase", 0, js_glwe_phase, 0, 0, 0, napi_enumerable, 0},
+      {"snsPhase", 0, js_sns_phase, 0, 0, 0, napi_enumerable, 0},
   };
   napi_define_properties(env, exports, sizeof(d) / sizeof(d[0]), d);
   return exports;

@@ -34,7 +34,9 @@ def test_js_addon_cpu(product_keys):
     out = _run("cpu_check.js", 300)
     assert out["exports"] == sorted(["paramsPreset", "keygen", "encrypt", "phase", "lutConstant", "lutFromTable",
                                      "createEngine", "destroyEngine", "loadKeys", "pbs", "nand", "lastError",
-                                     "keyswitch", "blindRotate", "engineInfo"])
+                                     "keyswitch", "blindRotate", "engineInfo", "createPacker", "createSquasher",
+                                     "destroyAux", "pksKeygen", "snsKeygen", "loadAuxKey", "packCompress", "squash",
+                                     "extractGlwe", "glwePhase", "snsPhase"])
     ck, sk = product_keys
     sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
     assert out["lwe_key_sha"] == sha(ck.lwe_key)
@@ -102,3 +104,43 @@ def test_js_server_fhevm_gpu():
 @pytest.mark.gpu
 def test_js_server_gpu():
     assert _run_plain("server_check.js", "gpu", timeout=900).startswith("OK server (gpu)")
+
+
+@pytest.mark.gpu
+def test_js_adjacent_gpu(tmp_path):
+    """packCompress and squash through N-API (compression.rs:222,276; the sns-worker,
+    coprocessor-docker-compose.yml:124-140) equal the Python / ctypes path byte for byte on the same keys."""
+    import tfhe_amd
+    from conftest import KEY_SEED
+    from tfhe_amd import compression as C
+    from tfhe_amd import sns as S
+    pp = C.PksParams.preset(C.PKS_PRESET_ML2048)
+    in_key = np.random.default_rng(5).integers(0, 2, pp.in_dim).astype(np.uint64)
+    count = 2048 + 77                                         # one full group + a ragged one
+    lwes = np.random.default_rng(6).integers(0, 2 ** 64 - 1, size=(count, pp.in_dim + 1), dtype=np.uint64)
+    in_key.tofile(tmp_path / "in_key.bin")
+    lwes.tofile(tmp_path / "lwes.bin")
+    out = _run("adjacent_gpu_check.js", 600, str(tmp_path), str(KEY_SEED))
+    assert out["ok"] and out["squash_decrypt_ok"] and out["groups"] == 2
+    assert out["extract_max_err_log2"] <= 64 - pp.storage_log + 1    # modulus switch to 26 bits
+    ck_pks = C.CompressionKey(pp, KEY_SEED, in_key)
+    assert np.array_equal(np.fromfile(tmp_path / "js_out_key.bin", dtype=np.uint64), ck_pks.post_packing_key)
+    packer = C.Packer(pp, 0).load_key(ck_pks)
+    glwes = packer.pack(lwes)
+    comp = packer.compress_ciphertexts_into_list(lwes)
+    packer.close()
+    assert np.array_equal(np.fromfile(tmp_path / "js_glwes.bin", dtype=np.uint64), glwes.reshape(-1))
+    assert np.array_equal(np.fromfile(tmp_path / "js_packed.bin", dtype=np.uint64),
+                          np.concatenate([c.packed for c in comp]))
+    params = tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM_FFT)
+    ck, sk = tfhe_amd.gen_keys(params, KEY_SEED)
+    msgs = np.array([(i * 7 + 3) % 16 for i in range(64)], dtype=np.uint64)
+    cts = ck.encrypt(msgs, 16, seed=KEY_SEED + 1)
+    sp = S.SnsParams.preset(0)
+    key = S.SquashedKey(sp, KEY_SEED, ck.lwe_key)
+    with tfhe_amd.Engine(params, 0) as eng:
+        eng.load_keys(sk)
+        sq = S.Squasher(sp, 0).load_key(key)
+        ref = S.squash_noise(eng, sq, cts)
+        sq.close()
+    assert np.array_equal(np.fromfile(tmp_path / "js_squash.bin", dtype=np.uint64), ref.reshape(-1))
