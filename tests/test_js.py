@@ -122,7 +122,9 @@ def test_js_adjacent_gpu(tmp_path):
     lwes.tofile(tmp_path / "lwes.bin")
     out = _run("adjacent_gpu_check.js", 600, str(tmp_path), str(KEY_SEED))
     assert out["ok"] and out["squash_decrypt_ok"] and out["groups"] == 2
-    assert out["extract_max_err_log2"] <= 64 - pp.storage_log + 1    # modulus switch to 26 bits
+    # 26-bit storage: each coefficient moves by < 2^37, the phase by < 2^44 over 2048 key bits (the bound
+    # tests/test_gpu_compression.py decodes messages spaced 2^45 apart under)
+    assert out["extract_max_err_log2"] <= 44
     ck_pks = C.CompressionKey(pp, KEY_SEED, in_key)
     assert np.array_equal(np.fromfile(tmp_path / "js_out_key.bin", dtype=np.uint64), ck_pks.post_packing_key)
     packer = C.Packer(pp, 0).load_key(ck_pks)
