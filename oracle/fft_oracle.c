@@ -385,7 +385,11 @@ void or_blind_rotate_fft(const or_params* p, const or_c64* bsk_f, const uint64_t
   const uint32_t bt = or_mod_switch(lwe_in[n], 2 * N);
   monomial_torus(acc + N, lt, N, (2 * N - bt) % (2 * N));
   static _Thread_local double dig[8][4 * FFT_M];
-  or_c64 D[2 * FFT_M], O[2][2 * FFT_M];
+  or_c64 D[2 * FFT_M], O[2][2 * FFT_M], Oc[2][2 * FFT_M];
+  /* MAC order.  N = 1024 (pbs_fft.hip: component-pair and latency kernels): one fma chain per component,
+   * O_j = O_j^0 + O_j^1 with O_j^c = chain over the levels of D_(c,l) (.) BSK_i[(c, l)][j] from zero.
+   * N = 2048 (pbs_fft2k.hip): one chain over every (c, l) from zero. */
+  const int split = N == 2 * FFT_M;
   double res[4 * FFT_M];
   int64_t d[64];
   for (uint32_t i = 0; i < n; i++) {
@@ -398,19 +402,30 @@ void or_blind_rotate_fft(const or_params* p, const or_c64* bsk_f, const uint64_t
         or_decompose(rot[j] - acc[(size_t)c * N + j], p->pbs_base_log, L, d);
         for (uint32_t l = 0; l < L; l++) dig[l][j] = (double)d[l];
       }
+      or_c64 (*A)[2 * FFT_M] = split ? Oc : O; /* this component's chain (split) or the running one */
+      if (split) memset(Oc, 0, sizeof(Oc));
       for (int l = (int)L - 1; l >= 0; l--) {
         or_fft_fwd(dig[l], N, D);
         const or_c64* row = bsk_f + per_i * i + (size_t)(c * L + l) * (k + 1) * M;
         for (uint32_t j = 0; j <= k; j++) {
           const or_c64* K = row + (size_t)j * M;
           for (uint32_t f = 0; f < M; f++) {
-            O[j][f].re = fma(D[f].re, K[f].re, O[j][f].re);
-            O[j][f].re = fma(-D[f].im, K[f].im, O[j][f].re);
-            O[j][f].im = fma(D[f].re, K[f].im, O[j][f].im);
-            O[j][f].im = fma(D[f].im, K[f].re, O[j][f].im);
+            A[j][f].re = fma(D[f].re, K[f].re, A[j][f].re);
+            A[j][f].re = fma(-D[f].im, K[f].im, A[j][f].re);
+            A[j][f].im = fma(D[f].re, K[f].im, A[j][f].im);
+            A[j][f].im = fma(D[f].im, K[f].re, A[j][f].im);
           }
         }
       }
+      if (split)
+        for (uint32_t j = 0; j <= k; j++)
+          for (uint32_t f = 0; f < M; f++) {
+            if (c == 0) O[j][f] = Oc[j][f];
+            else {
+              O[j][f].re = O[j][f].re + Oc[j][f].re;
+              O[j][f].im = O[j][f].im + Oc[j][f].im;
+            }
+          }
     }
     for (uint32_t j = 0; j <= k; j++) {
       or_fft_inv(O[j], N, res);

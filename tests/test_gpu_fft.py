@@ -111,23 +111,24 @@ def test_batch_4096_decrypts_and_sampled_bitexact(fft_engine, fft_keys, oracle_m
     assert np.array_equal(out[sample], ref)
 
 
-def test_batch_kernel_wave_counts_agree(fft_engine, fft_keys):
-    """Batches up to 1024 (above the latency kernel's range) run 4-ciphertext workgroups, larger ones 8:
-    every ciphertext's output is the same either way (1025 ciphertexts vs their first 1024)."""
+def test_batch_kernel_ragged_workgroups_agree(fft_engine, fft_keys):
+    """The component-pair batch kernel runs 4 ciphertexts per workgroup at any batch size above the latency
+    range: a ragged batch (1025 = 256 full workgroups + one with three padding pairs) gives every ciphertext the
+    same output as its first 1024 alone, and every output decrypts."""
     ck, _ = fft_keys
     bits = np.random.default_rng(0x4A8).integers(0, 2, 1025).astype(bool)
     cts = ck.encrypt_bool(bits, seed=0xC0FFEE4A)
     lut = fft_engine.gate_lut()
-    out8 = fft_engine.pbs(cts, lut)          # 1025 > 1024: 8 per workgroup
-    out4 = fft_engine.pbs(cts[:1024], lut)   # 4 per workgroup
-    assert np.array_equal(out8[:1024], out4)
-    assert np.array_equal(ck.decrypt_bool(out8), bits)
+    out_r = fft_engine.pbs(cts, lut)
+    out_f = fft_engine.pbs(cts[:1024], lut)
+    assert np.array_equal(out_r[:1024], out_f)
+    assert np.array_equal(ck.decrypt_bool(out_r), bits)
 
 
 @pytest.mark.parametrize("B", [1, 9, 300])
 def test_latency_and_batch_kernels_agree(fft_engine, fft_keys, oracle_mod, fft_params, fft_okeys, B):
-    """The latency-mode kernel (one ciphertext per workgroup, 6 transforms in parallel) and the batch
-    kernel (4 ciphertexts per workgroup at these sizes) produce identical accumulators and PBS outputs."""
+    """The latency-mode kernel (one ciphertext per workgroup, 6 transforms in parallel) and the component-pair
+    batch kernel (4 ciphertexts x 2 waves per workgroup) produce identical accumulators and PBS outputs."""
     ck, _ = fft_keys
     rng = np.random.default_rng(B + 1024)
     msgs = rng.integers(0, 8, B).astype(np.uint64) * np.uint64((1 << 63) // 8)

@@ -207,6 +207,102 @@ __device__ __forceinline__ void dft512_fwd_t(double (&xr)[8], double (&xi)[8], d
   dft8<false>(xr, xi);
 }
 
+// the same with pass A's twiddles (this lane's 8, slot 0 included: the merged twist) held in registers
+__device__ __forceinline__ void dft512_fwd_ra(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
+                                              const double2 (&wa)[8], const double2* twB) {
+  dft8<false>(xr, xi);
+#pragma unroll
+  for (int e = 0; e < 8; e++) cmul<false>(xr[e], xi[e], wa[e]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[lane + S1 * e] = make_double2(xr[e], xi[e]);
+  lds_order();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[tb.b1 + 8 * e];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  lds_order();
+  dft8<false>(xr, xi);
+#pragma unroll
+  for (int e = 1; e < 8; e++) cmul<false>(xr[e], xi[e], twB[64 * e + lane]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[lane + S2 * e] = make_double2(xr[e], xi[e]);
+  lds_order();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[tb.b2 + e];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  lds_order();
+  dft8<false>(xr, xi);
+}
+
+// pass A and pass B twiddles both in registers (wb[0] unused)
+__device__ __forceinline__ void dft512_fwd_rab(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
+                                               const double2 (&wa)[8], const double2 (&wb)[8]) {
+  dft8<false>(xr, xi);
+#pragma unroll
+  for (int e = 0; e < 8; e++) cmul<false>(xr[e], xi[e], wa[e]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[lane + S1 * e] = make_double2(xr[e], xi[e]);
+  lds_order();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[tb.b1 + 8 * e];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  lds_order();
+  dft8<false>(xr, xi);
+#pragma unroll
+  for (int e = 1; e < 8; e++) cmul<false>(xr[e], xi[e], wb[e]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[lane + S2 * e] = make_double2(xr[e], xi[e]);
+  lds_order();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[tb.b2 + e];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  lds_order();
+  dft8<false>(xr, xi);
+}
+
+// inverse with pass C''s twiddles (= pass B's table, conjugated by cmul<true>) in registers, pass B' from twI
+__device__ __forceinline__ void dft512_inv_rb(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
+                                              const double2 (&wb)[8], const double2* twI) {
+  dft8<true>(xr, xi);
+#pragma unroll
+  for (int e = 1; e < 8; e++) cmul<true>(xr[e], xi[e], wb[e]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[tb.b2 + e] = make_double2(xr[e], xi[e]);
+  lds_order();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[lane + S2 * e];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  lds_order();
+  dft8<true>(xr, xi);
+#pragma unroll
+  for (int e = 0; e < 8; e++) cmul<true>(xr[e], xi[e], twI[64 * e + lane]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[tb.b1 + 8 * e] = make_double2(xr[e], xi[e]);
+  lds_order();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[lane + S1 * e];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  lds_order();
+  dft8<true>(xr, xi);
+}
+
 template <bool TW0 = false>
 __device__ __forceinline__ void dft512_fwd(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
                                            const double2* tw) {

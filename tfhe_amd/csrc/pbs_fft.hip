@@ -149,7 +149,7 @@ __global__ __launch_bounds__(64) void fft_inv_kernel(const double2* __restrict__
 #ifndef FFT_INVTW
 #define FFT_INVTW 1
 #endif
-constexpr int FB_WAVES = 8;
+[[maybe_unused]] constexpr int FB_WAVES = 8;
 constexpr int CHUNK_C64 = 2 * M;                   // one level step: rows (c, l), j = 0, 1 (16 KB)
 constexpr int CHUNK_GLDS = CHUNK_C64 * 16 / 1024;  // 1 KB wave-instructions per chunk (16)
 // KBUF 3: s_waitcnt vmcnt(CHUNK_GLDS / W), the global_load_lds a wave issues per chunk (gfx9 encoding:
@@ -394,12 +394,243 @@ __global__ __launch_bounds__(64 * W, 1) void blind_rotate_fft_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
+// Component-pair batch kernel (round 3, the default above the latency range): workgroup = 4 ciphertexts x 2
+// waves, wave (p, c) owns COMPONENT c of ciphertext p.  Per CMUX i:
+//   rotate + decompose acc_c (wave-local: the wave's own transpose area holds the rotation image)
+//   level steps q = 0, 1, 2 (least significant first): digits -> twist -> DFT -> MAC into BOTH outputs'
+//     partial sums  O_j^c = fma chain over q of D_(c,q) (.) BSK_i[(c, q)][j]      (j = 0, 1)
+//     one step's chunk = rows (0, q) and (1, q) of BSK_i (32 KB), streamed once per workgroup by
+//     global_load_lds, double-buffered
+//   exchange: wave c publishes O_(1-c)^c in its transpose area and takes O_c^(1-c) from its partner's:
+//     O_c = O_c^c + O_c^(1-c)  (= O_c^0 + O_c^1: f64 addition commutes, the oracle's split order)
+//   ONE inverse transform: acc_c += rint(iFFT(O_c)) mod 2^64
+// Against the 8-ciphertext kernel above: the same transforms per ciphertext, half of them per wave, one
+// barrier fewer per CMUX (3 chunk steps + 2 for the exchange), 1/2 the accumulator / partial-sum registers
+// per wave, and twice the waves per ciphertext -- a batch of 1024 fills all 256 CUs at 2 waves / SIMD.
+// The MAC order (per-component chains, then one add) is restated in oracle/fft_oracle.c.
+// LDS: 8 x 9 KB transpose areas | 2 x 32 KB level steps | pass A, B, B' tables (24 KB) = 160 KB.
+constexpr int FP_WAVES = 8, FP_CTS = 4;
+// FFT_PAIR_TWREG: pass A's twiddles held in registers across the CMUX loop (the round-2 ablation: -4 %)
+#ifndef FFT_PAIR_TWREG
+#define FFT_PAIR_TWREG 2
+#endif
+constexpr int STEP_C64 = 4 * M;                    // rows (0, q), (1, q), j = 0, 1
+struct FpShared {
+  double2 tw[3 * M];                               // TW_A | TW_B | TW_I of the global table (no twist table)
+  double2 T[FP_WAVES][T_C64];                      // after the tables: T - 8 KB is still inside the block
+  double2 K[2][STEP_C64];
+};
+typedef __attribute__((address_space(3))) u64 lds_u64;
+
+// (X^a v - v), v = this wave's polynomial (slot e <-> coefficient 64 e + L), to decomposition states.  The
+// rotation image is the wave's transpose area.  Coefficient 64 e + L reads image entry (u + 64 e) mod 1024 with
+// u = (L - a) mod 1024, negated iff the negacyclic source index (L - a + 64 e) mod 2048 lies in [1024, 2048):
+// reads before the per-lane wrap use base u and DS offset 512 e, wrapped reads the base 8 KB lower (one compare
+// and one select per slot instead of the index arithmetic; the sign mask is an SGPR xor).
+__device__ __forceinline__ void rotate_states(const u64 (&v)[16], int a, int lane, double2* T, u32 (&st)[16]) {
+  u64* Tu = (u64*)T;
+#pragma unroll
+  for (int e = 0; e < 16; e++) Tu[64 * e + lane] = v[e];
+  lds_order();
+  const int t0 = (lane - a) & 2047;        // a < 2048
+  const int u = t0 & 1023;
+  const bool neg0 = t0 >= 1024;
+  const u32 a0 = (u32)(uintptr_t)(lds_u64*)&Tu[u];
+  const u32 a1 = a0 - 8192u;
+#pragma unroll
+  for (int e = 0; e < 16; e++) {
+    const bool wrap = u >= 1024 - 64 * e;
+    const u32 base = wrap ? a1 : a0;
+    const u64 x = ((const lds_u64*)(uintptr_t)base)[64 * e];
+    const bool neg = neg0 != wrap;
+    const u64 r = neg ? 0 - x : x;
+    st[e] = decomp_state(r - v[e]);
+  }
+  lds_order();
+}
+
+// the partial-sum exchange of wave c (compile-time): publish O_(1-c)^c in this wave's area, add O_c^(1-c) from
+// the partner's (two workgroup barriers)
+template <int C>
+__device__ __forceinline__ void exchange_partials(const double (&o0r)[8], const double (&o0i)[8], const double (&o1r)[8],
+                                                  const double (&o1i)[8], double (&xr)[8], double (&xi)[8], double2* T,
+                                                  const double2* Tp, int lane) {
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    T[64 * e + lane] = C ? make_double2(o0r[e], o0i[e]) : make_double2(o1r[e], o1i[e]);
+    xr[e] = C ? o1r[e] : o0r[e];
+    xi[e] = C ? o1i[e] : o0i[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 w = Tp[64 * e + lane];
+    xr[e] = xr[e] + w.x;
+    xi[e] = xi[e] + w.y;
+  }
+  __syncthreads();  // the partner has read this wave's area before the inverse overwrites it
+}
+
+// level step g = 3 i + q: 32 KB in 1 KB blocks; wave w loads blocks 4 w .. 4 w + 3 (16 per component row)
+__device__ __forceinline__ void load_step(const double2* __restrict__ bsk, int g, double2* dst, int wave_s, int lane) {
+  const int i = g / 3, q = g - 3 * (g / 3);
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int blk = wave_s * 4 + u;
+    const int c = blk >> 4;
+    const char* src = (const char*)(bsk + ((size_t)i * 6 + c * 3 + q) * (2 * M)) + (blk & 15) * 1024;
+    __builtin_amdgcn_global_load_lds((const void*)(src + lane * 16),
+                                     (__attribute__((address_space(3))) void*)((char*)dst + blk * 1024), 16, 0, 0);
+  }
+}
+
+template <bool WRITE_ACC, bool WRITE_BIG>
+__global__ __launch_bounds__(64 * FP_WAVES, 1) void blind_rotate_fft_pair_kernel(
+    const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
+    int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tw_g, u64* __restrict__ out_big,
+    u64* __restrict__ out_acc) {
+  __shared__ __attribute__((aligned(16))) FpShared sh;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = wave & 1;
+  const size_t b_raw = (size_t)blockIdx.x * FP_CTS + (wave >> 1);
+  const bool live = b_raw < B;
+  const size_t b = live ? b_raw : B - 1;  // padding pairs run a copy of the last ciphertext, store nothing
+  const u64* ct = lwe_in + b * (size_t)(n + 1);
+  double2* T = sh.T[wave];
+  const double2* Tp = sh.T[wave ^ 1];
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const int c_s = wave_s & 1;
+  const int n_steps = 3 * n;
+
+  for (int q = threadIdx.x; q < 3 * M; q += 64 * FP_WAVES) sh.tw[q] = tw_g[TW_A + q];
+  load_step(bsk, 0, sh.K[0], wave_s, lane);
+
+  // acc_c: A = 0, B = X^{-b~} * lut (LUT values in the Z_p encoding, mapped to the torus first)
+  u64 acc[16];
+  {
+    int li = lut_index ? (int)lut_index[b] : 0;
+    li = (li < 0 || li >= n_lut) ? 0 : li;
+    const u64* lut = luts + (size_t)li * N1K;
+    const int s = (2048 - ms2048(ct[n])) & 2047;
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      int d = 64 * e + lane - s;
+      bool neg = false;
+      if (d < 0) { d += N1K; neg = !neg; }
+      if (d < 0) { d += N1K; neg = !neg; }
+      const u64 v = gl_to_torus(lut[d]);
+      acc[e] = c ? (neg ? 0 - v : v) : 0;
+    }
+  }
+
+  const TBase tb(lane);
+  const double2* twA = sh.tw;
+  const double2* twB = sh.tw + M;
+  const double2* twI = sh.tw + 2 * M;
+#if FFT_PAIR_TWREG
+  double2 wa[8];  // pass A's twiddles (twist merged) for the whole CMUX loop: 8 LDS reads fewer per transform
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 8; e++) wa[e] = twA[64 * e + lane];
+#endif
+#if FFT_PAIR_TWREG >= 2
+  double2 wb[8];  // and pass B's (the inverse's pass C' conjugates the same table): 7 more per forward, 7 per inverse
+#pragma unroll
+  for (int e = 1; e < 8; e++) wb[e] = twB[64 * e + lane];
+  wb[0] = make_double2(1.0, 0.0);
+#endif
+#if FFT_PRIO == 1
+  if (wave_s >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
+  for (int i = 0; i < n; i++) {
+    // (X^a acc_c - acc_c), decomposed: the rotation image in this wave's own transpose area (its previous
+    // user, the last inverse, is this wave: DS operations of a wave run in order)
+    u32 st[16];
+    rotate_states(acc, ms2048(ct[i]), lane, T, st);
+    double o0r[8], o0i[8], o1r[8], o1i[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) { o0r[e] = 0; o0i[e] = 0; o1r[e] = 0; o1i[e] = 0; }
+#pragma unroll 1
+    for (int q = 0; q < 3; q++) {
+      const int g = 3 * i + q;
+      glds_barrier();  // step g's chunk is in K[g & 1]; every wave is done with K[(g + 1) & 1]
+      if (g + 1 < n_steps) load_step(bsk, g + 1, sh.K[(g + 1) & 1], wave_s, lane);
+      const u32 bmask = q < 2 ? 1u : 0u;
+      double xr[8], xi[8];
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        xr[e] = (double)decomp_step(st[e], bmask);
+        xi[e] = (double)decomp_step(st[e + 8], bmask);
+      }
+      twist_slots<false>(xr, xi);
+#if FFT_PAIR_TWREG >= 2
+      dft512_fwd_rab(xr, xi, T, lane, tb, wa, wb);
+#elif FFT_PAIR_TWREG
+      dft512_fwd_ra(xr, xi, T, lane, tb, wa, twB);
+#else
+      dft512_fwd_t<true>(xr, xi, T, lane, tb, twA, twB);
+#endif
+      const double2* k0 = sh.K[g & 1] + c * (2 * M) + lane;
+      const double2* k1 = k0 + M;
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const double2 u = k0[64 * e], v = k1[64 * e];
+        o0r[e] = __builtin_fma(xr[e], u.x, o0r[e]);
+        o0r[e] = __builtin_fma(-xi[e], u.y, o0r[e]);
+        o0i[e] = __builtin_fma(xr[e], u.y, o0i[e]);
+        o0i[e] = __builtin_fma(xi[e], u.x, o0i[e]);
+        o1r[e] = __builtin_fma(xr[e], v.x, o1r[e]);
+        o1r[e] = __builtin_fma(-xi[e], v.y, o1r[e]);
+        o1i[e] = __builtin_fma(xr[e], v.y, o1i[e]);
+        o1i[e] = __builtin_fma(xi[e], v.x, o1i[e]);
+      }
+    }
+    // exchange the partial sums: publish O_(1-c)^c, take O_c^(1-c) (c wave-uniform: a scalar branch, no selects)
+    double xr[8], xi[8];
+    if (c_s) exchange_partials<1>(o0r, o0i, o1r, o1i, xr, xi, T, Tp, lane);
+    else exchange_partials<0>(o0r, o0i, o1r, o1i, xr, xi, T, Tp, lane);
+#if FFT_PAIR_TWREG >= 2
+    dft512_inv_rb(xr, xi, T, lane, tb, wb, twI);
+#else
+    dft512_inv_t(xr, xi, T, lane, tb, twB, twI);
+#endif
+    twist_slots<true>(xr, xi);
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      acc[e] += f64_to_torus(xr[e]);
+      acc[e + 8] += f64_to_torus(xi[e]);
+    }
+  }
+
+  if (!live) return;
+  if (WRITE_ACC) {
+    u64* oa = out_acc + b * 2048 + c * N1K;
+#pragma unroll
+    for (int e = 0; e < 16; e++) oa[64 * e + lane] = acc[e];
+  }
+  if (WRITE_BIG) {
+    // sample extraction at degree 0 (computations.rs:109-132): a'_0 = A[0], a'_j = -A[N-j], b' = B[0]
+    u64* ob = out_big + b * (size_t)(N1K + 1);
+    if (c == 0) {
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        const int idx = 64 * e + lane;
+        if (idx == 0) ob[0] = acc[e];
+        else ob[N1K - idx] = 0 - acc[e];
+      }
+    } else if (lane == 0) {
+      ob[N1K] = acc[0];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Latency-mode blind rotation (small batches): ONE ciphertext per workgroup of 8 waves.  Per CMUX:
 //   A  waves 0..5: wave r = chain position (c, q) (c = r / 3; q = 0, 1, 2: levels least significant
 //      first) rotates + decomposes accumulator polynomial c, keeps step q's digits and transforms
 //      them -> F[r]                                                     (6 transforms in parallel)
-//   B  all 8 waves: O_j = fma chain over r = 0..5 of F[r] (.) BSK_i[r][j] (the oracle's order) on 2
-//      of the 8 slots each (j = wave >> 2); the BSK words come straight from L2, loaded into
+//   B  all 8 waves: O_j = O_j^0 + O_j^1, O_j^c = fma chain over r = 3c .. 3c + 2 of F[r] (.) BSK_i[r][j]
+//      (the oracle's split order) on 2 of the 8 slots each (j = wave >> 2); the BSK words come straight from L2, loaded into
 //      registers before phase A so their latency hides behind the transforms
 //   C  waves 0, 1: inverse transform of O_j, acc_j += rint mod 2^64      (2 transforms in parallel)
 // Three barriers per CMUX; the critical path is 1 forward + 1 inverse transform + 1/4 of the MAC
@@ -485,16 +716,17 @@ __global__ __launch_bounds__(FL_THREADS, 1) void blind_rotate_fft_lat_kernel(
 #pragma unroll
       for (int t = 0; t < 2; t++) {
         const int e = s0 + t;
-        double re = 0.0, im = 0.0;
+        double re[2] = {0.0, 0.0}, im[2] = {0.0, 0.0};  // per-component chains, then one add (oracle order)
 #pragma unroll
         for (int r = 0; r < 6; r++) {
           const double2 D = sh.F[r][64 * e + lane], K = kv[r][t];
-          re = __builtin_fma(D.x, K.x, re);
-          re = __builtin_fma(-D.y, K.y, re);
-          im = __builtin_fma(D.x, K.y, im);
-          im = __builtin_fma(D.y, K.x, im);
+          const int cc = r / 3;
+          re[cc] = __builtin_fma(D.x, K.x, re[cc]);
+          re[cc] = __builtin_fma(-D.y, K.y, re[cc]);
+          im[cc] = __builtin_fma(D.x, K.y, im[cc]);
+          im[cc] = __builtin_fma(D.y, K.x, im[cc]);
         }
-        O[64 * e + lane] = make_double2(re, im);
+        O[64 * e + lane] = make_double2(re[0] + re[1], im[0] + im[1]);
       }
     }
     __syncthreads();
@@ -631,6 +863,9 @@ hipError_t launch_bsk_to_fourier(const u64* bsk_std, double* bsk_f, size_t polys
 #ifndef FFT_W4_MAX
 #define FFT_W4_MAX 1024
 #endif
+#ifndef FFT_LEGACY_BATCH
+#define FFT_LEGACY_BATCH 0
+#endif
 template <int W>
 static hipError_t launch_batch(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index, int n_lut,
                                const double2* bk, const double2* t, u64* out_big, u64* out_acc, hipStream_t s) {
@@ -667,8 +902,23 @@ hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64
                          n_lut, bk, t, out_big, out_acc);
     return hipGetLastError();
   }
+#if FFT_LEGACY_BATCH
+  // the round-2 8-ciphertext kernel (chain MAC order: NOT bit-identical with the split-order oracle; A/B timing only)
   if (B <= FFT_W4_MAX) return launch_batch<4>(lwe_in, B, n, luts, lut_index, n_lut, bk, t, out_big, out_acc, s);
   return launch_batch<FB_WAVES>(lwe_in, B, n, luts, lut_index, n_lut, bk, t, out_big, out_acc, s);
+#else
+  dim3 grid((unsigned)((B + FP_CTS - 1) / FP_CTS)), block(64 * FP_WAVES);
+  if (out_acc && out_big)
+    hipLaunchKernelGGL((blind_rotate_fft_pair_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                       n_lut, bk, t, out_big, out_acc);
+  else if (out_acc)
+    hipLaunchKernelGGL((blind_rotate_fft_pair_kernel<true, false>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                       n_lut, bk, t, out_big, out_acc);
+  else
+    hipLaunchKernelGGL((blind_rotate_fft_pair_kernel<false, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                       n_lut, bk, t, out_big, out_acc);
+  return hipGetLastError();
+#endif
 }
 
 hipError_t launch_sample_extract_torus(const u64* acc, size_t B, u64* out, hipStream_t s) {
