@@ -142,7 +142,7 @@ def test_latency_and_batch_kernels_agree(fft_engine, fft_keys, oracle_mod, fft_p
         acc_l = fft_engine.blind_rotate(cts, lut)
         out_l = fft_engine.pbs(cts, lut)
     finally:
-        fft_engine.set_latency_batch(512)  # the FFT64 default
+        fft_engine.set_latency_batch(256)  # the P-GATE FFT64 default
     assert np.array_equal(acc_l, acc_b)
     assert np.array_equal(out_l, out_b)
     i = B // 2
@@ -165,7 +165,7 @@ def test_fft_edge_cases(fft_engine, oracle_mod, fft_params, fft_okeys):
         fft_engine.set_latency_batch(lat)
         assert np.array_equal(fft_engine.pbs(triv, gate), oracle_mod.pbs_batch_fft(fft_params, fft_okeys, triv, lut))
         assert np.array_equal(fft_engine.pbs(edge, gate), oracle_mod.pbs_batch_fft(fft_params, fft_okeys, edge, lut))
-    fft_engine.set_latency_batch(512)
+    fft_engine.set_latency_batch(256)
     with pytest.raises(tfhe_amd.TfheError) as e:
         fft_engine.pbs(triv, gate, lut_index=[0, 1, 0])
     assert e.value.code == -1

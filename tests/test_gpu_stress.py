@@ -55,7 +55,7 @@ def test_stress_pgate_fft64_64k(gate_fft_engine, gate_fft_keys):
             want = bits if rep % 2 == 0 else bits[::-1]
             bad += int(np.count_nonzero(ck.decrypt_bool(out) != want))
     finally:
-        gate_fft_engine.set_latency_batch(512)
+        gate_fft_engine.set_latency_batch(256)
     assert bad == 0, f"{bad} wrong of {4 * B}"
 
 

@@ -742,7 +742,9 @@ int tfhe_hip_create(const tfhe_params* p, const int* devices, int ndev, tfhe_ctx
   // measured latency-kernel crossovers (tools/latency_sweep.py, tools/latency_sweep_fft.sh): NTT engine
   // 1024 (N = 1024) / 512 (N = 2048); FFT64 512 for both N (from the third round of latency workgroups
   // on, workgroups that start staggered stream the BSK from L2 at different CMUX indices)
-  c->lat_max = is_fft(*p) ? 512 : p->N == 2048 ? 512 : 1024;
+  // round 3: the P-GATE FFT64 component-pair batch kernel runs any batch up to 1024 in one 6.7 ms round, the
+  // latency kernel 3.5-3.7 ms up to 256 and 7.1 ms from 257 (profiles/r03_latsweep.json): crossover 256
+  c->lat_max = is_fft(*p) ? (p->N == 1024 ? 256 : 512) : p->N == 2048 ? 512 : 1024;
   {
     const char* e = getenv("TFHE_HIP_KS_VALU");
     c->ks_valu = e && e[0] == '1';

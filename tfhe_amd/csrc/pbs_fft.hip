@@ -410,6 +410,11 @@ __global__ __launch_bounds__(64 * W, 1) void blind_rotate_fft_kernel(
 // The MAC order (per-component chains, then one add) is restated in oracle/fft_oracle.c.
 // LDS: 8 x 9 KB transpose areas | 2 x 32 KB level steps | pass A, B, B' tables (24 KB) = 160 KB.
 constexpr int FP_WAVES = 8, FP_CTS = 4;
+// FFT_ROT_BATCH: the rotation's 16 image reads issued together before their first use (measured with the
+// first level peeled: 27.04 -> 27.55 ms per 4096, slower; kept for A/B runs)
+#ifndef FFT_ROT_BATCH
+#define FFT_ROT_BATCH 0
+#endif
 // FFT_PAIR_TWREG: pass A's twiddles held in registers across the CMUX loop (the round-2 ablation: -4 %)
 #ifndef FFT_PAIR_TWREG
 #define FFT_PAIR_TWREG 2
@@ -437,6 +442,21 @@ __device__ __forceinline__ void rotate_states(const u64 (&v)[16], int a, int lan
   const bool neg0 = t0 >= 1024;
   const u32 a0 = (u32)(uintptr_t)(lds_u64*)&Tu[u];
   const u32 a1 = a0 - 8192u;
+#if FFT_ROT_BATCH
+  u64 x[16];
+#pragma unroll
+  for (int e = 0; e < 16; e++) {
+    const bool wrap = u >= 1024 - 64 * e;
+    x[e] = ((const lds_u64*)(uintptr_t)(wrap ? a1 : a0))[64 * e];
+  }
+  __builtin_amdgcn_sched_barrier(0);  // all 16 reads in flight before the first use
+#pragma unroll
+  for (int e = 0; e < 16; e++) {
+    const bool neg = neg0 != (u >= 1024 - 64 * e);
+    const u64 r = neg ? 0 - x[e] : x[e];
+    st[e] = decomp_state(r - v[e]);
+  }
+#else
 #pragma unroll
   for (int e = 0; e < 16; e++) {
     const bool wrap = u >= 1024 - 64 * e;
@@ -446,6 +466,7 @@ __device__ __forceinline__ void rotate_states(const u64 (&v)[16], int a, int lan
     const u64 r = neg ? 0 - x : x;
     st[e] = decomp_state(r - v[e]);
   }
+#endif
   lds_order();
 }
 

@@ -294,6 +294,40 @@ __device__ __forceinline__ void rotate_decompose(const u64 (&acc)[16], int a, in
   pair_sync();
 }
 
+// F2_ROT_OWN (default): the rotation image in split halves, half p (the parity-p coefficients) in the transpose area
+// of the pair's wave p, so each wave writes only its own area: the barrier that guarded the partner's previous
+// inverse transposes goes, and the rotated reads take the P-GATE form.  For this wave's coefficient c = 2 m + h
+// (m = L + 64 e) the source c - a has the uniform parity p = (h - a) mod 2 and position (t >> 1) mod 1024 in half p,
+// t >> 1 = L + K + 64 e with K = (h - a + 4096) >> 1; negated iff bit 10 of t >> 1 is set.  So: base u = (L + K) mod
+// 1024, DS offset 512 e, the base 8 KB lower after the per-lane wrap, sign = bit 10 of (L + K) xor wrap.
+#ifndef F2_ROT_OWN
+#define F2_ROT_OWN 1
+#endif
+typedef __attribute__((address_space(3))) u64 lds_u64;
+__device__ __forceinline__ void rotate_decompose_own(const u64 (&acc)[16], int a, int h, int lane, double2* Tm,
+                                                     const double2* T0, const double2* T1, int (&dig)[16]) {
+  u64* Tu = (u64*)Tm;
+#pragma unroll
+  for (int e = 0; e < 16; e++) Tu[64 * e + lane] = acc[e];
+  pair_sync();
+  const int p = (h - a) & 1;  // wave-uniform
+  const int u0 = (lane + ((h - a + 4096) >> 1)) & 2047;
+  const int u = u0 & 1023;
+  const bool neg0 = u0 >= 1024;
+  const u64* src = (const u64*)(p ? T1 : T0);
+  const u32 a0 = (u32)(uintptr_t)(const lds_u64*)&src[u];
+  const u32 a1 = a0 - 8192u;
+#pragma unroll
+  for (int e = 0; e < 16; e++) {
+    const bool wrap = u >= 1024 - 64 * e;
+    const u64 x = ((const lds_u64*)(uintptr_t)(wrap ? a1 : a0))[64 * e];
+    const u64 m = 0ull - (u64)(neg0 != wrap);  // all ones iff negated
+    const u64 y = ((x ^ m) - m) - acc[e];
+    dig[e] = decomp_23x1_hi((u32)(y >> 32));
+  }
+  pair_sync();
+}
+
 // LDS address of this wave's slot 0 in K, laundered: with K's absolute offset folded in, the MAC's
 // reads would exceed the 16-bit DS immediate and each take a VGPR of its own
 __device__ __forceinline__ lds_c64* kbase(const double2* kbuf, int h, int lane) {
@@ -371,7 +405,7 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
   double2* T0 = sh.T[2 * pr];
   double2* T1 = sh.T[2 * pr + 1];
   double2* Tm = sh.T[wave];
-  u64* R = (u64*)T0;  // 16 KB across the pair's two regions
+  [[maybe_unused]] u64* R = (u64*)T0;  // 16 KB across the pair's two regions (F2_ROT_OWN = 0)
   const double2* tt = sh.tw;
   const TBase tb(lane);
 
@@ -413,15 +447,23 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
     const int a = ms4096(ct[i]);
     int dg[16];
     double d0r[8], d0i[8], xr[8], xi[8], o0r[8], o0i[8];
+#if F2_ROT_OWN
+    rotate_decompose_own(accA, a, h, lane, Tm, T0, T1, dg);
+#else
     __syncthreads();  // the previous CMUX's inverse transforms are done with T
     rotate_decompose(accA, a, h, lane, R, dg);
+#endif
 #pragma unroll
     for (int e = 0; e < 8; e++) {
       d0r[e] = (double)dg[e];
       d0i[e] = (double)dg[e + 8];
     }
     fwd_half(d0r, d0i, h, lane, tb, T0, T1, tt);
+#if F2_ROT_OWN
+    rotate_decompose_own(accB, a, h, lane, Tm, T0, T1, dg);
+#else
     rotate_decompose(accB, a, h, lane, R, dg);
+#endif
 #pragma unroll
     for (int e = 0; e < 8; e++) {
       xr[e] = (double)dg[e];

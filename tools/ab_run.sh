@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 for round in ${ROUNDS:-1}; do
-  for d in build_ab/*/; do
+  for d in build_ab/${ONLY:-*}/; do
     n=$(basename $d)
     rm -f gpurun_out/ab_$n.json
     TFHE_HIP_LIB=$PWD/$d/libtfhe_hip.so timeout -k 10 300 python bench.py ${BENCH_ARGS:-} --steps 5 --warmup 2 --no-cpu > gpurun_out/ab_$n.json 2>/dev/null
