@@ -270,15 +270,16 @@ int tfhe_hip_glwe_phase(uint32_t k, uint32_t N, const uint64_t* key, const uint6
  * fhEVM's sns-worker (coprocessor-docker-compose.yml:124-140) turns each 64-bit P-FHEVM ciphertext into
  * a Z_2^128 LWE with tiny noise for threshold decryption: keyswitch to the small key, modulus-switch
  * noise reduction (tfhe_hip_ms_reduce), then a PBS with a BSK under a 128-bit GLWE key (k=2, N=2048,
- * 2^24 x 3) and the identity LUT.  The GLWE ring is Z_Q, Q = (2^64-2^32+1)(2^64-2^34+1), as residues;
- * rule and conversions: oracle/sns_oracle.c.  Output: (k*N + 1) x (lo, hi) u64 per ciphertext. */
+ * 2^24 x 3) and the identity LUT.  The GLWE ring is the native 2^128 torus (as tfhe-rs): a coefficient
+ * is one u128 word, a polynomial two u64 planes [lo][N], [hi][N]; rule: oracle/sns_oracle.c.
+ * Output: (k*N + 1) x (lo, hi) u64 per ciphertext. */
 typedef struct tfhe_sns_params {
   uint32_t n, k, N, base_log, level;
   int32_t noise_log2; /* Gaussian noise round(N(0,1) * 2^(64 + x)) on the 128-bit bodies */
 } tfhe_sns_params;
 #define TFHE_HIP_SNS_PRESET_FHEVM 0 /* n = 918 (P-FHEVM small key), k = 2, N = 2048, 2^24 x 3, noise 2^30 */
 int tfhe_hip_sns_params_preset(int preset, tfhe_sns_params* out);
-size_t tfhe_hip_sns_bsk_len(const tfhe_sns_params* sp); /* n*(k+1)L*(k+1)*2*N: [i][c*L+l][j][prime][N] */
+size_t tfhe_hip_sns_bsk_len(const tfhe_sns_params* sp); /* n*(k+1)L*(k+1)*2*N: [i][c*L+l][j][lo, hi][N] */
 /* 128-bit GLWE key (k*N bits, ChaCha stream 5) and BSK (stream 0x400000 + i) for the small LWE key */
 int tfhe_hip_sns_keygen(const tfhe_sns_params* sp, uint64_t seed, const uint64_t* lwe_key, uint64_t* glwe_key,
                         uint64_t* bsk /* nullable */);
@@ -288,17 +289,16 @@ int tfhe_hip_sns_keygen_k(const tfhe_sns_params* sp, const tfhe_rng_key* rk, con
 typedef struct tfhe_sns_ctx tfhe_sns_ctx;
 int tfhe_hip_sns_create(const tfhe_sns_params* sp, int device, tfhe_sns_ctx** out);
 void tfhe_hip_sns_destroy(tfhe_sns_ctx* ctx);
-/* Loading rounds every key coefficient (centred mod Q) to the nearest multiple of 2^16 (oracle:
- * or_sns_bsk_round; ~2^20 of extra phase noise beside the key's 2^30).  The default external product
+/* Loading rounds every key word (read as a signed 128-bit integer) to the nearest multiple of 2^16
+ * (oracle: or_sns_bsk_round; ~2^20 of extra phase noise beside the key's 2^30).  The external product
  * splits the rounded key into seven 16-bit limbs and computes each digit x limb convolution as an
- * exact f64 FFT product (5.7 KB of key spectra per coefficient row: n x 9 x 3 x 7 x 1024 complex, 2.8 GB
- * at n = 918); TFHE_HIP_SNS_NTT=1 at create selects the Z_p NTT product instead (same results). */
+ * exact f64 FFT product (n x 9 x 3 x 7 x 1024 complex of key spectra: 2.8 GB at n = 918). */
 int tfhe_hip_sns_load_key(tfhe_sns_ctx* ctx, const uint64_t* bsk, size_t len);
 /* B small-key ciphertexts (B x (n+1)) -> B x (k*N+1) x 2 u64; identity LUT over msg_modulus values */
 int tfhe_hip_sns_squash(tfhe_sns_ctx* ctx, const uint64_t* lwe_small, size_t B, uint32_t msg_modulus, uint64_t* out);
 int tfhe_hip_sns_squash_async(tfhe_sns_ctx* ctx, const uint64_t* d_lwe_small, size_t B, uint32_t msg_modulus,
                               uint64_t* d_out, void* stream);
-/* stage-level (parity tests): accumulator after the CMUX loop, B x (k+1) x 2 x N residues */
+/* stage-level (parity tests): accumulator after the CMUX loop, B x (k+1) x (lo, hi) x N words */
 int tfhe_hip_sns_blind_rotate(tfhe_sns_ctx* ctx, const uint64_t* lwe_small, size_t B, uint32_t msg_modulus,
                               uint64_t* acc_out);
 /* client: phase b - <a, s> mod 2^128 of count squashed ciphertexts -> (lo, hi) pairs */

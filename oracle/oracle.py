@@ -455,36 +455,38 @@ class SnsKeys:
     def __init__(self, sp: SnsParams, seed: int, lwe_key: np.ndarray, with_bsk: bool = True):
         L = lib()
         L.or_sns_bsk_len.restype = ctypes.c_size_t
+        L.or_sns_limb_ntt_len.restype = ctypes.c_size_t
         self.sp, self.seed = sp, seed
         self.lwe_key = np.ascontiguousarray(lwe_key, dtype=np.uint64)
         self.glwe_key = np.zeros(sp.k * sp.N, dtype=np.uint64)
         self.bsk = np.zeros(L.or_sns_bsk_len(ctypes.byref(sp)), dtype=np.uint64) if with_bsk else None
         L.or_sns_keygen(ctypes.byref(sp), ctypes.c_uint64(seed), _p(self.lwe_key), _p(self.glwe_key),
                         _p(self.bsk) if with_bsk else None)
-        self._bsk_ntt = None
+        self._bsk_limb = None
 
     @property
-    def bsk_ntt(self) -> np.ndarray:
-        if self._bsk_ntt is None:
-            # the device rounds the key to multiples of 2^16 at load (or_sns_bsk_round): same here
+    def bsk_limb(self) -> np.ndarray:
+        """The key as the blind rotation consumes it: rounded to multiples of 2^16 at load (or_sns_bsk_round,
+        as the device does), then the NTTs of its seven 16-bit limb polynomials (2.8 GB at n = 918)."""
+        if self._bsk_limb is None:
             rounded = np.zeros_like(self.bsk)
             lib().or_sns_bsk_round(ctypes.byref(self.sp), _p(self.bsk), _p(rounded))
-            self._bsk_ntt = rounded
-            lib().or_sns_bsk_to_ntt(ctypes.byref(self.sp), _p(rounded), _p(self._bsk_ntt))
-        return self._bsk_ntt
+            self._bsk_limb = np.zeros(lib().or_sns_limb_ntt_len(ctypes.byref(self.sp)), dtype=np.uint64)
+            lib().or_sns_bsk_to_limb_ntt(ctypes.byref(self.sp), _p(rounded), _p(self._bsk_limb))
+        return self._bsk_limb
 
 
 def sns_squash(sp: SnsParams, keys: SnsKeys, small: np.ndarray, msg_modulus: int = 16, threads: int = 0) -> np.ndarray:
     small = np.ascontiguousarray(small, dtype=np.uint64).reshape(-1, sp.n + 1)
     out = np.zeros((small.shape[0], sp.k * sp.N + 1, 2), dtype=np.uint64)
-    lib().or_sns_squash(ctypes.byref(sp), _p(keys.bsk_ntt), _p(small), ctypes.c_size_t(small.shape[0]),
+    lib().or_sns_squash(ctypes.byref(sp), _p(keys.bsk_limb), _p(small), ctypes.c_size_t(small.shape[0]),
                         ctypes.c_uint32(msg_modulus), _p(out), ctypes.c_int(threads))
     return out
 
 
 def sns_blind_rotate(sp: SnsParams, keys: SnsKeys, small: np.ndarray, lut: np.ndarray) -> np.ndarray:
     acc = np.zeros((sp.k + 1, 2, sp.N), dtype=np.uint64)
-    lib().or_sns_blind_rotate(ctypes.byref(sp), _p(keys.bsk_ntt), _p(np.ascontiguousarray(small, dtype=np.uint64)),
+    lib().or_sns_blind_rotate(ctypes.byref(sp), _p(keys.bsk_limb), _p(np.ascontiguousarray(small, dtype=np.uint64)),
                               _p(np.ascontiguousarray(lut, dtype=np.uint64)), _p(acc))
     return acc
 

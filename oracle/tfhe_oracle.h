@@ -188,29 +188,31 @@ size_t or_pks_packed_words(const or_pks_params* pp, uint32_t bodies);
 void or_pks_compress(const or_pks_params* pp, const uint64_t* glwe, uint32_t bodies, uint64_t* packed);
 void or_pks_extract(const or_pks_params* pp, const uint64_t* packed, uint32_t bodies, uint64_t* glwe);
 
-/* ---- switch-and-squash / noise squashing to Z_2^128 (sns_oracle.c) --------------------------- */
+/* ---- switch-and-squash / noise squashing to Z_2^128 (sns_oracle.c): the native 2^128 torus --------
+ * Coefficients are Z_2^128 words held as two u64 planes per polynomial, [lo][N] then [hi][N]. */
 typedef struct or_sns_params {
   uint32_t n, k, N, base_log, level;
   int32_t noise_log2; /* Gaussian integer noise round(N(0,1) * 2^(64 + x)) added to 128-bit bodies */
 } or_sns_params;
+#define OR_SNS_LIMBS 7 /* balanced 16-bit limbs of a rounded key word (2^16 x a 112-bit integer) */
 int or_sns_params_preset(int preset, or_sns_params* out); /* 0: n=918 (P-FHEVM small key) k=2 N=2048 2^24x3 */
-uint64_t or_sns_prime(int which);                        /* 0: 2^64-2^32+1, 1: 2^64-2^34+1 */
+uint64_t or_sns_prime(int which);                        /* 0: 2^64-2^32+1 (the limb products), 1: 2^64-2^34+1 */
 uint64_t or_sns_psi(int which, uint32_t N);
 void or_sns_ntt_fwd(int which, uint64_t* a, uint32_t N);
 void or_sns_ntt_inv(int which, uint64_t* a, uint32_t N);
-size_t or_sns_bsk_len(const or_sns_params* sp);          /* n*(k+1)L*(k+1)*2*N: [i][c*L+l][j][prime][N] */
+size_t or_sns_bsk_len(const or_sns_params* sp);          /* n*(k+1)L*(k+1)*2*N: [i][c*L+l][j][lo, hi][N] */
 void or_sns_keygen(const or_sns_params* sp, uint64_t seed, const uint64_t* lwe_key, uint64_t* glwe_key /* k*N */,
                    uint64_t* bsk /* nullable */);
-/* load-time rounding of the squashing key to multiples of 2^16 (centred mod Q; sns_oracle.c) */
+/* load-time rounding of the squashing key to multiples of 2^16 (signed 128-bit words; sns_oracle.c) */
 void or_sns_bsk_round(const or_sns_params* sp, const uint64_t* bsk, uint64_t* out);
-void or_sns_bsk_to_ntt(const or_sns_params* sp, const uint64_t* bsk, uint64_t* bsk_ntt);
-void or_sns_tor_to_q(const uint64_t* t, uint64_t* r);
-void or_sns_q_to_tor(const uint64_t* r, uint64_t* t);
-void or_sns_lut_identity(const or_sns_params* sp, uint32_t msg_modulus, uint64_t* lut /* [prime][N] */);
-void or_sns_blind_rotate(const or_sns_params* sp, const uint64_t* bsk_ntt, const uint64_t* lwe_small,
-                         const uint64_t* lut, uint64_t* acc /* [(k+1)][prime][N] */);
+/* rounded key -> NTTs (mod prime 0) of its 7 signed 16-bit limb polynomials: [i][r][j][limb][N] */
+size_t or_sns_limb_ntt_len(const or_sns_params* sp);
+void or_sns_bsk_to_limb_ntt(const or_sns_params* sp, const uint64_t* rounded, uint64_t* out);
+void or_sns_lut_identity(const or_sns_params* sp, uint32_t msg_modulus, uint64_t* lut /* [lo, hi][N] */);
+void or_sns_blind_rotate(const or_sns_params* sp, const uint64_t* bsk_limb, const uint64_t* lwe_small,
+                         const uint64_t* lut, uint64_t* acc /* [(k+1)][lo, hi][N] */);
 void or_sns_sample_extract(const or_sns_params* sp, const uint64_t* acc, uint64_t* out /* (kN+1) x (lo,hi) */);
-void or_sns_squash(const or_sns_params* sp, const uint64_t* bsk_ntt, const uint64_t* lwe_small, size_t B,
+void or_sns_squash(const or_sns_params* sp, const uint64_t* bsk_limb, const uint64_t* lwe_small, size_t B,
                    uint32_t msg_modulus, uint64_t* out, int threads);
 void or_sns_phase(const or_sns_params* sp, const uint64_t* glwe_key, const uint64_t* cts, size_t count,
                   uint64_t* out);

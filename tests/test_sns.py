@@ -1,7 +1,8 @@
 """Switch-and-squash / noise squashing (tfhe_amd/sns.py) on CPU: product key
-generation and decryption against the oracle (oracle/sns_oracle.c), the oracle's Z_Q NTT against a
-schoolbook product, and the oracle pipeline end to end at the full parameter set (keyswitch ->
-modulus-switch noise reduction -> 128-bit bootstrap) decrypting every message with ~2^-63 noise."""
+generation and decryption against the oracle (oracle/sns_oracle.c), the oracle's limb-convolution NTT
+against a schoolbook product, the load-time key rounding and its limb split on the native 2^128 torus,
+and the oracle pipeline end to end at the full parameter set (keyswitch -> modulus-switch noise
+reduction -> 128-bit bootstrap) decrypting every message with ~2^-63 noise."""
 import numpy as np
 import pytest
 
@@ -66,33 +67,50 @@ def test_oracle_squash_end_to_end(oracle_mod):
     assert max(abs(e) for e in noise) < 2 ** 70      # squashed: ~2^65 of the 2^128 torus
 
 
-def test_key_rounding(oracle_mod):
-    """or_sns_bsk_round (the device's load-time rounding): every coefficient becomes the multiple of
-    2^16 nearest to its centred value mod Q, so a rounded key is 2^16 x a 112-bit integer (seven
-    balanced 16-bit limbs) and moves each coefficient by at most 2^15."""
+def _words(a):
+    """(lo, hi) planes [..][2][N] -> python ints [..][N]"""
+    a = a.reshape(-1, 2, a.shape[-1])
+    return [[int(lo) | (int(hi) << 64) for lo, hi in zip(p[0], p[1])] for p in a]
+
+
+def test_key_rounding_and_limbs(oracle_mod):
+    """or_sns_bsk_round (the device's load-time rounding): every key word, read as a signed 128-bit
+    integer, becomes the nearest multiple of 2^16 (moved by at most 2^15), so a rounded word is 2^16 x a
+    112-bit integer; the seven balanced 16-bit limbs of or_sns_bsk_to_limb_ntt recombine to it mod 2^128
+    (the inverse NTT of the limb spectra returns the signed limbs)."""
     import ctypes
     osp = oracle_mod.sns_params(0)
     osp.n = 1
     keys = oracle_mod.SnsKeys(osp, KEY_SEED, np.array([1], dtype=np.uint64))
     out = np.zeros_like(keys.bsk)
     oracle_mod.lib().or_sns_bsk_round(ctypes.byref(osp), oracle_mod._p(keys.bsk), oracle_mod._p(out))
-    p1, p2 = 0xFFFFFFFF00000001, 0xFFFFFFFC00000001
-    Q = p1 * p2
-    inv = pow(p1, -1, p2)
-
-    def crt(r1, r2):
-        return int(r1) + p1 * (((int(r2) - int(r1)) * inv) % p2)
-
-    pairs = keys.bsk.reshape(-1, 2, 2048)
-    rpairs = out.reshape(-1, 2, 2048)
+    words, rounded = _words(keys.bsk.reshape(-1, 2, 2048)), _words(out.reshape(-1, 2, 2048))
+    limb = keys.bsk_limb.reshape(-1, 7, 2048)
+    p1 = 0xFFFFFFFF00000001
     rng = np.random.default_rng(5)
-    for pp in rng.integers(0, pairs.shape[0], 6):
-        for t in rng.integers(0, 2048, 40):
-            x = crt(pairs[pp, 0, t], pairs[pp, 1, t])
-            y = crt(rpairs[pp, 0, t], rpairs[pp, 1, t])
-            xc = x - Q if x > Q // 2 else x
-            yc = y - Q if y > Q // 2 else y
-            assert yc % 65536 == 0 and abs(yc - xc) <= 32768 and abs(yc // 65536) < 2 ** 111
+    signed = lambda v: v - (1 << 128) if v >> 127 else v
+    for pp in rng.integers(0, len(words), 4):
+        lv = [oracle_mod.sns_ntt(0, limb[pp, t].copy(), inverse=True) for t in range(7)]
+        for t in list(rng.integers(0, 2048, 40)) + [0, 2047]:
+            x, y = signed(words[pp][t]), signed(rounded[pp][t])
+            assert y % 65536 == 0 and abs(y - x) <= 32768 and abs(y >> 16) < 2 ** 111
+            ls = [int(lv[u][t]) - p1 if int(lv[u][t]) > p1 // 2 else int(lv[u][t]) for u in range(7)]
+            assert all(abs(v) <= 32768 for v in ls)
+            assert sum(v << (16 + 16 * u) for u, v in enumerate(ls)) % (1 << 128) == rounded[pp][t]
+
+
+def test_lut_identity_native(oracle_mod):
+    """The oracle's identity LUT on the 2^128 torus (one padding bit, delta = 2^127 / 16, half-box
+    rotation: coefficient i holds the message of box (i + box/2) / box, the wrapped half negated); the
+    device's copy (client library) is checked through the accumulators of tests/test_gpu_sns.py."""
+    osp = oracle_mod.sns_params(0)
+    w = _words(oracle_mod.sns_lut_identity(osp, 16).reshape(1, 2, 2048))[0]
+    box, delta = 2048 // 16, (1 << 127) // 16
+    for i in range(2048):
+        src = i + box // 2
+        want = (src // box) * delta if src < 2048 else (-(((src - 2048) // box) * delta)) % (1 << 128)
+        assert w[i] == want
+    assert w[box // 2] == delta and w[2047 - box // 2] == 15 * delta
 
 
 def test_fft_limb_product_exactness(tmp_path):

@@ -379,67 +379,24 @@ void pks_extract(const tfhe_pks_params& pp, const uint64_t* packed, uint32_t bod
   }
 }
 
-// ------------------------------------------------------------ noise squashing (128-bit GLWE over Z_Q)
-// Q = p1 * p2, p1 = 2^64 - 2^32 + 1, p2 = 2^64 - 2^34 + 1; keys as residues (see sns.hip).
+// ------------------------------------------------------------ noise squashing (128-bit GLWE, native 2^128 torus)
+// Words of Z_2^128 as two u64 planes per polynomial ([lo][N] then [hi][N]); oracle/sns_oracle.c is the rule.
 typedef unsigned __int128 u128;
-static const uint64_t SNS_P[2] = {0xFFFFFFFF00000001ull, 0xFFFFFFFC00000001ull};
-
-static inline uint64_t smul(uint64_t a, uint64_t b, uint64_t p) { return (uint64_t)(((u128)a * b) % p); }
-static inline uint64_t sadd(uint64_t a, uint64_t b, uint64_t p) {
-  const u128 s = (u128)a + b;
-  return (uint64_t)(s >= p ? s - p : s);
-}
-static uint64_t spow(uint64_t a, uint64_t e, uint64_t p) {
-  uint64_t r = 1;
-  for (; e; e >>= 1, a = smul(a, a, p))
-    if (e & 1) r = smul(r, a, p);
-  return r;
-}
-// negacyclic product helper: cyclic NTT with psi twist (any exact method gives the same product)
-static void sns_host_ntt(std::vector<uint64_t>& a, uint64_t p, bool inverse) {
-  const uint32_t N = (uint32_t)a.size();
-  uint64_t nr = 2;
-  while (spow(nr, (p - 1) / 2, p) != p - 1) nr++;
-  uint64_t psi = spow(nr, (p - 1) / (2ull * N), p);
-  if (inverse) psi = spow(psi, p - 2, p);
-  if (!inverse) {
-    uint64_t t = 1;
-    for (uint32_t i = 0; i < N; i++, t = smul(t, psi, p)) a[i] = smul(a[i], t, p);
-  }
-  for (uint32_t i = 1, j = 0; i < N; i++) {
-    uint32_t bit = N >> 1;
-    for (; j & bit; bit >>= 1) j ^= bit;
-    j ^= bit;
-    if (i < j) std::swap(a[i], a[j]);
-  }
-  const uint64_t w = smul(psi, psi, p);
-  for (uint32_t len = 2; len <= N; len <<= 1) {
-    const uint64_t wl = spow(w, N / len, p);
-    for (uint32_t i = 0; i < N; i += len) {
-      uint64_t wn = 1;
-      for (uint32_t j = 0; j < len / 2; j++, wn = smul(wn, wl, p)) {
-        const uint64_t u = a[i + j], v = smul(a[i + j + len / 2], wn, p);
-        a[i + j] = sadd(u, v, p);
-        a[i + j + len / 2] = u >= v ? u - v : u + (p - v);
-      }
-    }
-  }
-  if (inverse) {
-    uint64_t t = spow(N, p - 2, p);
-    for (uint32_t i = 0; i < N; i++, t = smul(t, psi, p)) a[i] = smul(a[i], t, p);
-  }
-}
 
 size_t sns_bsk_len(const tfhe_sns_params& sp) {
   return (size_t)sp.n * (sp.k + 1) * sp.level * (sp.k + 1) * 2 * sp.N;
 }
 
-static u128 sns_gadget(uint32_t shift) {
-  const u128 Q = (u128)SNS_P[0] * SNS_P[1];
-  return (Q >> shift) + ((Q >> (shift - 1)) & 1);
+static inline u128 sns_ld(const uint64_t* plane, size_t N, size_t t) { return ((u128)plane[N + t] << 64) | plane[t]; }
+static inline void sns_st(uint64_t* plane, size_t N, size_t t, u128 v) {
+  plane[t] = (uint64_t)v;
+  plane[N + t] = (uint64_t)(v >> 64);
 }
 
-// GLWE key from ChaCha stream 5; BSK row i from stream 0x400000 + i; layout [i][c*L+l][j][prime][N]
+// GLWE key from ChaCha stream 5; BSK row i from stream 0x400000 + i: masks uniform over Z_2^128 (lo word, then hi
+// word, per coefficient), one Gaussian integer per body coefficient, body = sum_j mask_j (*) S_j + e (exact
+// negacyclic products mod 2^128: the binary key's set bits add rotated masks), s_i 2^(128 - B (l + 1)) on
+// coefficient 0 of component c.  Layout [i][c*L+l][j][lo, hi][N].
 void sns_keygen(const tfhe_sns_params& sp, const tfhe_rng_key& rk, const uint64_t* lwe_key, uint64_t* glwe_key, uint64_t* bsk) {
   const uint32_t k = sp.k, N = sp.N, L = sp.level;
   {
@@ -447,74 +404,48 @@ void sns_keygen(const tfhe_sns_params& sp, const tfhe_rng_key& rk, const uint64_
     for (uint32_t i = 0; i < k * N; i++) glwe_key[i] = r.next() & 1;
   }
   if (!bsk) return;
-  std::vector<std::vector<uint64_t>> skey(2 * k);
-  for (int q = 0; q < 2; q++)
-    for (uint32_t c = 0; c < k; c++) {
-      skey[q * k + c].assign(glwe_key + (size_t)c * N, glwe_key + (size_t)(c + 1) * N);
-      sns_host_ntt(skey[q * k + c], SNS_P[q], false);
-    }
+  // set-bit lists of the key polynomials
+  std::vector<std::vector<uint32_t>> bits(k);
+  for (uint32_t j = 0; j < k; j++)
+    for (uint32_t u = 0; u < N; u++)
+      if (glwe_key[(size_t)j * N + u]) bits[j].push_back(u);
   const size_t row = (size_t)(k + 1) * 2 * N, per_i = (size_t)(k + 1) * L * row;
   parallel_for((int64_t)sp.n, [&](int64_t i) {
     ChaCha r(rk, 0x400000 + (uint64_t)i);
-    std::vector<uint64_t> tmp(N), acc(N);
-    std::vector<int64_t> e(N);
+    std::vector<u128> body(N), mask(N);
     for (uint32_t c = 0; c <= k; c++)
       for (uint32_t l = 0; l < L; l++) {
         uint64_t* out = bsk + per_i * i + row * (c * L + l);
         for (uint32_t j = 0; j < k; j++)
-          for (int q = 0; q < 2; q++)
-            for (uint32_t t = 0; t < N; t++) {
-              uint64_t v;
-              do v = r.next(); while (v >= SNS_P[q]);
-              out[((size_t)j * 2 + q) * N + t] = v;
-            }
-        for (uint32_t t = 0; t < N; t++) e[t] = r.gauss(sp.noise_log2);
-        for (int q = 0; q < 2; q++) {
-          const uint64_t p = SNS_P[q];
-          std::fill(acc.begin(), acc.end(), 0);
-          for (uint32_t j = 0; j < k; j++) {
-            std::copy(out + ((size_t)j * 2 + q) * N, out + ((size_t)j * 2 + q + 1) * N, tmp.begin());
-            sns_host_ntt(tmp, p, false);
-            const auto& s = skey[q * k + j];
-            for (uint32_t t = 0; t < N; t++) acc[t] = sadd(acc[t], smul(tmp[t], s[t], p), p);
-          }
-          sns_host_ntt(acc, p, true);
-          uint64_t* body = out + ((size_t)k * 2 + q) * N;
           for (uint32_t t = 0; t < N; t++) {
-            const uint64_t ev = e[t] >= 0 ? (uint64_t)e[t] % p : p - ((uint64_t)(-e[t]) % p);
-            body[t] = sadd(acc[t], ev, p);
+            const uint64_t lo = r.next(), hi = r.next();
+            sns_st(out + (size_t)j * 2 * N, N, t, ((u128)hi << 64) | lo);
           }
-          if (lwe_key[i]) {
-            const u128 g = sns_gadget(sp.base_log * (l + 1));
-            uint64_t* dst = out + ((size_t)c * 2 + q) * N;
-            dst[0] = sadd(dst[0], (uint64_t)(g % p), p);
+        for (uint32_t t = 0; t < N; t++) body[t] = (u128)(__int128)r.gauss(sp.noise_log2);
+        for (uint32_t j = 0; j < k; j++) {
+          for (uint32_t t = 0; t < N; t++) mask[t] = sns_ld(out + (size_t)j * 2 * N, N, t);
+          for (const uint32_t u : bits[j]) {
+            for (uint32_t x = 0; x < u; x++) body[x] -= mask[x + N - u];
+            for (uint32_t x = u; x < N; x++) body[x] += mask[x - u];
           }
+        }
+        for (uint32_t t = 0; t < N; t++) sns_st(out + (size_t)k * 2 * N, N, t, body[t]);
+        if (lwe_key[i]) {
+          uint64_t* dst = out + (size_t)c * 2 * N;
+          sns_st(dst, N, 0, sns_ld(dst, N, 0) + ((u128)1 << (128 - sp.base_log * (l + 1))));
         }
       }
   });
 }
 
-// torus (u128) -> Z_Q: t - round(t * (2^128 - Q) / 2^128)
-static u128 mulhi128(u128 x, u128 y) {
-  const uint64_t x0 = (uint64_t)x, x1 = (uint64_t)(x >> 64), y0 = (uint64_t)y, y1 = (uint64_t)(y >> 64);
-  const u128 p00 = (u128)x0 * y0, p01 = (u128)x0 * y1, p10 = (u128)x1 * y0, p11 = (u128)x1 * y1;
-  const u128 mid = (p00 >> 64) + (uint64_t)p01 + (uint64_t)p10;
-  return p11 + (p01 >> 64) + (p10 >> 64) + (mid >> 64);
-}
-
-// identity LUT over msg_modulus values (delta = 2^127 / msg_modulus, half-box rotation): [prime][N]
+// identity LUT over msg_modulus values (delta = 2^127 / msg_modulus, half-box rotation): [lo, hi][N]
 void sns_lut_identity(const tfhe_sns_params& sp, uint32_t msg_modulus, uint64_t* lut) {
   const uint32_t N = sp.N, box = N / msg_modulus;
-  const u128 delta = ((u128)1 << 127) / msg_modulus, d = (u128)0 - (u128)SNS_P[0] * SNS_P[1];
+  const u128 delta = ((u128)1 << 127) / msg_modulus;
   for (uint32_t i = 0; i < N; i++) {
     const uint32_t src = i + box / 2;
     const u128 t = (u128)((src < N ? src : src - N) / box) * delta;
-    const u128 lo = t * d;
-    const u128 v = t - (mulhi128(t, d) + ((lo >> 127) & 1));
-    for (int q = 0; q < 2; q++) {
-      const uint64_t r = (uint64_t)(v % SNS_P[q]);
-      lut[(size_t)q * N + i] = (src < N || r == 0) ? r : SNS_P[q] - r;
-    }
+    sns_st(lut, N, i, src < N ? t : (u128)0 - t);
   }
 }
 

@@ -29,7 +29,7 @@ void glwe_phase_native(uint32_t k, uint32_t N, const uint64_t* key, const uint64
 size_t pks_packed_words(const tfhe_pks_params& pp, uint32_t bodies);
 void pks_compress(const tfhe_pks_params& pp, const uint64_t* glwe, uint32_t bodies, uint64_t* packed);
 void pks_extract(const tfhe_pks_params& pp, const uint64_t* packed, uint32_t bodies, uint64_t* glwe);
-// noise squashing (128-bit GLWE over Z_Q, residues mod p1, p2)
+// noise squashing (128-bit GLWE over the native 2^128 torus, words as (lo, hi) planes)
 size_t sns_bsk_len(const tfhe_sns_params& sp);
 void sns_keygen(const tfhe_sns_params& sp, const tfhe_rng_key& rk, const uint64_t* lwe_key, uint64_t* glwe_key, uint64_t* bsk);
 void sns_lut_identity(const tfhe_sns_params& sp, uint32_t msg_modulus, uint64_t* lut);

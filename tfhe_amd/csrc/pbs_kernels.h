@@ -63,24 +63,19 @@ hipError_t launch_blind_rotate_2048(const u64* lwe_in, size_t B, int n, const u6
                                    hipStream_t s, size_t latency_max_batch = 0);
 hipError_t launch_sample_extract_2048(const u64* acc, size_t B, u64* out, hipStream_t s);
 hipError_t launch_ntt2048_fwd(u64* polys, size_t count, const u64* tw, hipStream_t s);
-// noise squashing (sns.hip); d_const: device copy of make_sns_const()
-size_t sns_const_bytes();
-void make_sns_const(void* out);
-hipError_t launch_sns_bsk_to_ntt(const u64* bsk_std, u64* bsk_ntt, size_t polys, const void* d_const, hipStream_t s);
-hipError_t launch_sns_blind_rotate(const u64* lwe, size_t B, int n, const u64* lut, const u64* bsk_ntt, u64* acc,
-                                   u64* D, const void* d_const, hipStream_t s);
-hipError_t launch_sns_extract(const u64* acc, size_t B, u64* out, const void* d_const, hipStream_t s);
-// the f64 FFT external product (default path; sns_fft.h): d_fconst = device copy of make_sns_fft_const()
+// noise squashing on the native 2^128 torus (sns.hip; sns_fft.h): d_fconst = device copy of
+// make_sns_fft_const(); words as (lo, hi) planes per polynomial
 size_t sns_fft_const_bytes();
 void make_sns_fft_const(void* out);
-size_t sns_fft_key_len(size_t n);  // key spectra, in 16-byte complex
-constexpr size_t SNS_FFT_PAIR_BYTES = 7 * 1024 * 16;  // limb spectra of one (i, r, j) pair
-hipError_t launch_sns_bsk_to_fft(const u64* bsk_std, void* bsk_fft, size_t pairs, const void* d_const,
-                                 const void* d_fconst, hipStream_t s);
+size_t sns_fft_key_len(size_t n);  // key limb spectra, in 16-byte complex
+size_t sns_digit_len(size_t B);    // digit spectra workspace, in 16-byte complex
 size_t sns_fft_prod_len(size_t B);  // MAC product workspace, in 16-byte complex
-hipError_t launch_sns_blind_rotate_fft(const u64* lwe, size_t B, int n, const u64* lut, const void* bsk_fft, u64* acc,
-                                       void* D, void* Oprod, const void* d_const, const void* d_fconst,
-                                       hipStream_t s);
+constexpr size_t SNS_FFT_POLY_BYTES = 7 * 1024 * 16;  // limb spectra of one (i, r, j) key polynomial
+hipError_t launch_sns_bsk_to_fft(const u64* bsk_std, void* bsk_fft, size_t polys, const void* d_fconst,
+                                 hipStream_t s);
+hipError_t launch_sns_blind_rotate(const u64* lwe, size_t B, int n, const u64* lut, const void* bsk_fft, u64* acc,
+                                   void* D, void* Oprod, const void* d_fconst, hipStream_t s);
+hipError_t launch_sns_extract(const u64* acc, size_t B, u64* out, hipStream_t s);
 // packing keyswitch (pks.hip)
 hipError_t launch_pks_corr(const u64* pksk, int K, int Nc, int base_log, u64* corr, hipStream_t s);
 hipError_t launch_pks_pack(const u64* lwes, size_t count, int in_dim, int base_log, int L, int k, int N, int lpg,

@@ -37,7 +37,7 @@ int fail(int code, const char* fmt, ...) {
                   hipGetErrorString(_e), __FILE__, __LINE__);                                            \
   } while (0)
 
-// the device kernels of this build: k = 2, N = 2048, 2^24 x 3 (any n)
+// the device kernels of this build: k = 2, N = 2048, 2^24 x 3 (any n), words over Z_2^128
 bool sns_valid(const tfhe_sns_params* sp) {
   return sp && sp->n > 0 && sp->k == 2 && sp->N == 2048 && sp->base_log == 24 && sp->level == 3 &&
          sp->noise_log2 < 0 && sp->noise_log2 > -64;
@@ -55,8 +55,8 @@ struct DevGuard {
   }
 };
 
-// ciphertexts per pass (acc 96 KB + digit spectra 147-288 KB + FFT products 344 KB each);
-// TFHE_HIP_SNS_CHUNK overrides (the FFT path's per-CMUX working set is ~0.5 MB per ciphertext)
+// ciphertexts per pass (acc 96 KB + digit spectra 147 KB + MAC products 344 KB each);
+// TFHE_HIP_SNS_CHUNK overrides
 size_t sns_chunk() {
   static const size_t v = [] {
     const char* e = getenv("TFHE_HIP_SNS_CHUNK");
@@ -72,15 +72,12 @@ struct tfhe_sns_ctx {
   tfhe_sns_params sp{};
   int device = 0;
   hipStream_t stream = nullptr;
-  void* d_const = nullptr;
   void* d_fconst = nullptr;
-  bool ntt = false;        // TFHE_HIP_SNS_NTT=1 at create: the Z_p NTT external product instead of the f64 FFT
-  u64* d_bsk = nullptr;    // NTT path: key in the NTT domain (n x 9 x 3 x 2 x N u64)
-  void* d_bskf = nullptr;  // FFT path: key limb spectra (n x 9 x 3 x 7 x 1024 complex f64)
+  void* d_bskf = nullptr;  // key limb spectra (n x 9 x 3 x 7 x 1024 complex f64)
   bool key = false;
-  u64* d_acc = nullptr;
-  u64* d_D = nullptr;
-  void* d_O = nullptr;  // FFT path: MAC products (chunk x 21 x 1024 complex)
+  u64* d_acc = nullptr;    // chunk x 3 x (lo, hi) x N
+  void* d_D = nullptr;     // digit spectra (chunk x 9 x 1024 complex)
+  void* d_O = nullptr;     // MAC products (chunk x 21 x 1024 complex)
   u64* d_lut = nullptr;
   uint32_t lut_mm = 0;
   size_t ws_cap = 0;
@@ -96,13 +93,13 @@ int ensure_ws(tfhe_sns_ctx* c, size_t B) {
   (void)hipFree(c->d_acc);
   (void)hipFree(c->d_D);
   (void)hipFree(c->d_O);
-  c->d_acc = c->d_D = nullptr;
-  c->d_O = nullptr;
+  c->d_acc = nullptr;
+  c->d_D = c->d_O = nullptr;
   c->ws_cap = 0;
   const size_t poly = 2 * (size_t)c->sp.N;
   SNS_TRY(hipMalloc(&c->d_acc, B * (c->sp.k + 1) * poly * 8));
-  SNS_TRY(hipMalloc(&c->d_D, B * (c->sp.k + 1) * c->sp.level * poly * 8));
-  if (!c->ntt) SNS_TRY(hipMalloc(&c->d_O, tfhe::sns_fft_prod_len(B) * 16));
+  SNS_TRY(hipMalloc(&c->d_D, tfhe::sns_digit_len(B) * 16));
+  SNS_TRY(hipMalloc(&c->d_O, tfhe::sns_fft_prod_len(B) * 16));
   c->ws_cap = B;
   return 0;
 }
@@ -126,13 +123,9 @@ int run_device(tfhe_sns_ctx* c, const u64* d_in, size_t B, u64* d_out, u64* d_ac
   const size_t acc_len = (size_t)(c->sp.k + 1) * 2 * c->sp.N;
   for (size_t f = 0; f < B; f += chunk) {
     const size_t nb = std::min(chunk, B - f);
-    if (c->ntt)
-      SNS_TRY(tfhe::launch_sns_blind_rotate(d_in + f * in_dim, nb, (int)c->sp.n, c->d_lut, c->d_bsk, c->d_acc,
-                                            c->d_D, c->d_const, s));
-    else
-      SNS_TRY(tfhe::launch_sns_blind_rotate_fft(d_in + f * in_dim, nb, (int)c->sp.n, c->d_lut, c->d_bskf, c->d_acc,
-                                                c->d_D, c->d_O, c->d_const, c->d_fconst, s));
-    if (d_out) SNS_TRY(tfhe::launch_sns_extract(c->d_acc, nb, d_out + f * out_dim, c->d_const, s));
+    SNS_TRY(tfhe::launch_sns_blind_rotate(d_in + f * in_dim, nb, (int)c->sp.n, c->d_lut, c->d_bskf, c->d_acc, c->d_D,
+                                          c->d_O, c->d_fconst, s));
+    if (d_out) SNS_TRY(tfhe::launch_sns_extract(c->d_acc, nb, d_out + f * out_dim, s));
     if (d_acc_out)
       SNS_TRY(hipMemcpyAsync(d_acc_out + f * acc_len, c->d_acc, nb * acc_len * 8, hipMemcpyDeviceToDevice, s));
   }
@@ -208,14 +201,9 @@ int tfhe_hip_sns_create(const tfhe_sns_params* sp, int device, tfhe_sns_ctx** ou
   tfhe_sns_ctx* c = new tfhe_sns_ctx();
   c->sp = *sp;
   c->device = device;
-  const char* e = getenv("TFHE_HIP_SNS_NTT");
-  c->ntt = e && e[0] == '1';
-  std::vector<unsigned char> K(tfhe::sns_const_bytes()), F(tfhe::sns_fft_const_bytes());
-  tfhe::make_sns_const(K.data());
+  std::vector<unsigned char> F(tfhe::sns_fft_const_bytes());
   tfhe::make_sns_fft_const(F.data());
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&c->d_const, K.size()) != hipSuccess ||
-      hipMemcpy(c->d_const, K.data(), K.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMalloc(&c->d_fconst, F.size()) != hipSuccess ||
       hipMemcpy(c->d_fconst, F.data(), F.size(), hipMemcpyHostToDevice) != hipSuccess) {
     tfhe_hip_sns_destroy(c);
@@ -230,8 +218,7 @@ void tfhe_hip_sns_destroy(tfhe_sns_ctx* c) {
   {
     DevGuard g(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (void* p : {(void*)c->d_const, c->d_fconst, (void*)c->d_bsk, c->d_bskf, (void*)c->d_acc, (void*)c->d_D,
-                    c->d_O, (void*)c->d_lut, (void*)c->d_io})
+    for (void* p : {c->d_fconst, c->d_bskf, (void*)c->d_acc, c->d_D, c->d_O, (void*)c->d_lut, (void*)c->d_io})
       (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
   }
@@ -245,11 +232,10 @@ int tfhe_hip_sns_load_key(tfhe_sns_ctx* c, const uint64_t* bsk, size_t len) {
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
   c->key = false;
-  if (c->ntt && !c->d_bsk) SNS_TRY(hipMalloc(&c->d_bsk, len * 8));
-  if (!c->ntt && !c->d_bskf) SNS_TRY(hipMalloc(&c->d_bskf, tfhe::sns_fft_key_len(c->sp.n) * 16));
-  // stage the standard-domain key in chunks through the io buffer, convert in place
-  const size_t polys = len / c->sp.N, per = 4096;
-  const size_t bytes = per * c->sp.N * 8;
+  if (!c->d_bskf) SNS_TRY(hipMalloc(&c->d_bskf, tfhe::sns_fft_key_len(c->sp.n) * 16));
+  // stage the key words in chunks of polynomials (lo, hi planes) through the io buffer, convert to limb spectra
+  const size_t poly_words = 2 * (size_t)c->sp.N, polys = len / poly_words, per = 2048;
+  const size_t bytes = per * poly_words * 8;
   if (c->io_cap < bytes) {
     (void)hipFree(c->d_io);
     c->d_io = nullptr;
@@ -259,12 +245,10 @@ int tfhe_hip_sns_load_key(tfhe_sns_ctx* c, const uint64_t* bsk, size_t len) {
   }
   for (size_t f = 0; f < polys; f += per) {
     const size_t np = std::min(per, polys - f);
-    SNS_TRY(hipMemcpyAsync(c->d_io, bsk + f * c->sp.N, np * c->sp.N * 8, hipMemcpyHostToDevice, c->stream));
-    if (c->ntt)
-      SNS_TRY(tfhe::launch_sns_bsk_to_ntt(c->d_io, c->d_bsk + f * c->sp.N, np, c->d_const, c->stream));
-    else  // np is even (pairs of primes never straddle a chunk): 7 limb spectra per pair
-      SNS_TRY(tfhe::launch_sns_bsk_to_fft(c->d_io, (char*)c->d_bskf + (f / 2) * tfhe::SNS_FFT_PAIR_BYTES, np / 2,
-                                          c->d_const, c->d_fconst, c->stream));
+    SNS_TRY(hipMemcpyAsync(c->d_io, bsk + f * poly_words, np * poly_words * 8, hipMemcpyHostToDevice, c->stream));
+    SNS_TRY(tfhe::launch_sns_bsk_to_fft(c->d_io, (char*)c->d_bskf + f * tfhe::SNS_FFT_POLY_BYTES, np, c->d_fconst,
+                                        c->stream));
+    // the io buffer is reused by the next chunk's copy: same stream, ordered
   }
   SNS_TRY(hipStreamSynchronize(c->stream));
   c->key = true;

@@ -5,6 +5,8 @@ fhEVM's sns-worker (coprocessor-docker-compose.yml:124-140) squashes each 64-bit
 threshold decryption.  Here: `squash_noise(engine, squasher, cts)` = keyswitch to the small key and
 modulus-switch noise reduction on the P-FHEVM engine, then the 128-bit bootstrap with the identity
 LUT on the squasher; `SquashedKey.decrypt` recovers the message from the (k*N+1) x 128-bit LWE.
+The GLWE ring is the native 2^128 torus, as in tfhe-rs: a coefficient is one u128 word, held as
+(lo, hi) u64 pairs in the LWEs and as [lo][N], [hi][N] planes in keys and accumulators.
 """
 from __future__ import annotations
 
