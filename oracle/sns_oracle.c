@@ -202,8 +202,8 @@ void or_sns_bsk_round(const or_sns_params* sp, const uint64_t* bsk, uint64_t* ou
 #pragma omp parallel for schedule(static)
   for (size_t pp = 0; pp < planes; pp++)
     for (size_t t = 0; t < N; t++) {
-      const __int128 xc = (__int128)ld128(bsk + 2 * pp * N, N, t);
-      const __int128 rr = (xc + ((__int128)1 << 15)) >> 16; /* floor: arithmetic shift */
+      /* the add wraps mod 2^128 (a word within 2^15 of 2^127 rounds to -2^127: the same torus point) */
+      const __int128 rr = (__int128)(ld128(bsk + 2 * pp * N, N, t) + ((u128)1 << 15)) >> 16; /* floor: arithmetic shift */
       st128(out + 2 * pp * N, N, t, (u128)(rr * 65536));
     }
 }

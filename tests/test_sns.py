@@ -130,3 +130,20 @@ def test_fft_limb_product_exactness(tmp_path):
                 if l.startswith("trial")]
         assert len(errs) == 6
         assert all(e < 0.07 for mode, e in errs if mode != 2)
+
+
+def test_device_arithmetic_replay_matches_oracle(tmp_path):
+    """tools/sns_native_check.cpp replays the squash blind rotation on the host with the device's own
+    shared code (sns_fft.h: key rounding + limb split, 128-bit decomposition, Horner recombination, the
+    one-wave forward passes of step 1, the stage-form key / inverse transforms, the MAC order) and
+    compares every accumulator word with oracle/sns_oracle.c (exact Goldilocks limb NTTs): arbitrary
+    64-bit input words and a trivial-mask ciphertext at n = 24."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "sns_native_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", f"{root}/tfhe_amd/csrc", "-I", f"{root}/oracle",
+                    f"{root}/tools/sns_native_check.cpp", "-L", f"{root}/oracle", "-loracle",
+                    f"-Wl,-rpath,{root}/oracle", "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), "24", "3"], capture_output=True, text=True)
+    assert out.returncode == 0 and "OK: device arithmetic == oracle" in out.stdout, out.stdout + out.stderr

@@ -85,21 +85,12 @@ __global__ void __launch_bounds__(ST) sns_bsk_to_fft_kernel(const u64* __restric
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int x = threadIdx.x + 256 * u + SF_M * h;
-      const __int128 w = (__int128)ld128(pr, x);
-      rr[2 * u + h] = (w + ((__int128)1 << 15)) >> 16;  // nearest multiple of 2^16, ties up (arithmetic shift)
+      rr[2 * u + h] = snsf::key_round16(ld128(pr, x));
     }
   for (int t = 0; t < SF_LIMBS; t++) {
     double lv[8];
 #pragma unroll
-    for (int e = 0; e < 8; e++) {
-      if (t == SF_LIMBS - 1) {
-        lv[e] = (double)(long long)rr[e];  // the top limb keeps the remainder (|.| <= 2^15)
-      } else {
-        const __int128 l = ((rr[e] + 0x8000) & 0xFFFF) - 0x8000;
-        rr[e] = (rr[e] - l) >> 16;
-        lv[e] = (double)(long long)l;
-      }
-    }
+    for (int e = 0; e < 8; e++) lv[e] = (double)snsf::key_limb(rr[e], t == SF_LIMBS - 1);
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const int m = threadIdx.x + 256 * u;
@@ -136,18 +127,10 @@ __device__ __forceinline__ void step1_digits(const u64* __restrict__ lwe, int n,
     const u32 t1 = ((u32)t - ai) & 4095u;
     const int src = (int)(t1 & (u32)(SN - 1));
     const u128 v = ld128(a, src);
-    const u128 y = (t1 >= (u32)SN ? (u128)0 - v : v) - ld128(a, t);
-    u128 state = ((y >> 55) + 1) >> 1;
-    u64 lo = (u64)state, hi = (u64)(state >> 64) & 0xFFu;  // 72 bits
+    int d[SL];
+    snsf::digits72((t1 >= (u32)SN ? (u128)0 - v : v) - ld128(a, t), d);
 #pragma unroll
-    for (int l = SL - 1; l >= 0; l--) {
-      const u64 res = lo & 0xFFFFFFull;
-      lo = (lo >> 24) | (hi << 40);
-      hi >>= 24;
-      const u64 carry = ((((res - 1) | lo) & res) >> 23) & 1;
-      lo += carry;  // lo < 2^48 here: no carry into hi
-      dig[l][t] = (int)((long long)res - (long long)(carry << 24));
-    }
+    for (int l = 0; l < SL; l++) dig[l][t] = d[l];
   }
   __syncthreads();
 }
@@ -300,8 +283,8 @@ __global__ void __launch_bounds__(ST, 3) sns_inv_kernel(const cd* __restrict__ O
     for (int u = 0; u < 4; u++) {
       const int m = threadIdx.x + 256 * u;
       const cd y = snsf::cmulc(yr[u], F.P[m]);
-      h[2 * u] = (h[2 * u] << 16) + (u128)(__int128)(long long)__builtin_rint(y.x);
-      h[2 * u + 1] = (h[2 * u + 1] << 16) + (u128)(__int128)(long long)__builtin_rint(y.y);
+      h[2 * u] = snsf::horner16(h[2 * u], __builtin_rint(y.x));
+      h[2 * u + 1] = snsf::horner16(h[2 * u + 1], __builtin_rint(y.y));
     }
     __syncthreads();
   }

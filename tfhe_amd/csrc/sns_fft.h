@@ -1,13 +1,14 @@
-// sns_fft.h — the f64 negacyclic FFT of the noise-squashing external product (sns.hip),
-// shared by the device kernels and the host accuracy check (tools/sns_fft_check.cpp).
+// sns_fft.h — the f64 negacyclic FFT of the noise-squashing external product (sns.hip) and the
+// native 2^128 word arithmetic around it, shared by the device kernels and the host checks
+// (tools/sns_fft_check.cpp: FFT accuracy; tools/sns_native_check.cpp: the whole CMUX vs the oracle).
 //
-// The squashing ring is Z_Q (Q = p1 p2 ~ 2^128, see sns.hip).  Its product digits x BSK is computed as
-// EXACT integer convolutions: the BSK coefficient, centred in (-Q/2, Q/2] and rounded to a multiple of
-// 2^SF_DROP (the load-time rounding; oracle: or_sns_bsk_round), is split into SF_LIMBS balanced 16-bit
-// limbs, and each digit-polynomial x limb-polynomial convolution (|value| <= 9 * 2048 * 2^23 * 2^15 =
-// 2^52.2) is one f64 FFT product whose rounding error stays far below 1/2 (tools/sns_fft_check.cpp
-// measures it), so rint() returns the exact integer and the product mod Q is bit-identical to the
-// oracle's NTT over p1, p2.  The limbs recombine with the weights 2^(SF_DROP + 16 t) mod p.
+// The squashing ring is the native 2^128 torus.  Its product digits x BSK is computed as EXACT integer
+// convolutions: every BSK word, read as a signed 128-bit integer and rounded to a multiple of 2^16 (the
+// load-time rounding; oracle: or_sns_bsk_round), is split into SF_LIMBS balanced 16-bit limbs, and each
+// digit-polynomial x limb-polynomial convolution (|value| <= 9 * 2048 * 2^23 * 2^15 = 2^52.2) is one f64
+// FFT product whose rounding error stays far below 1/2 (tools/sns_fft_check.cpp measures it), so rint()
+// returns the exact integer; the limbs recombine as sum_t c_t 2^(16 + 16 t) mod 2^128 -- bit-identical to
+// the oracle's exact NTT limb products.
 //
 // Transform: N = 2048 real coefficients folded to M = 1024 complex z_m = (a_m + i a_{m+1024}) psi^m,
 // psi = e^{i pi / 2048} (so the cyclic DFT of z evaluates a at the odd powers of psi), then a radix-4
@@ -124,6 +125,40 @@ SF_HD void dit_pass10(cd (&x)[16], int t, const cd* T) {
   for (int k1 = 0; k1 < 4; k1++) r4_dit(x[4 * k1], x[4 * k1 + 1], x[4 * k1 + 2], x[4 * k1 + 3], 4 * t, T);
   for (int k2 = 0; k2 < 4; k2++) r4_dit(x[k2], x[4 + k2], x[8 + k2], x[12 + k2], t + 64 * k2, T);
 }
+
+// ---- native 2^128 words ---------------------------------------------------------------------------
+typedef unsigned __int128 w128;
+
+// load-time key rounding: the word as a signed integer, to the nearest multiple of 2^16 (ties up), / 2^16.
+// The add wraps mod 2^128, so a word within 2^15 of 2^127 rounds to -2^127: the same torus point.
+SF_HD __int128 key_round16(w128 w) { return (__int128)(w + ((w128)1 << 15)) >> 16; }
+
+// the next balanced 16-bit limb of a rounded key word (rr = word / 2^16, consumed from the bottom); the
+// top limb (t = SF_LIMBS - 1) keeps the remainder, |.| <= 2^15
+SF_HD long long key_limb(__int128& rr, bool top) {
+  if (top) return (long long)rr;
+  const __int128 l = ((rr + 0x8000) & 0xFFFF) - 0x8000;
+  rr = (rr - l) >> 16;
+  return (long long)l;
+}
+
+// tfhe-rs SignedDecomposer on a 128-bit word, 72 bits as 3 digits of 24 (gadget 2^(128 - 24 (l + 1)),
+// d[0] most significant): closest representable, then balanced digits with the tie carry rule
+SF_HD void digits72(w128 y, int (&d)[3]) {
+  const w128 state = ((y >> 55) + 1) >> 1;
+  unsigned long long lo = (unsigned long long)state, hi = (unsigned long long)(state >> 64) & 0xFFu;
+  for (int l = 2; l >= 0; l--) {
+    const unsigned long long res = lo & 0xFFFFFFull;
+    lo = (lo >> 24) | (hi << 40);
+    hi >>= 24;
+    const unsigned long long carry = ((((res - 1) | lo) & res) >> 23) & 1;
+    lo += carry;  // lo < 2^48 after the first shift: no carry into hi
+    d[l] = (int)((long long)res - (long long)(carry << 24));
+  }
+}
+
+// one Horner step over the limbs (top limb first): h = sum_t c_t 2^(16 t) mod 2^128; acc += h << 16
+SF_HD w128 horner16(w128 h, double c_rounded) { return (h << 16) + (w128)(__int128)(long long)c_rounded; }
 
 }  // namespace snsf
 }  // namespace tfhe
