@@ -30,11 +30,12 @@ function lin(terms, c, dim) {
 
 class Circuit {
   /** engine: { params: {n}, gateLut(), async pbs(cts: BigUint64Array, lut) } */
-  constructor(engine, capacity = 2048) {
+  constructor(engine, capacity = 2048, roundSize = 1024) {
     this.engine = engine;
     this.dim = engine.params.n + 1;
     this.lut = engine.gateLut();
     this.capacity = capacity;
+    this.roundSize = roundSize;  // PBS per batch-kernel round: the carry-out circuit's cost model
     this.pbsCount = 0;
     this.launches = 0;
   }
@@ -95,6 +96,33 @@ class Circuit {
   }
 
   preferPrefix(B, w) { return B * w * 2 <= this.capacity; }
+
+  /** block size of carryOut with the fewest launch rounds, then the fewest PBS (tfhe_amd/integer.py twin) */
+  carryBlock(B, w) {
+    const cands = new Set([w]);
+    for (let s = 1; s <= w; s *= 2) cands.add(s);
+    let best = null;
+    for (const s of [...cands].sort((x, y) => x - y)) {
+      const lv = carryLevels(B, w, s);
+      const key = [lv.reduce((t, n) => t + Math.max(1, Math.ceil(n / this.roundSize)), 0), lv.reduce((t, n) => t + n, 0), -s];
+      if (best === null || key[0] < best[0][0] || (key[0] === best[0][0] && (key[1] < best[0][1] ||
+          (key[1] === best[0][1] && key[2] < best[0][2])))) best = [key, s];
+    }
+    return best[1];
+  }
+}
+
+/** PBS per launch of carryOut(width w, block size s) over a batch of B */
+function carryLevels(B, w, s) {
+  const nb = Math.ceil(w / s);
+  const lv = [];
+  for (let j = 0; j < s; j++) {
+    let act = 0;
+    for (let k = 1; k < nb; k++) if (k * s + j < w) act++;
+    lv.push(B * (1 + 2 * act));
+  }
+  for (let n = nb; n > 1; n -= Math.floor(n / 2)) lv.push(B * (1 + 2 * (Math.floor(n / 2) - 1)));
+  return lv;
 }
 
 /** an encrypted batch: B values of width w, columns LSB first */
@@ -158,8 +186,49 @@ function* gBitwise(c, kind, a, b) {
   return yield a.map((x, i) => gate(x, b[i]));
 }
 
+/** carry-out of a + b + cin in blocks of s bits: block ripple in lockstep (block 0 from the known carry-in,
+ * blocks k >= 1 for both carry-ins G / P), then a reduction tree of (G, P) merges onto block 0 */
+function* carryOut(c, a, b, B, cin, s) {
+  const w = a.length, nb = Math.ceil(w / s);
+  let C = c.trivialConst(cin, B);
+  let G = [], P = [];
+  for (let j = 0; j < s; j++) {
+    const ks = [];
+    for (let k = 1; k < nb; k++) if (k * s + j < w) ks.push(k);
+    const m = ks.length;
+    const lvl = [c.MAJ(a[j], b[j], C)];
+    if (j === 0) {
+      for (const k of ks) lvl.push(c.AND(a[k * s], b[k * s]));
+      for (const k of ks) lvl.push(c.OR(a[k * s], b[k * s]));
+    } else {
+      ks.forEach((k, i) => lvl.push(c.MAJ(a[k * s + j], b[k * s + j], G[i])));
+      ks.forEach((k, i) => lvl.push(c.MAJ(a[k * s + j], b[k * s + j], P[i])));
+    }
+    const out = yield lvl;
+    C = out[0];
+    G = out.slice(1, 1 + m).concat(G.slice(m));
+    P = out.slice(1 + m, 1 + 2 * m).concat(P.slice(m));
+  }
+  while (G.length > 0) {
+    const n = G.length + 1, np = Math.floor(n / 2) - 1;
+    const lvl = [c.MAJ(G[0], P[0], C)];
+    for (let i = 1; i <= np; i++) lvl.push(c.MAJ(G[2 * i], P[2 * i], G[2 * i - 1]));
+    for (let i = 1; i <= np; i++) lvl.push(c.MAJ(G[2 * i], P[2 * i], P[2 * i - 1]));
+    const out = yield lvl;
+    C = out[0];
+    const nG = out.slice(1, 1 + np), nP = out.slice(1 + np, 1 + 2 * np);
+    if (n % 2) { nG.push(G[n - 2]); nP.push(P[n - 2]); }
+    G = nG; P = nP;
+  }
+  return C;
+}
+
 function* gAdd(c, a, b, B, cin = false, wantSum = true, wantCarry = false, prefix = null) {
   const w = a.length;
+  if (!wantSum) {
+    const s = prefix === null ? c.carryBlock(B, w) : (prefix ? 1 : w);
+    return [null, yield* carryOut(c, a, b, B, cin, s)];
+  }
   if (prefix === null) prefix = c.preferPrefix(B, w);
   if (!prefix) {
     let carry = c.trivialConst(cin, B);
@@ -177,17 +246,6 @@ function* gAdd(c, a, b, B, cin = false, wantSum = true, wantCarry = false, prefi
   }
   const gp = yield a.map((x, i) => c.AND(x, b[i])).concat(a.map((x, i) => c.OR(x, b[i])));
   let G = gp.slice(0, w), P = gp.slice(w);
-  if (!wantSum) {
-    while (G.length > 1) {
-      if (G.length % 2) { G = G.concat([c.trivialConst(false, B)]); P = P.concat([c.trivialConst(true, B)]); }
-      const lvl = [];
-      for (let k = 0; k < G.length; k += 2) lvl.push(c.MAJ(G[k + 1], P[k + 1], G[k]));
-      for (let k = 0; k < G.length; k += 2) lvl.push(c.MAJ(G[k + 1], P[k + 1], P[k]));
-      const out = yield lvl;
-      G = out.slice(0, lvl.length / 2); P = out.slice(lvl.length / 2);
-    }
-    return [null, cin ? P[0] : G[0]];
-  }
   for (let d = 1; d < w; d *= 2) {
     const lvl = [];
     for (let i = d; i < w; i++) lvl.push(c.MAJ(G[i], P[i], G[i - d]));

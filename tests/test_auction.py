@@ -84,3 +84,36 @@ def test_max_tree_gloo_world2():
     c = I.Circuit(CleartextEngine())
     max_tree(c, I.FheUint.trivial(c, _bids(64, seed=11), 32))
     assert max(r[3] for r in res) < c.pbs_count
+
+
+def test_max_tree_launch_shape():
+    """The comparisons' carry-out runs as a block ripple + reduction tree sized by the circuit's cost
+    model (tfhe_amd.integer._carry_out): 69 launches for the 256-bidder tree instead of the ripple's 116
+    (level 1: 8 chain steps of 896 PBS + 2 tree levels instead of 32 steps of 128)."""
+    c = I.Circuit(CleartextEngine())
+    sizes = []
+    pbs = c.engine.pbs
+    c.engine.pbs = lambda x, lut, *a, **k: (sizes.append(x.shape[0]), pbs(x, lut, *a, **k))[1]
+    v = _bids(256)
+    mx, idx = max_tree(c, I.FheUint.trivial(c, v, 32))
+    assert (int(mx.decrypt(ClearKey())[0]), int(idx.decrypt(ClearKey())[0])) == _expected(v)
+    assert c.launches == len(sizes) == 69
+    assert sizes[:10] == [896] * 8 + [384, 128]
+    assert [c.carry_block(B, 32) for B in (128, 64, 32, 1)] == [8, 4, 2, 2]
+
+
+def test_carry_out_every_block_size():
+    """_carry_out at every block size (ragged last blocks included) equals a >= b on random and edge operands."""
+    rng = np.random.default_rng(11)
+    for w in (1, 5, 8, 13, 32):
+        a = rng.integers(0, 1 << w, 40, dtype=np.uint64)
+        b = rng.integers(0, 1 << w, 40, dtype=np.uint64)
+        b[:6] = a[:6]
+        a[6], b[6] = 0, (1 << w) - 1
+        a[7], b[7] = (1 << w) - 1, 0
+        for s in range(1, w + 1):
+            c = I.Circuit(CleartextEngine())
+            A, Bv = I.FheUint.trivial(c, a, w).bits, I.FheUint.trivial(c, b, w).bits
+            cout = c.run(I._carry_out(c, A, I.NOT(Bv), True, s))
+            assert np.array_equal(ClearKey().decrypt_bool(cout), a >= b), (w, s)
+            assert c.launches == len(I._carry_levels(40, w, s))

@@ -68,9 +68,17 @@ def _run_plain(script, *args, timeout=600):
 
 
 def test_js_integer_kats_cpu():
-    """js/integer.js replays all 2,394 fhEVM KATs (ebool .. euint256; cleartext test double; the same
-    27 launches as Python)."""
-    assert _run_plain("integer_check.js").startswith("OK 2394 KATs, 27 launches")
+    """js/integer.js replays all 2,394 fhEVM KATs (ebool .. euint256; cleartext test double) with the same
+    launch and PBS counts as tfhe_amd/integer.py (the block carry-out circuit's cost model included)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from conftest import load_kats
+    from test_integer import CleartextEngine, build_kat_op
+    from tfhe_amd import integer as I
+    kats = load_kats()
+    c = I.Circuit(CleartextEngine(n=1))
+    c.run_many([build_kat_op(c, k) for k in kats])
+    assert _run_plain("integer_check.js") == f"OK 2394 KATs, {c.launches} launches, {c.pbs_count} PBS"
 
 
 def test_js_radix_kats_cpu():

@@ -88,11 +88,14 @@ Op = Generator[Level, List[np.ndarray], object]
 class Circuit:
     """Runs operator coroutines on an Engine: every yielded level is one batched PBS launch."""
 
-    def __init__(self, engine: Engine, capacity: int = 2048):
+    def __init__(self, engine: Engine, capacity: int = 2048, round_size: int = 1024):
         self.engine = engine
         self.dim = engine.params.n + 1
         self.lut = engine.gate_lut()
         self.capacity = capacity      # PBS one launch completes in ~one PBS latency (8 x 256 CUs)
+        # PBS per round of the batch kernel (the FFT64 pair kernel: 4 ciphertexts x 256 CUs); a launch of
+        # n PBS costs ~max(1, ceil(n / round_size)) rounds -- the carry-out circuit's cost model
+        self.round_size = round_size
         self.pbs_count = 0
         self.launches = 0
 
@@ -156,6 +159,19 @@ class Circuit:
         """Latency-bound (the level's PBS fit in one launch wave) -> log-depth prefix adder."""
         return batch * width * 2 <= self.capacity
 
+    def carry_block(self, batch: int, width: int) -> int:
+        """Block size of the carry-out circuit (_carry_out) with the fewest launch rounds (then the
+        fewest PBS): s = width is the ripple chain, s = 1 the bit-level reduction tree."""
+        best = None
+        for s in sorted({1 << k for k in range(width.bit_length())} | {width}):
+            if s > width:
+                continue
+            lv = _carry_levels(batch, width, s)
+            key = (sum(max(1, -(-n // self.round_size)) for n in lv), sum(lv), -s)
+            if best is None or key < best[0]:
+                best = (key, s)
+        return best[1]
+
 
 # --------------------------------------------------------------------------------------------
 # bit-vector circuits: arrays of shape (B, w, dim), LSB first
@@ -174,6 +190,10 @@ def g_add(c: Circuit, a: np.ndarray, b: np.ndarray, cin: bool = False, want_sum:
           want_carry: bool = False, prefix: bool = None) -> Op:
     """a + b + cin over w bits.  Returns (sum bits or None, carry-out or None)."""
     B, w = a.shape[0], a.shape[1]
+    if not want_sum:
+        # only the carry-out (comparisons): block ripple + reduction tree, block size by the cost model
+        s = c.carry_block(B, w) if prefix is None else (1 if prefix else w)
+        return None, (yield from _carry_out(c, a, b, cin, s))
     if prefix is None:
         prefix = c.prefer_prefix(B, w)
     if not prefix:
@@ -194,16 +214,6 @@ def g_add(c: Circuit, a: np.ndarray, b: np.ndarray, cin: bool = False, want_sum:
         return (np.stack(sums, axis=1) if want_sum else None), (carry if want_carry else None)
     # Kogge-Stone: inclusive prefixes (G, P)[0..i]
     G, P = yield [AND(a, b), OR(a, b)]
-    if not want_sum:
-        # only the full-span carry is needed: reduction tree
-        while G.shape[1] > 1:
-            if G.shape[1] % 2:
-                # pad with an identity element on the high side: G = 0, P = 1
-                G = np.concatenate([G, _zeros(c, B, 1)], axis=1)
-                P = np.concatenate([P, NOT(_zeros(c, B, 1))], axis=1)
-            lo_G, hi_G, lo_P, hi_P = G[:, 0::2], G[:, 1::2], P[:, 0::2], P[:, 1::2]
-            G, P = yield [MAJ(hi_G, hi_P, lo_G), MAJ(hi_G, hi_P, lo_P)]
-        return None, (P[:, 0] if cin else G[:, 0])
     d = 1
     while d < w:
         hi_G, hi_P = G[:, d:], P[:, d:]
@@ -215,6 +225,68 @@ def g_add(c: Circuit, a: np.ndarray, b: np.ndarray, cin: bool = False, want_sum:
     carries = np.concatenate([c.trivial(np.full((B, 1), cin, dtype=bool)), pref[:, :w - 1]], axis=1)
     (s,) = yield [XOR3(a, b, carries)]
     return s, (pref[:, w - 1] if want_carry else None)
+
+
+def _carry_levels(B: int, w: int, s: int) -> List[int]:
+    """PBS per launch of _carry_out(width w, block size s) over a batch of B."""
+    nb = -(-w // s)
+    lv = [B * (1 + 2 * sum(1 for k in range(1, nb) if k * s + j < w)) for j in range(s)]
+    n = nb
+    while n > 1:
+        lv.append(B * (1 + 2 * (n // 2 - 1)))
+        n = n - n // 2
+    return lv
+
+
+def _carry_out(c: Circuit, a: np.ndarray, b: np.ndarray, cin: bool, s: int) -> Op:
+    """Carry-out of a + b + cin over w bits (B, w, dim) in blocks of s bits: every block ripples its
+    carries in lockstep with the others (block 0 from the known carry-in: one MAJ per bit; blocks k >= 1
+    for both carry-ins, G = given 0 and P = given 1: AND / OR at their first bit, then two MAJ per bit),
+    then a reduction tree merges neighbours, (G, P)_hi o (G, P)_lo = (MAJ(G_hi, P_hi, G_lo),
+    MAJ(G_hi, P_hi, P_lo)) and C = MAJ(G_hi, P_hi, C_lo) onto block 0 (G implies P, so MAJ selects).
+    s + ceil(log2(w / s)) levels: s = w is the ripple chain, s = 1 the bit-level tree."""
+    B, w = a.shape[0], a.shape[1]
+    nb = -(-w // s)
+    C = c.trivial(np.full((B,), cin, dtype=bool))
+    G = P = None                                   # (B, nb - 1, dim): blocks 1 .. nb - 1
+    for j in range(s):
+        ks = [k for k in range(1, nb) if k * s + j < w]
+        lvl = [MAJ(a[:, j], b[:, j], C)]
+        if ks:
+            bits = [k * s + j for k in ks]
+            ab, bb = a[:, bits], b[:, bits]
+            if j == 0:
+                lvl += [AND(ab, bb), OR(ab, bb)]
+            else:
+                m = len(ks)                        # the active blocks are 1 .. m (only the last can end early)
+                lvl += [MAJ(ab, bb, G[:, :m]), MAJ(ab, bb, P[:, :m])]
+        out = yield lvl
+        C = out[0]
+        if ks:
+            if j == 0:
+                G, P = out[1], out[2]
+            else:
+                G = np.concatenate([out[1], G[:, len(ks):]], axis=1)
+                P = np.concatenate([out[2], P[:, len(ks):]], axis=1)
+    while G is not None and G.shape[1] > 0:
+        # states: C (block 0), then (G, P) of blocks 1 .. n-1; merge (0, 1) and (2i, 2i+1)
+        n = G.shape[1] + 1
+        npairs = n // 2 - 1                        # merges among blocks >= 2: (2, 3), (4, 5), ...
+        lvl = [MAJ(G[:, 0], P[:, 0], C)]
+        if npairs:
+            hiG, hiP = G[:, 2:2 * npairs + 1:2], P[:, 2:2 * npairs + 1:2]
+            loG, loP = G[:, 1:2 * npairs:2], P[:, 1:2 * npairs:2]
+            lvl += [MAJ(hiG, hiP, loG), MAJ(hiG, hiP, loP)]
+        out = yield lvl
+        C = out[0]
+        nG = [out[1]] if npairs else []
+        nP = [out[2]] if npairs else []
+        if n % 2:                                  # an odd block at the top passes through
+            nG.append(G[:, n - 2:n - 1])
+            nP.append(P[:, n - 2:n - 1])
+        G = np.concatenate(nG, axis=1) if nG else None
+        P = np.concatenate(nP, axis=1) if nP else None
+    return C
 
 
 def g_sub(c: Circuit, a, b, want_sum=True, want_carry=False) -> Op:
