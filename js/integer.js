@@ -281,7 +281,8 @@ function* gSelect(c, cond, x, y) {
   const ncond = c.NOT(cond);
   const tf = yield x.map((xi) => c.AND(cond, xi)).concat(y.map((yi) => c.AND(ncond, yi)));
   const w = x.length;
-  return yield tf.slice(0, w).map((t, i) => c.OR(t, tf[w + i]));
+  // at most one of t, f is true: OR(t, f) = t + f + 1/8 exactly, no second bootstrap (tfhe_amd/integer.py)
+  return tf.slice(0, w).map((t, i) => c.OR(t, tf[w + i]));
 }
 
 function* gMul(c, a, b, B) {

@@ -88,8 +88,9 @@ def test_max_tree_gloo_world2():
 
 def test_max_tree_launch_shape():
     """The comparisons' carry-out runs as a block ripple + reduction tree sized by the circuit's cost
-    model (tfhe_amd.integer._carry_out): 69 launches for the 256-bidder tree instead of the ripple's 116
-    (level 1: 8 chain steps of 896 PBS + 2 tree levels instead of 32 steps of 128)."""
+    model (tfhe_amd.integer._carry_out), and the select is one level (its OR of exclusive terms is linear):
+    61 launches for the 256-bidder tree instead of the ripple's 116 (level 1: 8 chain steps of 896 PBS + 2
+    tree levels instead of 32 steps of 128, then one select launch of 2 x 128 x 40)."""
     c = I.Circuit(CleartextEngine())
     sizes = []
     pbs = c.engine.pbs
@@ -97,8 +98,8 @@ def test_max_tree_launch_shape():
     v = _bids(256)
     mx, idx = max_tree(c, I.FheUint.trivial(c, v, 32))
     assert (int(mx.decrypt(ClearKey())[0]), int(idx.decrypt(ClearKey())[0])) == _expected(v)
-    assert c.launches == len(sizes) == 69
-    assert sizes[:10] == [896] * 8 + [384, 128]
+    assert c.launches == len(sizes) == 61
+    assert sizes[:11] == [896] * 8 + [384, 128, 10240]
     assert [c.carry_block(B, 32) for B in (128, 64, 32, 1)] == [8, 4, 2, 2]
 
 

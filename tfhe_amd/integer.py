@@ -311,11 +311,13 @@ def g_eq(c: Circuit, a, b) -> Op:
 
 
 def g_select(cond: np.ndarray, x: np.ndarray, y: np.ndarray) -> Op:
-    """cond ? x : y bitwise (2 levels: two ANDs, one OR; at most one AND is true)."""
+    """cond ? x : y bitwise in ONE level: t = AND(cond, x), f = AND(NOT cond, y), and since at most one of
+    them is true, OR(t, f) = t + f + 1/8 holds exactly on the phases (-1/8 - 1/8 + 1/8 = -1/8, 1/8 - 1/8 + 1/8
+    = 1/8): the OR needs no bootstrap.  The result carries the noise of two PBS outputs, still far inside
+    the 1/8 decision margin of any gate it feeds."""
     cw = np.broadcast_to(cond[:, None, :], x.shape)
     t, f = yield [AND(cw, x), AND(NOT(cw), y)]
-    (r,) = yield [OR(t, f)]
-    return r
+    return OR(t, f)
 
 
 def g_mul(c: Circuit, a: np.ndarray, b: Union[np.ndarray, int], prefix=None) -> Op:
@@ -391,7 +393,7 @@ def _shift_clear(c: Circuit, a: np.ndarray, k: int, kind: str) -> np.ndarray:
 
 def g_shift(c: Circuit, a: np.ndarray, amount: Union[np.ndarray, int], kind: str) -> Op:
     """Shift / rotate by (amount mod w): a plaintext amount is rewiring (free); an encrypted one
-    is a barrel shifter, one select layer (2 levels) per amount bit."""
+    is a barrel shifter, one select level per amount bit."""
     if isinstance(amount, (int, np.integer)):
         return _shift_clear(c, a, int(amount), kind)
     w = a.shape[1]
