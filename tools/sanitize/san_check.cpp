@@ -1,7 +1,8 @@
 // AddressSanitizer + UndefinedBehaviorSanitizer run of the HOST code (SURVEY §5 aux: memory checking):
 // the product's client-side key material (tfhe_amd/csrc/client.cpp: ChaCha streams, keygen, server keys,
-// MS zeros, encryption, phase, LUT builders, packing key, compression) and the CPU oracle (oracle/*.c:
-// keygen, NTT and FFT64 blind rotations, keyswitch, full PBS of both parameter sets, MS reduction).
+// MS zeros, encryption, phase, LUT builders, packing key, compression, squashing key) and the CPU oracle
+// (oracle/*.c: keygen, NTT and FFT64 blind rotations, keyswitch, full PBS of both parameter sets, MS
+// reduction, the native 2^128 squash blind rotation).
 // Built by `make -C oracle san` into oracle/_san/ (test infrastructure; no GPU code: GPU sanitizers are
 // unavailable on the pool).  Also cross-checks that client and oracle draw identical keys.
 #include <stdio.h>
@@ -98,6 +99,36 @@ int main() {
   std::vector<uint64_t> packed(client::pks_packed_words(pp, 7));
   client::pks_compress(pp, glwe.data(), 7, packed.data());
   client::pks_extract(pp, packed.data(), 7, back.data());
+  // noise squashing at a reduced input dimension: client key words == oracle key words, the identity LUT,
+  // the oracle's native 2^128 blind rotation (key rounding, limb NTTs, 128-bit decomposition) and phase
+  {
+    or_sns_params osp{};
+    or_sns_params_preset(0, &osp);
+    osp.n = 3;
+    tfhe_sns_params sp{osp.n, osp.k, osp.N, osp.base_log, osp.level, osp.noise_log2};
+    std::vector<uint64_t> lk = {1, 0, 1}, g1((size_t)sp.k * sp.N), g2(g1.size());
+    std::vector<uint64_t> b1(client::sns_bsk_len(sp)), b2(or_sns_bsk_len(&osp));
+    CHECK(b1.size() == b2.size());
+    client::sns_keygen(sp, client::rng_key_from_seed(0x5A5), lk.data(), g1.data(), b1.data());
+    or_sns_keygen(&osp, 0x5A5, lk.data(), g2.data(), b2.data());
+    CHECK(g1 == g2 && b1 == b2);
+    std::vector<uint64_t> l1(2 * (size_t)sp.N), l2(l1.size());
+    client::sns_lut_identity(sp, 16, l1.data());
+    or_sns_lut_identity(&osp, 16, l2.data());
+    CHECK(l1 == l2);
+    std::vector<uint64_t> rounded(b2.size()), limb(or_sns_limb_ntt_len(&osp));
+    or_sns_bsk_round(&osp, b2.data(), rounded.data());
+    or_sns_bsk_to_limb_ntt(&osp, rounded.data(), limb.data());
+    std::vector<uint64_t> small(osp.n + 1), acc((size_t)(osp.k + 1) * 2 * osp.N), out(2 * ((size_t)osp.k * osp.N + 1));
+    for (size_t i = 0; i < small.size(); i++) small[i] = 0x9E3779B97F4A7C15ull * (i + 1);
+    or_sns_blind_rotate(&osp, limb.data(), small.data(), l2.data(), acc.data());
+    or_sns_sample_extract(&osp, acc.data(), out.data());
+    uint64_t p1[2], p2[2];
+    client::sns_phase(sp, g1.data(), out.data(), 1, p1);
+    or_sns_phase(&osp, g2.data(), out.data(), 1, p2);
+    CHECK(p1[0] == p2[0] && p1[1] == p2[1]);
+    printf("squash keys == oracle, native blind rotation clean\n");
+  }
   printf(fails ? "SANITIZE FAIL %d\n" : "SANITIZE OK\n", fails);
   return fails ? 1 : 0;
 }
