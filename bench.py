@@ -89,7 +89,7 @@ def profile_for(kernel: str, B: int):
         if d.get("source_id") != sid or d.get("batch", 4096) != B:
             continue
         for k, v in d["kernels"].items():
-            if k.split("<")[0].endswith("::" + kernel):
+            if k.split("<")[0].split("::")[-1] == kernel:
                 return dict(v, source=os.path.relpath(f, ROOT), source_id=sid)
     return None
 
@@ -243,8 +243,6 @@ def main() -> int:
     preset_id = {"gate": tfhe_amd.PRESET_GATE, "gate_fft": tfhe_amd.PRESET_GATE_FFT, "fhevm": tfhe_amd.PRESET_FHEVM,
                  "fhevm_fft": tfhe_amd.PRESET_FHEVM_FFT}[args.preset]
     params = tfhe_amd.Params.preset(preset_id)
-    br_kernel = {"gate": "blind_rotate_kernel", "gate_fft": "blind_rotate_fft_kernel",
-                 "fhevm": "blind_rotate2048_kernel", "fhevm_fft": "blind_rotate_fft2k_kernel"}[args.preset]
     br_bytes = BR_BYTES_PER_PBS_FHEVM if fhevm else BR_BYTES_PER_PBS
     strong = args.global_batch > 0
     if strong:  # contiguous slice [lo, hi) of one global batch (SURVEY 8e partition)
@@ -271,6 +269,7 @@ def main() -> int:
         dist.barrier()
         bcast_ms = broadcast_keys(d_bsk, d_ksk, src=0)
     eng = tfhe_amd.Engine(params, local)
+    br_kernel = eng.br_kernel(B)  # the kernel the library's dispatch launches for this batch (profile matching)
     eng.load_keys_device(d_bsk, d_ksk)
     del d_bsk, d_ksk
     if fhevm:  # P-FHEVM server keys carry the modulus-switch noise-reduction zeros (10.6 MB, per rank)
@@ -376,8 +375,9 @@ def main() -> int:
                                       bsk_bytes + B * 8 * ((pd["n"] + 1) + (pd["k"] * pd["N"] + 1))),
                              # the reuse the kernel implements and the true minimum traffic
                              bsk_reuse=(f"each BSK level-step chunk is streamed once per workgroup into LDS and shared "
-                                        f"by its {8 if not (fhevm and fft) else 4} ciphertexts; resident workgroups "
-                                        f"share it through L2"),
+                                        f"by its {8 if args.preset == 'gate' else 4} ciphertexts; resident workgroups share it through L2"
+                                        if "lat" not in br_kernel else
+                                        "latency kernel: one ciphertext per workgroup, key words from L2"),
                              min_traffic_bytes_per_pbs=round((bsk_bytes + ksk_bytes) / B + io_bytes),
                              launches=br_n),
             "keyswitch_ms": round(ks_ms / max(ks_n, 1), 3),

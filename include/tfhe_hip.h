@@ -216,6 +216,10 @@ int tfhe_hip_nand(tfhe_ctx* ctx, const uint64_t* c1, const uint64_t* c2, size_t 
  * batch kernel 14.5-15.5 ms up to 2048 ciphertexts at N=1024, 15.3-16.0 ms up to 1024 at N=2048);
  * 0 disables the latency kernel. */
 int tfhe_hip_set_latency_batch(tfhe_ctx* ctx, size_t max_batch);
+/* Name of the blind-rotate kernel the dispatch launches for a per-shard batch of `batch` ciphertexts under
+ * the current latency threshold (e.g. "blind_rotate_fft_pair_kernel"), or NULL for a null ctx.  No reference
+ * counterpart: a measurement aid, so a profile is matched to the kernel that actually ran (bench.py). */
+const char* tfhe_hip_br_kernel(const tfhe_ctx* ctx, size_t batch);
 /* Wait for all work on the ctx stream. */
 int tfhe_hip_sync(tfhe_ctx* ctx);
 /* Per-kernel device timing (HIP events recorded on the launch stream around every blind-rotate /

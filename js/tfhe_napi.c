@@ -978,6 +978,12 @@ static napi_value js_squash(napi_env env, napi_callback_info info) {
     napi_throw_range_error(env, "EINVAL", "squash: length is not a positive multiple of k*N + 1");
     return NULL;
   }
+  /* the squashing LUT's own rule (tfhe_hip_sns_squash): checked here so a bad modulus throws before the
+   * keyswitch and noise reduction are queued on the GPU */
+  if (!mm || mm > a->sp.N || a->sp.N % mm) {
+    napi_throw_range_error(env, "EINVAL", "squash: msgModulus must divide the squashing polynomial size N");
+    return NULL;
+  }
   job_t* j = (job_t*)calloc(1, sizeof(job_t));
   if (!j) return throw_tfhe(env, TFHE_HIP_ENOMEM);
   j->kind = JOB_SQUASH;

@@ -47,6 +47,9 @@ const wr = (f, a) => fs.writeFileSync(f, Buffer.from(a.buffer, a.byteOffset, a.b
   const sq = new t.Squasher(0).loadKey(bsk);
   const msgs = Array.from({ length: 64 }, (_, i) => (i * 7 + 3) % 16);
   const cts = ck.encrypt(msgs, 16, seed + 1n);
+  // a modulus the squashing LUT cannot take throws synchronously, before any GPU work is queued
+  for (const bad of [0, 3, 4096]) assert.throws(() => sq.squash(eng, cts, bad), /msgModulus/);
+  res.squash_bad_modulus_sync_throw = true;
   const out = await sq.squash(eng, cts, 16);
   wr(path.join(dir, 'js_squash.bin'), out);
   assert.deepStrictEqual(t.Squasher.decrypt(glweKey, out, 16), msgs);

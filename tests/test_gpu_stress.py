@@ -40,7 +40,7 @@ def test_stress_pfhevm_16k(fhevm_engine, fhevm_keys):
 
 
 def test_stress_pgate_fft64_64k(gate_fft_engine, gate_fft_keys):
-    """The headline kernel (FFT64 batch, blind_rotate_fft_kernel): 4 x 16,384 PBS, every output decrypted;
+    """The headline kernel (FFT64 batch, blind_rotate_fft_pair_kernel): 4 x 16,384 PBS, every output decrypted;
     the last pass through the latency kernel."""
     ck, _ = gate_fft_keys
     B = 16384

@@ -111,7 +111,7 @@ ABI_SYMBOLS = (
     "tfhe_hip_sns_squash_async", "tfhe_hip_sns_blind_rotate", "tfhe_hip_sns_phase", "tfhe_hip_fft_fwd",
     "tfhe_hip_fft_inv", "tfhe_hip_rng_key_entropy", "tfhe_hip_rng_key_from_seed", "tfhe_hip_keygen_k",
     "tfhe_hip_server_keygen_k", "tfhe_hip_ms_zeros_keygen_k", "tfhe_hip_lwe_encrypt_k", "tfhe_hip_ndev",
-    "tfhe_hip_device_at", "tfhe_hip_key_bcast_mode",
+    "tfhe_hip_device_at", "tfhe_hip_key_bcast_mode", "tfhe_hip_br_kernel",
 )
 
 # P-FHEVM modulus-switch noise reduction key (include/tfhe_hip.h TFHE_HIP_MS_FHEVM_*)
@@ -161,6 +161,8 @@ def lib():
         L.tfhe_hip_ndev.argtypes = [ctypes.c_void_p]
         L.tfhe_hip_device_at.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.tfhe_hip_key_bcast_mode.argtypes = [ctypes.c_void_p]
+        L.tfhe_hip_br_kernel.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.tfhe_hip_br_kernel.restype = ctypes.c_char_p
         _RKP = ctypes.POINTER(RngKey)
         L.tfhe_hip_rng_key_entropy.argtypes = [_RKP]
         L.tfhe_hip_rng_key_from_seed.argtypes = [ctypes.c_uint64, _RKP]
@@ -399,6 +401,17 @@ class Engine:
         self.devices = devs
         self.device = devs[0]
 
+    CUS_PER_DEVICE = 256  # MI355X
+
+    @property
+    def round_size(self) -> int:
+        """PBS one round of this engine's batch kernel holds across its shards (one workgroup per CU): 4
+        ciphertexts per workgroup on the FFT64 kernels (N = 1024 component pairs, N = 2048 parity pairs) and on
+        the N = 2048 NTT kernel, 8 on the N = 1024 NTT kernel.  The carry-out circuit's launch-round cost model
+        (integer.Circuit) reads it."""
+        per_wg = 8 if (self.params.transform == 0 and self.params.N == 1024) else 4
+        return per_wg * self.CUS_PER_DEVICE * len(self.devices)
+
     @property
     def key_bcast_mode(self) -> str:
         return {0: "single", 1: "copy", 2: "rccl"}.get(lib().tfhe_hip_key_bcast_mode(self._h), "?")
@@ -557,6 +570,10 @@ class Engine:
     def set_latency_batch(self, max_batch: int) -> None:
         """Batches up to ``max_batch`` use the latency blind-rotate kernel (0: always the batch kernel)."""
         _check(lib().tfhe_hip_set_latency_batch(self._h, ctypes.c_size_t(max_batch)))
+
+    def br_kernel(self, batch: int) -> str:
+        """Name of the blind-rotate kernel the dispatch launches for a per-shard batch of ``batch``."""
+        return lib().tfhe_hip_br_kernel(self._h, ctypes.c_size_t(batch)).decode()
 
     # -- timing (HIP events around each kernel launch) -----------------------------------------
     def timing(self, enable: bool = True) -> None:

@@ -581,16 +581,6 @@ extern "C" int tfhe_hip_debug_fft2k_stamps(unsigned long long* out) {
 }
 #endif
 
-#if FFT_STAMPS
-namespace tfhe {
-hipError_t read_fft_stamps(unsigned long long* out);
-}
-// diagnostic builds only (-DFFT_STAMPS=1): the P-GATE batch kernel's phase stamps (tools/stamps.py --gate)
-extern "C" int tfhe_hip_debug_fft_stamps(unsigned long long* out) {
-  return tfhe::read_fft_stamps(out) == hipSuccess ? 0 : TFHE_HIP_EDEVICE;
-}
-#endif
-
 // error slot shared with pks_api.cpp / sns_api.cpp
 int tfhe_hip_set_error(int code, const char* msg) {
   g_err = msg;
@@ -1089,6 +1079,16 @@ int tfhe_hip_set_latency_batch(tfhe_ctx* c, size_t max_batch) {
   std::lock_guard<std::mutex> lk(c->mu);
   c->lat_max = max_batch;
   return 0;
+}
+
+// mirrors launch_br / the launchers' B <= latency_max_batch switch
+const char* tfhe_hip_br_kernel(const tfhe_ctx* c, size_t B) {
+  if (!c) return nullptr;
+  const bool lat = B <= c->lat_max;
+  if (is_fft(c->p) && c->p.N == 2048) return lat ? "blind_rotate_fft2k_lat_kernel" : "blind_rotate_fft2k_kernel";
+  if (is_fft(c->p)) return lat ? "blind_rotate_fft_lat_kernel" : "blind_rotate_fft_pair_kernel";
+  if (c->p.N == 2048) return lat ? "blind_rotate2048_lat_kernel" : "blind_rotate2048_kernel";
+  return lat ? "blind_rotate_lat_kernel" : "blind_rotate_kernel";
 }
 
 int tfhe_hip_sync(tfhe_ctx* c) {

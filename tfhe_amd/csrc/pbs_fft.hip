@@ -5,9 +5,9 @@
 // Why: MI355X runs f64 add / mul / fma at the full VALU rate (~6 cycles per wave-instruction, the
 // same as a 32-bit integer op, tools/microbench/f64_rates.hip), and a complex radix-2 butterfly is ~8
 // such instructions where a Goldilocks butterfly is ~30 integer ones.  Same BSK bytes (N/2 complex
-// doubles = N u64 per polynomial), same workgroup structure (8 ciphertexts walk the CMUX loop in
-// lockstep, the BSK level-step chunks streamed once per workgroup into LDS by global_load_lds,
-// double-buffered).
+// doubles = N u64 per polynomial); the batch kernel walks the CMUX loop with 4 ciphertexts x 2 component
+// waves per workgroup in lockstep, the BSK level steps streamed once per workgroup into LDS by
+// global_load_lds, double-buffered.
 //
 // Arithmetic (one fixed f64 operation sequence, restated in oracle/fft_oracle.c, which this file
 // reproduces bit-for-bit — every product is written as an explicit fma or a lone multiply, and
@@ -130,270 +130,13 @@ __global__ __launch_bounds__(64) void fft_inv_kernel(const double2* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
-// Blind rotation + sample extraction (batch kernel): workgroup = W wavefronts = W ciphertexts (8; 4 for
-// batches of 513-1024, FFT_W4_MAX).
-// BSK chunk buffers: 2 = one level step in flight (default); 3 keeps two in flight (chunk g + 2 issued
-// while step g computes, the barrier before step g waits only for chunk g with a counted vmcnt):
-// measured 3 % slower on MI355X (31.2 vs 30.35 ms per 4096; the chunk arrives in time either way and
-// the third buffer costs registers), kept for A/B runs.
 // FFT_PRIO: s_setprio 1 for waves 4-7 (the second-dispatched wave of each SIMD pair) for the whole
-// CMUX loop; measured 29.36 -> 29.25 ms per 4096 (both waves of a SIMD run the same lockstep program, the
-// younger one otherwise loses VALU arbitration after every barrier).  2 = odd waves (same result).
+// CMUX loop (round 1, measured on the 8-ciphertext kernel 29.36 -> 29.25 ms per 4096: both waves of a SIMD run the
+// same lockstep program, the younger one otherwise loses VALU arbitration after every barrier).
 #ifndef FFT_PRIO
 #define FFT_PRIO 1
 #endif
-#ifndef FFT_KBUF
-#define FFT_KBUF 2
-#endif
-// FFT_INVTW: the two inverse transforms of a CMUX share one read of the inverse twiddles (registers)
-#ifndef FFT_INVTW
-#define FFT_INVTW 1
-#endif
-[[maybe_unused]] constexpr int FB_WAVES = 8;
-constexpr int CHUNK_C64 = 2 * M;                   // one level step: rows (c, l), j = 0, 1 (16 KB)
-constexpr int CHUNK_GLDS = CHUNK_C64 * 16 / 1024;  // 1 KB wave-instructions per chunk (16)
-// KBUF 3: s_waitcnt vmcnt(CHUNK_GLDS / W), the global_load_lds a wave issues per chunk (gfx9 encoding:
-// vmcnt[3:0] | expcnt[6:4] = 7 | lgkmcnt[11:8] = 15 | vmcnt[5:4] in [15:14])
 
-// FFT_STAMPS (diagnostic builds only, never the shipped library): s_memtime stamps at the phase
-// boundaries of the CMUX loop, summed per wave of every 64th workgroup into fft_stamps[slot][wave][phase]
-// (read with tfhe_hip_debug_fft_stamps, tools/stamps.py --gate).  Read the SHARES: the stamps' waits
-// forbid overlaps the shipped kernel has.
-#ifndef FFT_STAMPS
-#define FFT_STAMPS 0
-#endif
-[[maybe_unused]] constexpr int FS_NPH = 8;  // rotate, level barrier, digits + twist, forward DFT, MAC, inverse 0, inverse 1, top
-#if FFT_STAMPS
-__device__ unsigned long long fft_stamps[16][FB_WAVES][FS_NPH];
-#define FS_STAMP(k)                                                                              \
-  do {                                                                                           \
-    __builtin_amdgcn_sched_barrier(0);                                                           \
-    unsigned long long _t;                                                                       \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                     \
-    __builtin_amdgcn_sched_barrier(0);                                                           \
-    st_acc[k] += _t - st_prev;                                                                   \
-    st_prev = _t;                                                                                \
-  } while (0)
-#define FS_ARGS , unsigned long long (&st_acc)[FS_NPH], unsigned long long& st_prev
-#define FS_PASS , st_acc, st_prev
-#else
-#define FS_STAMP(k) \
-  do {              \
-  } while (0)
-#define FS_ARGS
-#define FS_PASS
-#endif
-
-// W waves = W ciphertexts per workgroup: 8 (two waves per SIMD) for full batches; 4 (one per SIMD) when
-// the batch is too small to give every CU a workgroup of 8 (FFT_W4_MAX)
-template <int W>
-struct FftShared {
-  double2 T[W][T_C64];         // per-wave transpose / rotation scratch  72 KB at W = 8
-  double2 K[FFT_KBUF][CHUNK_C64];  // BSK level-step chunks in flight   16 KB each
-  double2 tw[TW_C64];          // twist | pass A | pass B | inverse B'   32 KB
-};
-
-template <int W>
-__device__ __forceinline__ void load_chunk(const double2* __restrict__ bsk, int g, double2* dst, int wave, int lane) {
-  const char* src = (const char*)(bsk + (size_t)g * CHUNK_C64);
-#pragma unroll
-  for (int q = 0; q < CHUNK_GLDS / W; q++) {
-    const int blk = wave * (CHUNK_GLDS / W) + q;
-    __builtin_amdgcn_global_load_lds((const void*)(src + blk * 1024 + lane * 16),
-                                     (__attribute__((address_space(3))) void*)((char*)dst + blk * 1024), 16, 0, 0);
-  }
-}
-
-// component c of the external product for CMUX i: decompose (X^a - 1) acc_c; per level l (step
-// g = 6 i + 3 c + l) transform the digit polynomial and accumulate D (.) BSK_i[(c, l)][j] into O_j
-template <int W>
-__device__ __forceinline__ void ext_prod_component(const u64 (&acc)[16], int rbase, int c, int i, int n_steps,
-                                                   FftShared<W>& sh, double2* T, int wave, int lane, TBase tb,
-                                                   const double2* __restrict__ bsk, double (&o0r)[8],
-                                                   double (&o0i)[8], double (&o1r)[8], double (&o1i)[8] FS_ARGS) {
-  u64* Tu = (u64*)T;
-#pragma unroll
-  for (int e = 0; e < 16; e++) Tu[64 * e + lane] = acc[e];
-  lds_order();
-  // (X^a acc)[64 e + L] = +-acc[(t mod 1024)], t = 64 e + L - a + 2048: negated iff t in [1024, 2048)
-  u32 st[16];
-#pragma unroll
-  for (int e = 0; e < 16; e++) {
-    const int t = rbase + 64 * e;
-    const u64 x = Tu[t & (N1K - 1)];
-    const u64 r = (t & N1K) ? 0 - x : x;
-    st[e] = decomp_state(r - acc[e]);
-  }
-  lds_order();
-  FS_STAMP(0);
-#pragma unroll 1
-  for (int q = 0; q < 3; q++) {  // level 2 - q: least significant first
-    const int g = i * 6 + c * 3 + q;
-#if FFT_KBUF == 3
-    // chunk g is complete once at most chunk g + 1's loads (issued one step ago) are outstanding
-    // raw s_barrier: __syncthreads()'s fence would drain vmcnt(0), chunk g + 1 included
-    if (g + 1 < n_steps) __builtin_amdgcn_s_waitcnt(0x0F70 | (CHUNK_GLDS / W));  // vmcnt(loads per chunk)
-    else __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
-    if (g + 2 < n_steps) load_chunk<W>(bsk, g + 2, sh.K[(g + 2) % 3], wave, lane);
-#else
-    glds_barrier();
-    if (g + 1 < n_steps) load_chunk<W>(bsk, g + 1, sh.K[(g + 1) & 1], wave, lane);
-#endif
-    FS_STAMP(1);
-    const u32 bmask = q < 2 ? 1u : 0u;
-    double xr[8], xi[8];
-#pragma unroll
-    for (int e = 0; e < 8; e++) {
-      xr[e] = (double)decomp_step(st[e], bmask);
-      xi[e] = (double)decomp_step(st[e + 8], bmask);
-    }
-    twist_slots<false>(xr, xi);
-    FS_STAMP(2);
-    dft512_fwd<true>(xr, xi, T, lane, tb, sh.tw);
-    FS_STAMP(3);
-    const double2* k0 = sh.K[g % FFT_KBUF] + lane;
-    const double2* k1 = sh.K[g % FFT_KBUF] + M + lane;
-#pragma unroll
-    for (int e = 0; e < 8; e++) {
-      const double2 u = k0[64 * e], v = k1[64 * e];
-      o0r[e] = __builtin_fma(xr[e], u.x, o0r[e]);
-      o0r[e] = __builtin_fma(-xi[e], u.y, o0r[e]);
-      o0i[e] = __builtin_fma(xr[e], u.y, o0i[e]);
-      o0i[e] = __builtin_fma(xi[e], u.x, o0i[e]);
-      o1r[e] = __builtin_fma(xr[e], v.x, o1r[e]);
-      o1r[e] = __builtin_fma(-xi[e], v.y, o1r[e]);
-      o1i[e] = __builtin_fma(xr[e], v.y, o1i[e]);
-      o1i[e] = __builtin_fma(xi[e], v.x, o1i[e]);
-    }
-    FS_STAMP(4);
-  }
-}
-
-// acc_j += round(iFFT(O_j))
-__device__ __forceinline__ void accumulate(u64 (&acc)[16], double (&or_)[8], double (&oi)[8], double2* T, int lane,
-                                           TBase tb, const double2* tw) {
-  fft_inv_real(or_, oi, T, lane, tb, tw);
-#pragma unroll
-  for (int e = 0; e < 8; e++) {
-    acc[e] += f64_to_torus(or_[e]);
-    acc[e + 8] += f64_to_torus(oi[e]);
-  }
-}
-
-template <int W, bool WRITE_ACC, bool WRITE_BIG>
-__global__ __launch_bounds__(64 * W, 1) void blind_rotate_fft_kernel(
-    const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
-    int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tw_g, u64* __restrict__ out_big,
-    u64* __restrict__ out_acc) {
-  __shared__ __attribute__((aligned(16))) FftShared<W> sh;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const size_t b_raw = (size_t)blockIdx.x * W + wave;
-  const bool live = b_raw < B;
-  const size_t b = live ? b_raw : B - 1;  // padding waves run a copy of the last ciphertext, store nothing
-  const u64* ct = lwe_in + b * (size_t)(n + 1);
-  double2* T = sh.T[wave];
-  const int n_steps = n * 6;
-
-  for (int q = threadIdx.x; q < TW_C64; q += 64 * W) sh.tw[q] = tw_g[q];
-  load_chunk<W>(bsk, 0, sh.K[0], wave, lane);
-#if FFT_KBUF == 3
-  if (n_steps > 1) load_chunk<W>(bsk, 1, sh.K[1], wave, lane);
-#endif
-
-  // acc = (0, X^{-b~} * lut): LUT values arrive in the Z_p encoding, mapped to the torus first
-  u64 accA[16], accB[16];
-  {
-    int li = lut_index ? (int)lut_index[b] : 0;
-    li = (li < 0 || li >= n_lut) ? 0 : li;
-    const u64* lut = luts + (size_t)li * N1K;
-    const int s = (2048 - ms2048(ct[n])) & 2047;
-#pragma unroll
-    for (int e = 0; e < 16; e++) {
-      int d = 64 * e + lane - s;
-      bool neg = false;
-      if (d < 0) { d += N1K; neg = !neg; }
-      if (d < 0) { d += N1K; neg = !neg; }
-      const u64 v = gl_to_torus(lut[d]);
-      accA[e] = 0;
-      accB[e] = neg ? 0 - v : v;
-    }
-  }
-
-  const TBase tb(lane);
-#if FFT_PRIO == 1
-  if (W == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
-#elif FFT_PRIO == 2
-  if (wave & 1) __builtin_amdgcn_s_setprio(1);
-#endif
-#if FFT_STAMPS
-  unsigned long long st_acc[FS_NPH] = {0}, st_prev;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
-#endif
-  for (int i = 0; i < n; i++) {
-    const int rbase = lane - ms2048(ct[i]) + 2 * N1K;
-    double o0r[8], o0i[8], o1r[8], o1i[8];
-#pragma unroll
-    for (int e = 0; e < 8; e++) { o0r[e] = 0; o0i[e] = 0; o1r[e] = 0; o1i[e] = 0; }
-    FS_STAMP(7);
-    ext_prod_component<W>(accA, rbase, 0, i, n_steps, sh, T, wave, lane, tb, bsk, o0r, o0i, o1r, o1i FS_PASS);
-    ext_prod_component<W>(accB, rbase, 1, i, n_steps, sh, T, wave, lane, tb, bsk, o0r, o0i, o1r, o1i FS_PASS);
-#if FFT_INVTW
-    {  // both inverses with the twiddles read once
-      InvTw w;
-      w.load(sh.tw, lane);
-      dft512_inv_r(o0r, o0i, T, lane, tb, w);
-      twist_slots<true>(o0r, o0i);
-#pragma unroll
-      for (int e = 0; e < 8; e++) {
-        accA[e] += f64_to_torus(o0r[e]);
-        accA[e + 8] += f64_to_torus(o0i[e]);
-      }
-      FS_STAMP(5);
-      dft512_inv_r(o1r, o1i, T, lane, tb, w);
-      twist_slots<true>(o1r, o1i);
-#pragma unroll
-      for (int e = 0; e < 8; e++) {
-        accB[e] += f64_to_torus(o1r[e]);
-        accB[e + 8] += f64_to_torus(o1i[e]);
-      }
-    }
-#else
-    accumulate(accA, o0r, o0i, T, lane, tb, sh.tw);
-    FS_STAMP(5);
-    accumulate(accB, o1r, o1i, T, lane, tb, sh.tw);
-#endif
-    FS_STAMP(6);
-  }
-#if FFT_STAMPS
-  if ((blockIdx.x & 63) == 0 && lane == 0 && (blockIdx.x >> 6) < 16)
-    for (int k = 0; k < FS_NPH; k++) fft_stamps[blockIdx.x >> 6][wave][k] = st_acc[k];
-#endif
-
-  if (!live) return;
-  if (WRITE_ACC) {
-    u64* oa = out_acc + b * 2048;
-#pragma unroll
-    for (int e = 0; e < 16; e++) {
-      oa[64 * e + lane] = accA[e];
-      oa[N1K + 64 * e + lane] = accB[e];
-    }
-  }
-  if (WRITE_BIG) {
-    // sample extraction at degree 0 (computations.rs:109-132): a'_0 = A[0], a'_j = -A[N-j], b' = B[0]
-    u64* ob = out_big + b * (size_t)(N1K + 1);
-#pragma unroll
-    for (int e = 0; e < 16; e++) {
-      const int idx = 64 * e + lane;
-      if (idx == 0) ob[0] = accA[e];
-      else ob[N1K - idx] = 0 - accA[e];
-    }
-    if (lane == 0) ob[N1K] = accB[0];
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // Component-pair batch kernel (round 3, the default above the latency range): workgroup = 4 ciphertexts x 2
 // waves, wave (p, c) owns COMPONENT c of ciphertext p.  Per CMUX i:
 //   rotate + decompose acc_c (wave-local: the wave's own transpose area holds the rotation image)
@@ -867,40 +610,9 @@ bool fft_slot_constants_ok() {
   return true;
 }
 
-#if FFT_STAMPS
-hipError_t read_fft_stamps(unsigned long long* out) {  // 16 x 8 x FS_NPH
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(fftk::fft_stamps), sizeof(fftk::fft_stamps), 0, hipMemcpyDeviceToHost);
-}
-#endif
-
 hipError_t launch_bsk_to_fourier(const u64* bsk_std, double* bsk_f, size_t polys, const double* tw, hipStream_t s) {
   hipLaunchKernelGGL(fftk::bsk_to_fourier_kernel, dim3((unsigned)polys), dim3(64), 0, s, bsk_std, (double2*)bsk_f,
                      (const double2*)tw);
-  return hipGetLastError();
-}
-
-// batches up to this size (per device, above the latency kernel's range) run 4-wave workgroups: at 8
-// ciphertexts per workgroup a batch of 1024 would leave half the CUs idle
-#ifndef FFT_W4_MAX
-#define FFT_W4_MAX 1024
-#endif
-#ifndef FFT_LEGACY_BATCH
-#define FFT_LEGACY_BATCH 0
-#endif
-template <int W>
-static hipError_t launch_batch(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index, int n_lut,
-                               const double2* bk, const double2* t, u64* out_big, u64* out_acc, hipStream_t s) {
-  using namespace fftk;
-  dim3 grid((unsigned)((B + W - 1) / W)), block(64 * W);
-  if (out_acc && out_big)
-    hipLaunchKernelGGL((blind_rotate_fft_kernel<W, true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
-                       n_lut, bk, t, out_big, out_acc);
-  else if (out_acc)
-    hipLaunchKernelGGL((blind_rotate_fft_kernel<W, true, false>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
-                       n_lut, bk, t, out_big, out_acc);
-  else
-    hipLaunchKernelGGL((blind_rotate_fft_kernel<W, false, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
-                       n_lut, bk, t, out_big, out_acc);
   return hipGetLastError();
 }
 
@@ -923,11 +635,6 @@ hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64
                          n_lut, bk, t, out_big, out_acc);
     return hipGetLastError();
   }
-#if FFT_LEGACY_BATCH
-  // the round-2 8-ciphertext kernel (chain MAC order: NOT bit-identical with the split-order oracle; A/B timing only)
-  if (B <= FFT_W4_MAX) return launch_batch<4>(lwe_in, B, n, luts, lut_index, n_lut, bk, t, out_big, out_acc, s);
-  return launch_batch<FB_WAVES>(lwe_in, B, n, luts, lut_index, n_lut, bk, t, out_big, out_acc, s);
-#else
   dim3 grid((unsigned)((B + FP_CTS - 1) / FP_CTS)), block(64 * FP_WAVES);
   if (out_acc && out_big)
     hipLaunchKernelGGL((blind_rotate_fft_pair_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
@@ -939,7 +646,6 @@ hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64
     hipLaunchKernelGGL((blind_rotate_fft_pair_kernel<false, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
                        n_lut, bk, t, out_big, out_acc);
   return hipGetLastError();
-#endif
 }
 
 hipError_t launch_sample_extract_torus(const u64* acc, size_t B, u64* out, hipStream_t s) {

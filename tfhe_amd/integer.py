@@ -88,14 +88,15 @@ Op = Generator[Level, List[np.ndarray], object]
 class Circuit:
     """Runs operator coroutines on an Engine: every yielded level is one batched PBS launch."""
 
-    def __init__(self, engine: Engine, capacity: int = 2048, round_size: int = 1024):
+    def __init__(self, engine: Engine, capacity: int = 2048, round_size: Optional[int] = None):
         self.engine = engine
         self.dim = engine.params.n + 1
         self.lut = engine.gate_lut()
         self.capacity = capacity      # PBS one launch completes in ~one PBS latency (8 x 256 CUs)
-        # PBS per round of the batch kernel (the FFT64 pair kernel: 4 ciphertexts x 256 CUs); a launch of
-        # n PBS costs ~max(1, ceil(n / round_size)) rounds -- the carry-out circuit's cost model
-        self.round_size = round_size
+        # PBS per round of the engine's batch kernel (Engine.round_size: the FFT64 pair kernel holds 4
+        # ciphertexts x 256 CUs per GPU); a launch of n PBS costs ~max(1, ceil(n / round_size)) rounds -- the
+        # carry-out circuit's cost model.  Engines without the property (test doubles) model one P-GATE GPU.
+        self.round_size = round_size or getattr(engine, "round_size", 1024)
         self.pbs_count = 0
         self.launches = 0
 

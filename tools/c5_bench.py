@@ -1,0 +1,74 @@
+"""C5 wall time on one MI355X (BASELINE.json configs[4]: the blind-auction FheUint32 max tree over 256 bidders,
+chained PBS levels): 255 comparisons + selects in lockstep levels, one Engine.pbs launch per circuit level.
+
+Timed: the whole tree after one untimed warm-up tree (host-side bit encryption of the bids is outside), with
+every launch's batch size and wall time (host transfers and the host's circuit bookkeeping included, as an
+application sees it).  Prints ONE JSON line.
+  python tools/c5_bench.py [--bidders 256] [--preset gate_fft|gate] [--reps 2]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import tfhe_amd  # noqa: E402
+from tfhe_amd import integer as I  # noqa: E402
+from tfhe_amd.auction import max_tree  # noqa: E402
+
+
+class _Timed:
+    """Engine proxy that records (batch, ms) of every pbs call."""
+
+    def __init__(self, eng):
+        self._e, self.calls = eng, []
+
+    def pbs(self, cts, lut, idx=None):
+        t = time.perf_counter()
+        out = self._e.pbs(cts, lut) if idx is None else self._e.pbs(cts, lut, idx)
+        self.calls.append((int(cts.shape[0]), round((time.perf_counter() - t) * 1e3, 3)))
+        return out
+
+    def __getattr__(self, k):
+        return getattr(self._e, k)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bidders", type=int, default=256)
+    ap.add_argument("--preset", choices=["gate_fft", "gate"], default="gate_fft")
+    ap.add_argument("--reps", type=int, default=2)
+    a = ap.parse_args()
+    p = tfhe_amd.Params.preset(tfhe_amd.PRESET_GATE_FFT if a.preset == "gate_fft" else tfhe_amd.PRESET_GATE)
+    ck, sk = tfhe_amd.gen_keys(p, 0x7F4E0001)
+    eng = tfhe_amd.Engine(p, 0).load_keys(sk)
+    v = np.random.default_rng(5).integers(0, 2**32, a.bidders, dtype=np.uint64)
+    v[min(77, a.bidders - 1)] = np.uint64(2**32 - 3)
+    runs = []
+    for rep in range(a.reps + 1):
+        te = _Timed(eng)
+        c = I.Circuit(te)
+        bids = I.FheUint.encrypt(c, ck, v, 32, seed=0xB1D + rep, stream0=0)
+        t = time.perf_counter()
+        mx, idx = max_tree(c, bids)
+        wall = time.perf_counter() - t
+        ok = int(mx.decrypt(ck)[0]) == int(v.max()) and int(idx.decrypt(ck)[0]) == int(np.argmax(v))
+        runs.append({"wall_s": round(wall, 4), "pbs": c.pbs_count, "launches": c.launches, "ok": ok,
+                     "calls": te.calls})
+    timed = runs[1:]
+    best = min(timed, key=lambda r: r["wall_s"])
+    print(json.dumps({
+        "metric": f"C5 max-tree wall time, {a.bidders} FheUint32 bidders (255 comparisons + selects), 1 GPU",
+        "value": best["wall_s"], "unit": "s", "higher_is_better": False, "preset": a.preset,
+        "engine_kernels": {"lat_max": "per-shard batches <= the latency threshold run the latency kernel",
+                           "pbs_ms_sum": round(sum(ms for _, ms in best["calls"]), 1)},
+        "walls_s": [r["wall_s"] for r in timed], "warmup_wall_s": runs[0]["wall_s"],
+        "pbs": best["pbs"], "launches": best["launches"], "decrypt_ok": all(r["ok"] for r in runs),
+        "launch_batches_ms": best["calls"]}), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

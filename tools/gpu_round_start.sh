@@ -1,7 +1,7 @@
 #!/bin/bash
 # First GPU session of a round, in two parts (each fits one gpurun call; every GPU step has its own limit,
 # the script stops at the first failure):
-#   PART=1: the whole -m gpu suite, then the noise-squash bench and its rocprofv3 kernel summary
+#   PART=1: the whole -m gpu suite, then the noise-squash bench and its rocprofv3 kernel summary, then the C5 timing
 #   PART=2: the profile set of both FFT64 presets (tools/profile_round.sh: bench line, kernel stats, SQ and
 #           FETCH/WRITE counter passes -> <TAG>_roofline.json tagged with this tree's source_id)
 #   TAG=r04 PART=1 bash tools/gpu_round_start.sh
@@ -18,6 +18,8 @@ if [ "${PART:-1}" = "1" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_sns -o run --output-format csv -- python3 tools/sns_bench.py --batch 1024 --steps 1 > gpurun_out/prof_${TAG}_sns.log 2>&1 || { echo "sns profile failed"; tail -5 gpurun_out/prof_${TAG}_sns.log; exit 1; }
   find gpurun_out/prof_${TAG}_sns -name '*kernel_stats.csv' -exec cp {} gpurun_out/${TAG}_sns_kernel_stats.csv \;
   cut -c1-120 gpurun_out/${TAG}_sns_kernel_stats.csv | head -8
+  timeout -k 10 300 python -u tools/c5_bench.py > gpurun_out/${TAG}_c5_bench.json 2> gpurun_out/${TAG}_c5_bench.err || { echo "c5 bench failed"; tail -10 gpurun_out/${TAG}_c5_bench.err; exit 1; }
+  cut -c1-400 gpurun_out/${TAG}_c5_bench.json
 else
   TAG=${TAG} PRESET=gate_fft bash tools/profile_round.sh > gpurun_out/${TAG}_prof.log 2>&1 || { echo "gate profile failed"; tail -20 gpurun_out/${TAG}_prof.log; exit 1; }
   tail -4 gpurun_out/${TAG}_prof.log

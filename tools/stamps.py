@@ -1,8 +1,7 @@
-"""Phase shares of the FFT64 batch kernels from a diagnostic build:
-    P-FHEVM: tools/ab_build.sh stamps -DF2_STAMPS=1
-             TFHE_HIP_LIB=build_ab/stamps/libtfhe_hip.so python tools/stamps.py
-    P-GATE:  tools/ab_build.sh gstamps -DFFT_STAMPS=1
-             TFHE_HIP_LIB=build_ab/gstamps/libtfhe_hip.so python tools/stamps.py --gate
+"""Phase shares of the P-FHEVM FFT64 batch kernel from a diagnostic build:
+    tools/ab_build.sh stamps -DF2_STAMPS=1
+    TFHE_HIP_LIB=build_ab/stamps/libtfhe_hip.so python tools/stamps.py
+(The P-GATE stamps of round 2 instrumented the retired 8-ciphertext kernel; they left with it.)
 Runs one 4096-PBS launch and prints, per phase of the CMUX loop, the mean cycles per CMUX over the
 sampled waves (every 64th workgroup) and the share of the loop.  Read the shares, not the total (the
 stamps' waits forbid overlaps the shipped kernel has)."""
@@ -19,35 +18,7 @@ PHASES = ["top barrier", "rotate+decomp A", "fwd A", "rotate+decomp B", "vmcnt c
           "MAC0 (+col1 issue)", "vmcnt+barrier col1", "MAC1 + barrier", "inverse 0 + acc", "barrier", "inverse 1 + acc"]
 
 
-GATE_PHASES = ["rotate (x2)", "level barrier (x6)", "digits + twist (x6)", "forward DFT (x6)", "MAC (x6)",
-               "inverse 0 + acc", "inverse 1 + acc", "loop top"]
-
-
-def gate():
-    p = tfhe_amd.Params.preset(tfhe_amd.PRESET_GATE_FFT)
-    ck, sk = tfhe_amd.gen_keys(p, 0x7F4E0001)
-    B = 4096
-    bits = np.random.default_rng(1).integers(0, 2, B).astype(bool)
-    cts = ck.encrypt_bool(bits, seed=3)
-    with tfhe_amd.Engine(p, 0) as eng:
-        eng.load_keys(sk)
-        out = eng.pbs(cts, eng.gate_lut())
-        assert np.array_equal(ck.decrypt_bool(out), bits)
-        buf = np.zeros(16 * 8 * 8, dtype=np.uint64)
-        rc = tfhe_amd.lib().tfhe_hip_debug_fft_stamps(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
-        assert rc == 0, rc
-    buf = buf.reshape(16, 8, 8)
-    tot = buf.astype(np.float64).sum(axis=(0, 1))
-    waves = np.count_nonzero(buf.sum(axis=2))
-    per = tot / max(waves, 1) / p.n
-    for k, name in enumerate(GATE_PHASES):
-        print(f"{name:24s} {per[k]:10.0f} cycles/CMUX  {100 * tot[k] / tot.sum():5.1f} %")
-    print(f"total {per.sum():.0f} cycles per CMUX per wave ({waves} waves sampled)")
-
-
 def main():
-    if "--gate" in sys.argv:
-        return gate()
     p = tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM_FFT)
     ck, sk = tfhe_amd.gen_keys(p, 0x7F4E0001)
     B = 4096
