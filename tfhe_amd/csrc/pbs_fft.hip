@@ -152,7 +152,6 @@ __global__ __launch_bounds__(64) void fft_inv_kernel(const double2* __restrict__
 // per wave, and twice the waves per ciphertext -- a batch of 1024 fills all 256 CUs at 2 waves / SIMD.
 // The MAC order (per-component chains, then one add) is restated in oracle/fft_oracle.c.
 // LDS: 8 x 9 KB transpose areas | 2 x 32 KB level steps | pass A, B, B' tables (24 KB) = 160 KB.
-constexpr int FP_WAVES = 8, FP_CTS = 4;
 // FFT_ROT_BATCH: the rotation's 16 image reads issued together before their first use (measured with the
 // first level peeled: 27.04 -> 27.55 ms per 4096, slower; kept for A/B runs)
 #ifndef FFT_ROT_BATCH
@@ -163,11 +162,25 @@ constexpr int FP_WAVES = 8, FP_CTS = 4;
 #define FFT_PAIR_TWREG 2
 #endif
 constexpr int STEP_C64 = 4 * M;                    // rows (0, q), (1, q), j = 0, 1
+// CTS = ciphertexts per workgroup.  4 (default): 8 waves, one workgroup per CU, tables in LDS, level steps
+// double-buffered.  2 (FFT_PAIR_CTS=2, A/B): 4 waves, TWO independent workgroups per CU (76 KB each: only the
+// inverse's TW_I table in LDS, one level-step buffer), so the two workgroups drift apart and one's LDS
+// phases can overlap the other's VALU phases on every SIMD.
+template <int CTS>
 struct FpShared {
   double2 tw[3 * M];                               // TW_A | TW_B | TW_I of the global table (no twist table)
-  double2 T[FP_WAVES][T_C64];                      // after the tables: T - 8 KB is still inside the block
+  double2 T[2 * CTS][T_C64];                       // after the tables: T - 8 KB is still inside the block
   double2 K[2][STEP_C64];
 };
+template <>
+struct FpShared<2> {
+  double2 twI[M];                                  // TW_I only (passes A, B: registers, loaded from global)
+  double2 K[1][STEP_C64];
+  double2 T[4][T_C64];
+};
+#ifndef FFT_PAIR_CTS
+#define FFT_PAIR_CTS 4
+#endif
 typedef __attribute__((address_space(3))) u64 lds_u64;
 
 // (X^a v - v), v = this wave's polynomial (slot e <-> coefficient 64 e + L), to decomposition states.  The
@@ -235,12 +248,13 @@ __device__ __forceinline__ void exchange_partials(const double (&o0r)[8], const 
   __syncthreads();  // the partner has read this wave's area before the inverse overwrites it
 }
 
-// level step g = 3 i + q: 32 KB in 1 KB blocks; wave w loads blocks 4 w .. 4 w + 3 (16 per component row)
+// level step g = 3 i + q: 32 KB in 1 KB blocks; wave w of NW loads blocks (32 / NW) w .. (16 per component row)
+template <int NW>
 __device__ __forceinline__ void load_step(const double2* __restrict__ bsk, int g, double2* dst, int wave_s, int lane) {
   const int i = g / 3, q = g - 3 * (g / 3);
 #pragma unroll
-  for (int u = 0; u < 4; u++) {
-    const int blk = wave_s * 4 + u;
+  for (int u = 0; u < 32 / NW; u++) {
+    const int blk = wave_s * (32 / NW) + u;
     const int c = blk >> 4;
     const char* src = (const char*)(bsk + ((size_t)i * 6 + c * 3 + q) * (2 * M)) + (blk & 15) * 1024;
     __builtin_amdgcn_global_load_lds((const void*)(src + lane * 16),
@@ -248,15 +262,17 @@ __device__ __forceinline__ void load_step(const double2* __restrict__ bsk, int g
   }
 }
 
-template <bool WRITE_ACC, bool WRITE_BIG>
-__global__ __launch_bounds__(64 * FP_WAVES, 1) void blind_rotate_fft_pair_kernel(
+template <int CTS, bool WRITE_ACC, bool WRITE_BIG>
+__global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kernel(
     const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
     int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tw_g, u64* __restrict__ out_big,
     u64* __restrict__ out_acc) {
-  __shared__ __attribute__((aligned(16))) FpShared sh;
+  constexpr int NW = 2 * CTS;
+  constexpr bool LDS_TW = CTS == 4;
+  __shared__ __attribute__((aligned(16))) FpShared<CTS> sh;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int c = wave & 1;
-  const size_t b_raw = (size_t)blockIdx.x * FP_CTS + (wave >> 1);
+  const size_t b_raw = (size_t)blockIdx.x * CTS + (wave >> 1);
   const bool live = b_raw < B;
   const size_t b = live ? b_raw : B - 1;  // padding pairs run a copy of the last ciphertext, store nothing
   const u64* ct = lwe_in + b * (size_t)(n + 1);
@@ -266,8 +282,12 @@ __global__ __launch_bounds__(64 * FP_WAVES, 1) void blind_rotate_fft_pair_kernel
   const int c_s = wave_s & 1;
   const int n_steps = 3 * n;
 
-  for (int q = threadIdx.x; q < 3 * M; q += 64 * FP_WAVES) sh.tw[q] = tw_g[TW_A + q];
-  load_step(bsk, 0, sh.K[0], wave_s, lane);
+  if constexpr (LDS_TW) {
+    for (int q = threadIdx.x; q < 3 * M; q += 64 * NW) sh.tw[q] = tw_g[TW_A + q];
+    load_step<NW>(bsk, 0, sh.K[0], wave_s, lane);
+  } else {
+    for (int q = threadIdx.x; q < M; q += 64 * NW) sh.twI[q] = tw_g[TW_I + q];
+  }
 
   // acc_c: A = 0, B = X^{-b~} * lut (LUT values in the Z_p encoding, mapped to the torus first)
   u64 acc[16];
@@ -288,9 +308,15 @@ __global__ __launch_bounds__(64 * FP_WAVES, 1) void blind_rotate_fft_pair_kernel
   }
 
   const TBase tb(lane);
-  const double2* twA = sh.tw;
-  const double2* twB = sh.tw + M;
-  const double2* twI = sh.tw + 2 * M;
+  const double2* twA = tw_g + TW_A;
+  const double2* twI;
+  if constexpr (LDS_TW) {
+    twA = sh.tw;
+    twI = sh.tw + 2 * M;
+  } else {
+    twI = sh.twI;
+  }
+  const double2* twB = twA + M;
 #if FFT_PAIR_TWREG
   double2 wa[8];  // pass A's twiddles (twist merged) for the whole CMUX loop: 8 LDS reads fewer per transform
   __syncthreads();
@@ -317,8 +343,14 @@ __global__ __launch_bounds__(64 * FP_WAVES, 1) void blind_rotate_fft_pair_kernel
 #pragma unroll 1
     for (int q = 0; q < 3; q++) {
       const int g = 3 * i + q;
-      glds_barrier();  // step g's chunk is in K[g & 1]; every wave is done with K[(g + 1) & 1]
-      if (g + 1 < n_steps) load_step(bsk, g + 1, sh.K[(g + 1) & 1], wave_s, lane);
+      if constexpr (LDS_TW) {
+        glds_barrier();  // step g's chunk is in K[g & 1]; every wave is done with K[(g + 1) & 1]
+        if (g + 1 < n_steps) load_step<NW>(bsk, g + 1, sh.K[(g + 1) & 1], wave_s, lane);
+      } else {
+        // one buffer: every wave is done with step g - 1's chunk (the exchange's barriers order q = 0)
+        if (q > 0) __syncthreads();
+        load_step<NW>(bsk, g, sh.K[0], wave_s, lane);
+      }
       const u32 bmask = q < 2 ? 1u : 0u;
       double xr[8], xi[8];
 #pragma unroll
@@ -334,7 +366,8 @@ __global__ __launch_bounds__(64 * FP_WAVES, 1) void blind_rotate_fft_pair_kernel
 #else
       dft512_fwd_t<true>(xr, xi, T, lane, tb, twA, twB);
 #endif
-      const double2* k0 = sh.K[g & 1] + c * (2 * M) + lane;
+      if constexpr (!LDS_TW) glds_barrier();  // step g's chunk has landed
+      const double2* k0 = sh.K[LDS_TW ? (g & 1) : 0] + c * (2 * M) + lane;
       const double2* k1 = k0 + M;
 #pragma unroll
       for (int e = 0; e < 8; e++) {
@@ -635,16 +668,17 @@ hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64
                          n_lut, bk, t, out_big, out_acc);
     return hipGetLastError();
   }
-  dim3 grid((unsigned)((B + FP_CTS - 1) / FP_CTS)), block(64 * FP_WAVES);
+  constexpr int CTS = FFT_PAIR_CTS;
+  dim3 grid((unsigned)((B + CTS - 1) / CTS)), block(128 * CTS);
   if (out_acc && out_big)
-    hipLaunchKernelGGL((blind_rotate_fft_pair_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
-                       n_lut, bk, t, out_big, out_acc);
+    hipLaunchKernelGGL((blind_rotate_fft_pair_kernel<CTS, true, true>), grid, block, 0, s, lwe_in, n, B, luts,
+                       lut_index, n_lut, bk, t, out_big, out_acc);
   else if (out_acc)
-    hipLaunchKernelGGL((blind_rotate_fft_pair_kernel<true, false>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
-                       n_lut, bk, t, out_big, out_acc);
+    hipLaunchKernelGGL((blind_rotate_fft_pair_kernel<CTS, true, false>), grid, block, 0, s, lwe_in, n, B, luts,
+                       lut_index, n_lut, bk, t, out_big, out_acc);
   else
-    hipLaunchKernelGGL((blind_rotate_fft_pair_kernel<false, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
-                       n_lut, bk, t, out_big, out_acc);
+    hipLaunchKernelGGL((blind_rotate_fft_pair_kernel<CTS, false, true>), grid, block, 0, s, lwe_in, n, B, luts,
+                       lut_index, n_lut, bk, t, out_big, out_acc);
   return hipGetLastError();
 }
 
