@@ -375,7 +375,7 @@ def main() -> int:
                                       bsk_bytes + B * 8 * ((pd["n"] + 1) + (pd["k"] * pd["N"] + 1))),
                              # the reuse the kernel implements and the true minimum traffic
                              bsk_reuse=(f"each BSK level-step chunk is streamed once per workgroup into LDS and shared "
-                                        f"by its {8 if args.preset == 'gate' else 4} ciphertexts; resident workgroups share it through L2"
+                                        f"by its {dict(gate=8, gate_fft=2).get(args.preset, 4)} ciphertexts; resident workgroups share it through L2"
                                         if "lat" not in br_kernel else
                                         "latency kernel: one ciphertext per workgroup, key words from L2"),
                              min_traffic_bytes_per_pbs=round((bsk_bytes + ksk_bytes) / B + io_bytes),

@@ -137,21 +137,22 @@ __global__ __launch_bounds__(64) void fft_inv_kernel(const double2* __restrict__
 #define FFT_PRIO 1
 #endif
 
-// Component-pair batch kernel (round 3, the default above the latency range): workgroup = 4 ciphertexts x 2
-// waves, wave (p, c) owns COMPONENT c of ciphertext p.  Per CMUX i:
+// Component-pair batch kernel (round 3, the default above the latency range): workgroup = CTS ciphertexts x 2
+// waves (CTS = 2 by default, 4 in round 3), wave (p, c) owns COMPONENT c of ciphertext p.  Per CMUX i:
 //   rotate + decompose acc_c (wave-local: the wave's own transpose area holds the rotation image)
 //   level steps q = 0, 1, 2 (least significant first): digits -> twist -> DFT -> MAC into BOTH outputs'
 //     partial sums  O_j^c = fma chain over q of D_(c,q) (.) BSK_i[(c, q)][j]      (j = 0, 1)
 //     one step's chunk = rows (0, q) and (1, q) of BSK_i (32 KB), streamed once per workgroup by
-//     global_load_lds, double-buffered
+//     global_load_lds (CTS = 4: double-buffered; CTS = 2: one buffer, loaded at the step's start)
 //   exchange: wave c publishes O_(1-c)^c in its transpose area and takes O_c^(1-c) from its partner's:
 //     O_c = O_c^c + O_c^(1-c)  (= O_c^0 + O_c^1: f64 addition commutes, the oracle's split order)
 //   ONE inverse transform: acc_c += rint(iFFT(O_c)) mod 2^64
-// Against the 8-ciphertext kernel above: the same transforms per ciphertext, half of them per wave, one
-// barrier fewer per CMUX (3 chunk steps + 2 for the exchange), 1/2 the accumulator / partial-sum registers
-// per wave, and twice the waves per ciphertext -- a batch of 1024 fills all 256 CUs at 2 waves / SIMD.
+// Against round 2's 8-ciphertext kernel (one wave per ciphertext, retired in round 4): the same transforms per
+// ciphertext, half of them per wave, 1/2 the accumulator / partial-sum registers per wave, and twice the waves
+// per ciphertext -- a batch of 1024 fills all 256 CUs at 2 waves / SIMD.
 // The MAC order (per-component chains, then one add) is restated in oracle/fft_oracle.c.
-// LDS: 8 x 9 KB transpose areas | 2 x 32 KB level steps | pass A, B, B' tables (24 KB) = 160 KB.
+// LDS at CTS = 4: 8 x 9 KB transpose areas | 2 x 32 KB level steps | pass A, B, B' tables (24 KB) = 160 KB;
+// at CTS = 2: B' table (8 KB) | one 32 KB level step | 4 x 9 KB transpose areas = 76 KB, two workgroups per CU.
 // FFT_ROT_BATCH: the rotation's 16 image reads issued together before their first use (measured with the
 // first level peeled: 27.04 -> 27.55 ms per 4096, slower; kept for A/B runs)
 #ifndef FFT_ROT_BATCH
@@ -162,10 +163,11 @@ __global__ __launch_bounds__(64) void fft_inv_kernel(const double2* __restrict__
 #define FFT_PAIR_TWREG 2
 #endif
 constexpr int STEP_C64 = 4 * M;                    // rows (0, q), (1, q), j = 0, 1
-// CTS = ciphertexts per workgroup.  4 (default): 8 waves, one workgroup per CU, tables in LDS, level steps
-// double-buffered.  2 (FFT_PAIR_CTS=2, A/B): 4 waves, TWO independent workgroups per CU (76 KB each: only the
-// inverse's TW_I table in LDS, one level-step buffer), so the two workgroups drift apart and one's LDS
-// phases can overlap the other's VALU phases on every SIMD.
+// CTS = ciphertexts per workgroup.  2 (default since round 4): 4 waves, TWO independent workgroups per CU (76 KB
+// each: only the inverse's TW_I table in LDS, passes A / B from registers, one level-step buffer), so the two
+// workgroups drift apart and one's LDS phases overlap the other's VALU phases on every SIMD: 27.01 -> 26.63 ms per
+// 4096 on the same box (profiles/r04a_cts_ab.txt, two rounds).  4 (FFT_PAIR_CTS=4): 8 waves, one workgroup per CU,
+// all tables in LDS, level steps double-buffered (the round-3 kernel).
 template <int CTS>
 struct FpShared {
   double2 tw[3 * M];                               // TW_A | TW_B | TW_I of the global table (no twist table)
@@ -179,7 +181,7 @@ struct FpShared<2> {
   double2 T[4][T_C64];
 };
 #ifndef FFT_PAIR_CTS
-#define FFT_PAIR_CTS 4
+#define FFT_PAIR_CTS 2
 #endif
 typedef __attribute__((address_space(3))) u64 lds_u64;
 
