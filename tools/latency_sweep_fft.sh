@@ -9,7 +9,7 @@ ck, sk = tfhe_amd.gen_keys(tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM_FFT if f
                            0x7F4E0001)
 eng = tfhe_amd.Engine(ck.params, 0); eng.load_keys(sk)
 lut = eng.generate_accumulator(lambda m: m, 16) if fhevm else eng.gate_lut()
-for B in ((1, 8, 64, 128, 256, 384, 512, 640, 768, 1024) if fhevm else (1, 8, 64, 256, 512, 768, 1024, 1536, 2048)):
+for B in ((1, 8, 64, 128, 256, 384, 512, 640, 768, 1024) if fhevm else (1, 8, 64, 128, 192, 256, 320, 384, 512, 768, 1024, 1536, 2048)):
     cts = ck.encrypt(np.arange(B) % 16, 16, seed=7) if fhevm else ck.encrypt_bool(np.ones(B, dtype=bool), seed=7)
     res = {}
     for name, lm in (("lat", 1 << 20), ("batch", 0)):
