@@ -43,6 +43,18 @@ def test_max_tree_ragged_cleartext():
     assert (int(mx.decrypt(ck)[0]), int(idx.decrypt(ck)[0])) == _expected(v)
 
 
+def test_max_tree_sizes_public_index_bits():
+    """Odd leftovers and every tree shape: public index bits turn into encrypted ones (ge / NOT ge / trivial)
+    exactly where the pairs disagree, and the winner index is right for every bidder count."""
+    for B in (1, 2, 3, 5, 6, 17, 64, 100):
+        for seed in (1, 2):
+            v = np.random.default_rng(B * 10 + seed).integers(0, 16, B, dtype=np.uint64)   # many ties
+            c = I.Circuit(CleartextEngine())
+            mx, idx = max_tree(c, I.FheUint.trivial(c, v, 4))
+            ck = ClearKey()
+            assert (int(mx.decrypt(ck)[0]), int(idx.decrypt(ck)[0])) == _expected(v), (B, seed)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -90,7 +102,9 @@ def test_max_tree_launch_shape():
     """The comparisons' carry-out runs as a block ripple + reduction tree sized by the circuit's cost
     model (tfhe_amd.integer._carry_out), and the select is one level (its OR of exclusive terms is linear):
     61 launches for the 256-bidder tree instead of the ripple's 116 (level 1: 8 chain steps of 896 PBS + 2
-    tree levels instead of 32 steps of 128, then one select launch of 2 x 128 x 40)."""
+    tree levels instead of 32 steps of 128, then one select launch).  The bidder positions are public, so level l
+    selects only the l index bits already encrypted: the first select launch is 2 x 128 x 32 (bids only) instead of
+    2 x 128 x 40, and the tree bootstraps 3,586 ciphertexts fewer (38,168 -> 34,582)."""
     c = I.Circuit(CleartextEngine())
     sizes = []
     pbs = c.engine.pbs
@@ -99,7 +113,8 @@ def test_max_tree_launch_shape():
     mx, idx = max_tree(c, I.FheUint.trivial(c, v, 32))
     assert (int(mx.decrypt(ClearKey())[0]), int(idx.decrypt(ClearKey())[0])) == _expected(v)
     assert c.launches == len(sizes) == 61
-    assert sizes[:11] == [896] * 8 + [384, 128, 10240]
+    assert sizes[:11] == [896] * 8 + [384, 128, 8192]
+    assert c.pbs_count == sum(sizes) == 38_168 - 3_586
     assert [c.carry_block(B, 32) for B in (128, 64, 32, 1)] == [8, 4, 2, 2]
 
 

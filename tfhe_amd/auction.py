@@ -8,44 +8,84 @@ select over the concatenated (bid | index) bits with the shared condition.  All 
 level run in lockstep on the circuit (one PBS launch per circuit level); with a process group the
 level's pairs are sharded over the ranks (one GPU each) and the winners all_gathered
 (tfhe_amd.dist.sharded_map) — the only collective, once per tree level.
+
+The bidder positions are public, so an index bit stays a clear value while both sides of every pair agree
+on it and needs no bootstrap when they differ: ge ? 1 : 0 is the condition itself, ge ? 0 : 1 its negation
+(free).  Only index bits that are already encrypted on some candidate go through the select's two PBS.  In
+the power-of-two tree, level l therefore selects l encrypted index bits instead of all ceil(log2 B): the
+256-bidder tree bootstraps 3,586 fewer ciphertexts (the first level's select launch 10,240 -> 8,192).
 """
 from __future__ import annotations
 
+from typing import List, Tuple
+
 import numpy as np
 
-from .integer import Circuit, FheUint, g_ge, g_select
+from .integer import NOT, Circuit, FheUint, g_ge, g_select
+
+# an index bit column over the current candidates: ("pub", bool values (m,)) or ("enc", ciphertexts (m, dim))
+Col = Tuple[str, np.ndarray]
 
 
 def _level_op(c: Circuit, lhs: np.ndarray, rhs: np.ndarray, w: int):
-    """lhs / rhs: (P, w + iw, dim) = (bid bits | index bits); returns the winners (P, w + iw, dim)."""
+    """lhs / rhs: (P, w + k, dim) = (bid bits | encrypted index bits); returns (P, w + k + 1, dim): the winners'
+    selected columns, then the condition ge = lhs >= rhs."""
     ge = yield from g_ge(c, lhs[:, :w], rhs[:, :w])
-    return (yield from g_select(ge, lhs, rhs))
+    sel = yield from g_select(ge, lhs, rhs)
+    return np.concatenate([sel, ge[:, None]], axis=1)
 
 
 def _run_level(c: Circuit, pairs: np.ndarray, w: int) -> np.ndarray:
     if pairs.shape[0] == 0:
-        return pairs[:, 0]
+        return np.zeros((0, pairs.shape[2] + 1, pairs.shape[3]), dtype=np.uint64)
     return c.run(_level_op(c, np.ascontiguousarray(pairs[:, 0]), np.ascontiguousarray(pairs[:, 1]), w))
+
+
+def _index_level(c: Circuit, cols: List[Col], enc_sel: np.ndarray, ge: np.ndarray, P: int) -> List[Col]:
+    """The winners' index columns: encrypted columns come out of the select (enc_sel, in column order), public
+    columns stay public where every pair agrees, else become ge / NOT(ge) / trivial per pair (no PBS).  The
+    leftover candidate of an odd level (position 2P) keeps its bit."""
+    out, e = [], 0
+    for kind, v in cols:
+        if kind == "enc":
+            out.append(("enc", np.concatenate([enc_sel[:, e], v[2 * P:]], axis=0)))
+            e += 1
+            continue
+        vl, vr = v[0:2 * P:2], v[1:2 * P:2]
+        if np.array_equal(vl, vr):
+            out.append(("pub", np.concatenate([vl, v[2 * P:]])))
+            continue
+        triv = c.trivial(vl)
+        col = np.where((vl & ~vr)[:, None], ge, np.where((~vl & vr)[:, None], NOT(ge), triv))
+        out.append(("enc", np.concatenate([col, c.trivial(v[2 * P:])], axis=0)))
+    return out
 
 
 def max_tree(c: Circuit, bids: FheUint, group=None):
     """Returns (max bid: FheUint of width w, winner index: FheUint of width ceil(log2 B)), batch 1."""
     B, w, dim = bids.bits.shape
     iw = max(1, (B - 1).bit_length())
-    idx = FheUint.trivial(c, np.arange(B, dtype=np.uint64), iw).bits        # public positions
-    cur = np.concatenate([bids.bits, idx], axis=1)                           # (B, w + iw, dim)
+    pos = np.arange(B, dtype=np.int64)
+    cols: List[Col] = [("pub", ((pos >> j) & 1).astype(bool)) for j in range(iw)]   # public positions
+    cur = bids.bits                                                                    # (m, w, dim)
     while cur.shape[0] > 1:
-        P = cur.shape[0] // 2
-        pairs = cur[: 2 * P].reshape(P, 2, w + iw, dim)
+        m = cur.shape[0]
+        P = m // 2
+        enc = [v for kind, v in cols if kind == "enc"]
+        full = np.concatenate([cur] + [v[:, None] for v in enc], axis=1) if enc else cur   # (m, w + k, dim)
+        pairs = full[: 2 * P].reshape(P, 2, full.shape[1], dim)
         if group is None:
-            win = _run_level(c, pairs, w)
+            res = _run_level(c, pairs, w)
         else:
             import torch
 
             from .dist import sharded_map
             t = torch.from_numpy(pairs.view(np.int64).copy())
-            win_t = sharded_map(t, lambda s: torch.from_numpy(
+            res_t = sharded_map(t, lambda s: torch.from_numpy(
                 _run_level(c, s.numpy().view(np.uint64), w).view(np.int64).copy()), group=group)
-            win = win_t.numpy().view(np.uint64).reshape(P, w + iw, dim)
-        cur = np.concatenate([win, cur[2 * P:]], axis=0)                      # odd leftover advances
-    return FheUint(c, cur[:, :w]), FheUint(c, cur[:, w:])
+            res = res_t.numpy().view(np.uint64).reshape(P, full.shape[1] + 1, dim)
+        win, ge = res[:, :-1], res[:, -1]
+        cols = _index_level(c, cols, win[:, w:], ge, P)
+        cur = np.concatenate([win[:, :w], cur[2 * P:]], axis=0)                          # odd leftover advances
+    idx = np.stack([v[0] if kind == "enc" else c.trivial(v[:1])[0] for kind, v in cols], axis=0)[None]
+    return FheUint(c, cur[:, :w]), FheUint(c, idx)

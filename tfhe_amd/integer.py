@@ -43,12 +43,21 @@ WIDTHS = (8, 16, 32, 64, 128, 160, 256)   # ebool / euint* / eaddress of fhEVM (
 # linear combinations (all arithmetic mod 2^64, vectorised over any leading shape)
 # --------------------------------------------------------------------------------------------
 def _lin(terms, const: int = 0) -> np.ndarray:
+    """sum w * c + const on the body, mod 2^64, in one fresh array (weights +-1 as in-place adds / subtracts: the
+    circuits' levels are tens of MB, so the host time between launches is these passes)."""
     with np.errstate(over="ignore"):
         out = None
         for w, c in terms:
-            t = c * np.uint64(w % _M64)
-            out = t if out is None else out + t
-        out = np.array(out, dtype=np.uint64, copy=True)
+            w %= _M64
+            if out is None:
+                out = (np.array(c, dtype=np.uint64, copy=True) if w == 1 else
+                       np.subtract(np.uint64(0), c, dtype=np.uint64) if w == _M64 - 1 else c * np.uint64(w))
+            elif w == 1:
+                np.add(out, c, out=out)
+            elif w == _M64 - 1:
+                np.subtract(out, c, out=out)
+            else:
+                np.add(out, c * np.uint64(w), out=out)
         out[..., -1] += np.uint64(const % _M64)
     return out
 
@@ -75,7 +84,7 @@ def XOR3(a, b, c):
 
 def NOT(a):
     with np.errstate(over="ignore"):
-        return (np.uint64(0) - a).astype(np.uint64)
+        return np.subtract(np.uint64(0), a, dtype=np.uint64)
 
 
 # --------------------------------------------------------------------------------------------
@@ -317,7 +326,7 @@ def g_select(cond: np.ndarray, x: np.ndarray, y: np.ndarray) -> Op:
     = 1/8): the OR needs no bootstrap.  The result carries the noise of two PBS outputs, still far inside
     the 1/8 decision margin of any gate it feeds."""
     cw = np.broadcast_to(cond[:, None, :], x.shape)
-    t, f = yield [AND(cw, x), AND(NOT(cw), y)]
+    t, f = yield [AND(cw, x), _lin([(-1, cw), (1, y)], -MU)]      # AND(cw, x), AND(NOT cw, y)
     return OR(t, f)
 
 
