@@ -436,12 +436,97 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
 // instead of 6 + 2 + all of it.  LDS (tables first: small DS immediates): tw 32 KB | acc 16 KB |
 // F 48 KB | 6 transpose areas 54 KB (O_0, O_1 alias areas 2, 3, dead after phase A) = 150 KB.
 constexpr int FL_THREADS = 512;
+constexpr int FL_MAXN = 1024;  // rotation amounts staged in LDS up to this LWE dimension (global reads above)
 struct FftLatShared {
   double2 tw[TW_C64];
   u64 A[2][N1K];
   double2 F[6][M];
   double2 T[6][T_C64];
+  unsigned short ab[FL_MAXN];  // ms2048(ct[i]) for every CMUX
 };
+
+#ifndef FFT_LAT_PREFETCH
+#define FFT_LAT_PREFETCH 1
+#endif
+__device__ __forceinline__ void lat_load_key(const double2* __restrict__ bsk, int i, int j, int s0, int lane,
+                                             double2 (&kv)[6][2]) {
+#pragma unroll
+  for (int r = 0; r < 6; r++)
+#pragma unroll
+    for (int t = 0; t < 2; t++) kv[r][t] = bsk[((size_t)(i * 6 + r) * 2 + j) * M + 64 * (s0 + t) + lane];
+}
+
+// one CMUX of the latency kernel (phases A, B, C and their three barriers)
+__device__ __forceinline__ void lat_cmux(FftLatShared& sh, const u64* __restrict__ ct, int i, int wave, int lane,
+                                         TBase tb, int j, int s0, const double2 (&kv)[6][2]) {
+  const int a = i < FL_MAXN ? (int)sh.ab[i] : ms2048(ct[i]);
+  if (wave < 6) {  // phase A
+    const int c = wave / 3, q = wave % 3;
+    const u64* acc = sh.A[c];
+    u32 st[16];
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      const int t = 64 * e + lane - a + 2 * N1K;
+      const u64 x = acc[t & (N1K - 1)];
+      const u64 r = (t & N1K) ? 0 - x : x;
+      st[e] = decomp_state(r - acc[64 * e + lane]);
+    }
+    int dg[16];
+    for (int qq = 0; qq <= q; qq++) {
+      const u32 bmask = qq < 2 ? 1u : 0u;
+#pragma unroll
+      for (int e = 0; e < 16; e++) dg[e] = decomp_step(st[e], bmask);
+    }
+    double xr[8], xi[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      xr[e] = (double)dg[e];
+      xi[e] = (double)dg[e + 8];
+    }
+    twist_slots<false>(xr, xi);
+    dft512_fwd<true>(xr, xi, sh.T[wave], lane, tb, sh.tw);
+#pragma unroll
+    for (int e = 0; e < 8; e++) sh.F[wave][64 * e + lane] = make_double2(xr[e], xi[e]);
+  }
+  __syncthreads();
+  {  // phase B
+    double2* O = sh.T[2 + j];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      const int e = s0 + t;
+      double re[2] = {0.0, 0.0}, im[2] = {0.0, 0.0};  // per-component chains, then one add (oracle order)
+#pragma unroll
+      for (int r = 0; r < 6; r++) {
+        const double2 D = sh.F[r][64 * e + lane], K = kv[r][t];
+        const int cc = r / 3;
+        re[cc] = __builtin_fma(D.x, K.x, re[cc]);
+        re[cc] = __builtin_fma(-D.y, K.y, re[cc]);
+        im[cc] = __builtin_fma(D.x, K.y, im[cc]);
+        im[cc] = __builtin_fma(D.y, K.x, im[cc]);
+      }
+      O[64 * e + lane] = make_double2(re[0] + re[1], im[0] + im[1]);
+    }
+  }
+  __syncthreads();
+  if (wave < 2) {  // phase C
+    const double2* O = sh.T[2 + wave];
+    double xr[8], xi[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const double2 v = O[64 * e + lane];
+      xr[e] = v.x;
+      xi[e] = v.y;
+    }
+    fft_inv_real(xr, xi, sh.T[wave], lane, tb, sh.tw);
+    u64* acc = sh.A[wave];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      acc[64 * e + lane] += f64_to_torus(xr[e]);
+      acc[64 * (e + 8) + lane] += f64_to_torus(xi[e]);
+    }
+  }
+  __syncthreads();
+}
 
 template <bool WRITE_ACC, bool WRITE_BIG>
 __global__ __launch_bounds__(FL_THREADS, 1) void blind_rotate_fft_lat_kernel(
@@ -455,6 +540,7 @@ __global__ __launch_bounds__(FL_THREADS, 1) void blind_rotate_fft_lat_kernel(
   const TBase tb(lane);
 
   for (int q = threadIdx.x; q < TW_C64; q += FL_THREADS) sh.tw[q] = tw_g[q];
+  for (int q = threadIdx.x; q < n && q < FL_MAXN; q += FL_THREADS) sh.ab[q] = (unsigned short)ms2048(ct[q]);
   {
     int li = lut_index ? (int)lut_index[b] : 0;
     li = (li < 0 || li >= n_lut) ? 0 : li;
@@ -473,81 +559,25 @@ __global__ __launch_bounds__(FL_THREADS, 1) void blind_rotate_fft_lat_kernel(
   __syncthreads();
 
   const int j = wave >> 2, s0 = (wave & 3) * 2;  // phase B: output j, slots s0, s0 + 1
-  for (int i = 0; i < n; i++) {
-    const int a = ms2048(ct[i]);
-    // phase-B key words of this CMUX, requested now, consumed after phase A
-    double2 kv[6][2];
-#pragma unroll
-    for (int r = 0; r < 6; r++)
-#pragma unroll
-      for (int t = 0; t < 2; t++) kv[r][t] = bsk[((size_t)(i * 6 + r) * 2 + j) * M + 64 * (s0 + t) + lane];
-    if (wave < 6) {  // phase A
-      const int c = wave / 3, q = wave % 3;
-      const u64* acc = sh.A[c];
-      u32 st[16];
-#pragma unroll
-      for (int e = 0; e < 16; e++) {
-        const int t = 64 * e + lane - a + 2 * N1K;
-        const u64 x = acc[t & (N1K - 1)];
-        const u64 r = (t & N1K) ? 0 - x : x;
-        st[e] = decomp_state(r - acc[64 * e + lane]);
-      }
-      int dg[16];
-      for (int qq = 0; qq <= q; qq++) {
-        const u32 bmask = qq < 2 ? 1u : 0u;
-#pragma unroll
-        for (int e = 0; e < 16; e++) dg[e] = decomp_step(st[e], bmask);
-      }
-      double xr[8], xi[8];
-#pragma unroll
-      for (int e = 0; e < 8; e++) {
-        xr[e] = (double)dg[e];
-        xi[e] = (double)dg[e + 8];
-      }
-      twist_slots<false>(xr, xi);
-      dft512_fwd<true>(xr, xi, sh.T[wave], lane, tb, sh.tw);
-#pragma unroll
-      for (int e = 0; e < 8; e++) sh.F[wave][64 * e + lane] = make_double2(xr[e], xi[e]);
-    }
-    __syncthreads();
-    {  // phase B
-      double2* O = sh.T[2 + j];
-#pragma unroll
-      for (int t = 0; t < 2; t++) {
-        const int e = s0 + t;
-        double re[2] = {0.0, 0.0}, im[2] = {0.0, 0.0};  // per-component chains, then one add (oracle order)
-#pragma unroll
-        for (int r = 0; r < 6; r++) {
-          const double2 D = sh.F[r][64 * e + lane], K = kv[r][t];
-          const int cc = r / 3;
-          re[cc] = __builtin_fma(D.x, K.x, re[cc]);
-          re[cc] = __builtin_fma(-D.y, K.y, re[cc]);
-          im[cc] = __builtin_fma(D.x, K.y, im[cc]);
-          im[cc] = __builtin_fma(D.y, K.x, im[cc]);
-        }
-        O[64 * e + lane] = make_double2(re[0] + re[1], im[0] + im[1]);
-      }
-    }
-    __syncthreads();
-    if (wave < 2) {  // phase C
-      const double2* O = sh.T[2 + wave];
-      double xr[8], xi[8];
-#pragma unroll
-      for (int e = 0; e < 8; e++) {
-        const double2 v = O[64 * e + lane];
-        xr[e] = v.x;
-        xi[e] = v.y;
-      }
-      fft_inv_real(xr, xi, sh.T[wave], lane, tb, sh.tw);
-      u64* acc = sh.A[wave];
-#pragma unroll
-      for (int e = 0; e < 8; e++) {
-        acc[64 * e + lane] += f64_to_torus(xr[e]);
-        acc[64 * (e + 8) + lane] += f64_to_torus(xi[e]);
-      }
-    }
-    __syncthreads();
+#if FFT_LAT_PREFETCH
+  // key words one CMUX ahead (two register sets, the loop unrolled by two): a CMUX's row arrives while the
+  // previous CMUX runs instead of behind this CMUX's phase A
+  double2 kva[6][2], kvb[6][2];
+  lat_load_key(bsk, 0, j, s0, lane, kva);
+  for (int i = 0; i < n; i += 2) {
+    if (i + 1 < n) lat_load_key(bsk, i + 1, j, s0, lane, kvb);
+    lat_cmux(sh, ct, i, wave, lane, tb, j, s0, kva);
+    if (i + 1 >= n) break;
+    if (i + 2 < n) lat_load_key(bsk, i + 2, j, s0, lane, kva);
+    lat_cmux(sh, ct, i + 1, wave, lane, tb, j, s0, kvb);
   }
+#else
+  for (int i = 0; i < n; i++) {
+    double2 kv[6][2];  // phase-B key words of this CMUX, requested now, consumed after phase A
+    lat_load_key(bsk, i, j, s0, lane, kv);
+    lat_cmux(sh, ct, i, wave, lane, tb, j, s0, kv);
+  }
+#endif
 
   if (WRITE_ACC) {
     u64* oa = out_acc + b * 2048;

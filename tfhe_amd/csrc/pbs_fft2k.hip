@@ -720,11 +720,17 @@ __global__ __launch_bounds__(F2_THREADS, 1) void blind_rotate_fft2k_kernel(
 // Five barriers per CMUX.  LDS: table 48 KB | acc 32 KB | F 32 KB | 4 transpose areas 36 KB (O
 // aliases them between phase B and the uncombine) = 148 KB.
 constexpr int F2L_THREADS = 512;
+constexpr int F2L_MAXN = 1024;  // rotation amounts staged in LDS up to this LWE dimension (global reads above)
+// F2L_PREFETCH: the key words of CMUX i + 1 requested while CMUX i runs (two register sets, loop unrolled by 2)
+#ifndef F2L_PREFETCH
+#define F2L_PREFETCH 1
+#endif
 struct F2LatShared {
   double2 tw[G_C64];
   u64 A[2][N2];        // split layout: coefficient c at (c & 1) * 1024 + (c >> 1)
   double2 F[2][M2];    // spectra, device order (index h * 512 + 64 s + L)
   double2 T[4][T_C64];  // transposes; O_0, O_1 (2 x 1024 complex) alias T[0..3] after phase A
+  unsigned short ab[F2L_MAXN];  // ms4096(ct[i]) for every CMUX
 };
 
 template <bool WRITE_ACC, bool WRITE_BIG>
@@ -741,6 +747,7 @@ __global__ __launch_bounds__(F2L_THREADS, 1) void blind_rotate_fft2k_lat_kernel(
   double2* O = sh.T[0];  // 2 x 1024 complex across the four transpose areas
 
   for (int q = threadIdx.x; q < G_C64; q += F2L_THREADS) sh.tw[q] = tg[q];
+  for (int q = threadIdx.x; q < n && q < F2L_MAXN; q += F2L_THREADS) sh.ab[q] = (unsigned short)ms4096(ct[q]);
   {
     int li = lut_index ? (int)lut_index[b] : 0;
     li = (li < 0 || li >= n_lut) ? 0 : li;
@@ -760,13 +767,14 @@ __global__ __launch_bounds__(F2L_THREADS, 1) void blind_rotate_fft2k_lat_kernel(
 
   const int j = wave >> 2, sb = (wave & 3) * 4;  // phase B: output j, slots sb .. sb + 3 of 16
   const int c = (wave >> 1) & 1, h = wave & 1;   // phases A / C (waves 0..3): component or output, parity
-  for (int i = 0; i < n; i++) {
-    const int a = ms4096(ct[i]);
-    double2 kv[2][4];
+  auto load_key = [&](int i, double2 (&kv)[2][4]) {
 #pragma unroll
     for (int cc = 0; cc < 2; cc++)
 #pragma unroll
       for (int t = 0; t < 4; t++) kv[cc][t] = bsk[((size_t)(i * 2 + cc) * 2 + j) * M2 + 64 * (sb + t) + lane];
+  };
+  auto cmux = [&](int i, const double2 (&kv)[2][4]) {
+    const int a = i < F2L_MAXN ? (int)sh.ab[i] : ms4096(ct[i]);
     // ---- phase A
     double xr[8], xi[8];
     if (wave < 4) {
@@ -852,7 +860,24 @@ __global__ __launch_bounds__(F2L_THREADS, 1) void blind_rotate_fft2k_lat_kernel(
       }
     }
     __syncthreads();
+  };
+#if F2L_PREFETCH
+  double2 kva[2][4], kvb[2][4];
+  load_key(0, kva);
+  for (int i = 0; i < n; i += 2) {
+    if (i + 1 < n) load_key(i + 1, kvb);
+    cmux(i, kva);
+    if (i + 1 >= n) break;
+    if (i + 2 < n) load_key(i + 2, kva);
+    cmux(i + 1, kvb);
   }
+#else
+  for (int i = 0; i < n; i++) {
+    double2 kv[2][4];
+    load_key(i, kv);
+    cmux(i, kv);
+  }
+#endif
 
   if (WRITE_ACC) {
     u64* oa = out_acc + b * (2 * N2);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # FFT64: PBS time per batch for the latency kernel vs the batch kernel (crossover for lat_max).
-#   PRESET=gate (default) | fhevm
+#   PRESET=gate (default) | fhevm, BATCHES=1,64,256 (default: the full grid), TFHE_HIP_LIB=<variant .so>
 cd "${GRAFT_REPO_ROOT:-.}"
 PRESET=${PRESET:-gate} python - <<'PY'
 import os, time, numpy as np, tfhe_amd
@@ -9,7 +9,10 @@ ck, sk = tfhe_amd.gen_keys(tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM_FFT if f
                            0x7F4E0001)
 eng = tfhe_amd.Engine(ck.params, 0); eng.load_keys(sk)
 lut = eng.generate_accumulator(lambda m: m, 16) if fhevm else eng.gate_lut()
-for B in ((1, 8, 64, 128, 256, 384, 512, 640, 768, 1024) if fhevm else (1, 8, 64, 128, 192, 256, 320, 384, 512, 768, 1024, 1536, 2048)):
+Bs = os.environ.get("BATCHES")
+for B in (tuple(int(x) for x in Bs.split(",")) if Bs else
+          (1, 8, 64, 128, 256, 384, 512, 640, 768, 1024) if fhevm else
+          (1, 8, 64, 128, 192, 256, 320, 384, 512, 768, 1024, 1536, 2048)):
     cts = ck.encrypt(np.arange(B) % 16, 16, seed=7) if fhevm else ck.encrypt_bool(np.ones(B, dtype=bool), seed=7)
     res = {}
     for name, lm in (("lat", 1 << 20), ("batch", 0)):
