@@ -58,6 +58,9 @@
 #include "tfhe_oracle.h"
 
 #define FFT_M 512
+/* N = 2048: 1 = the round-1..3 two-wave transform (512-point halves + combine), 0 = the one-wave 1024-point
+ * transform of round 4 (set by tests comparing the two; the device runs the round-4 one) */
+int or_fft2k_legacy = 1;
 
 /* ---- twiddles: fixed series in plain double (no libm), |x| <= pi/4 ------------------------ */
 static double fs_sin(double x) {
@@ -310,8 +313,150 @@ static void fft2k_inv(const or_c64* in, double* out) {
   }
 }
 
+/* ---- N = 2048, one wave per polynomial (round 4, pbs_fft2k.hip / fft1k.h) ------------------------
+ * M = 1024 = 16 x 4 x 16 over the device's 64-lane x 16-slot grid, natural input n = L + 64 e:
+ *   z_n = (a_n + i a_{n+1024}) zeta^n, zeta = e^{2 pi i / 4096}: the slot part zeta^{64 e} multiplies slot e > 0,
+ *   the lane part zeta^L rides in pass A's table
+ *   A  lane L: DFT16 over e -> k1, then x[k1] *= ta[k1][L] = zeta^{L (1 + 4 k1)}        (every k1)
+ *   X  register exchange (v_permlane32_swap / v_permlane16_swap): slot bit 3 <-> lane bit 5, slot bit 2 <->
+ *      lane bit 4, so lane L' = l0 + 16 (k1 >> 2) holds slot s' = (k1 & 3) + 4 l1   (L = l0 + 16 l1)
+ *   B  per g = k1 & 3: radix-4 over l1 (slots g + 4 l1) -> m0 (slots g + 4 m0), then x *= tb[m0][l0] =
+ *      e^{2 pi i l0 m0 / 64}                                                          (m0 > 0)
+ *   T  LDS transpose: lane L'' = s' + 16 (L' >> 4) holds slot l0
+ *   C  DFT16 over l0 -> m1: slot m1 of lane L'' = Z[k], k = (L''&3) + 4 (L''>>4) + 16 ((L''>>2)&3) + 64 m1,
+ *      stored at device index L'' + 64 m1
+ *   inverse: C' (inverse DFT16), T back, conj tb + inverse radix-4, X back, conj ta, inverse DFT16 (A'),
+ *      conj(zeta^{64 e}) for e > 0; no 1/M (2^-10 is folded into the BSK)
+ * DFT16 (natural in and out): radix-4 over n1 for each n0 (positions n0 + 4 k0), x[n0 + 4 k0] *= W16^{n0 k0}
+ * (n0, k0 > 0: W^1 = (C16, S16), W^3 = (S16, C16), W^9 = (-C16, -S16) as cmul; W^2, W^6 as the w8 forms; W^4 = i),
+ * radix-4 over n0 for each k0 (positions 4 k0 + k1) -> X[k0 + 4 k1].  radix-4 (a, b, c, d): t0 = a + c,
+ * t1 = a - c, t2 = b + d, t3 = b - d; X0 = t0 + t2, X2 = t0 - t2, X1 = t1 + i t3, X3 = t1 - i t3 (inverse:
+ * X1 = t1 - i t3, X3 = t1 + i t3).  The inverse DFT16 is the same with conjugate twiddles. */
+#define C16 0.92387953251128675613
+#define S16 0.38268343236508977173
+typedef struct fft1k_tab {
+  or_c64 slot[16];    /* zeta^{64 e} */
+  or_c64 ta[16][64];  /* zeta^{L (1 + 4 k)} */
+  or_c64 tb[4][16];   /* zeta^{64 l0 m} = e^{2 pi i l0 m / 64} */
+} fft1k_tab;
+static fft1k_tab g_tab1k;
+static int g_tab1k_ready = 0;
+
+static const fft1k_tab* tab1k(void) {
+#pragma omp critical(or_fft_tab1k)
+  {
+    if (!g_tab1k_ready) {
+      for (uint32_t e = 0; e < 16; e++) or_fft_twiddle(64 * e, 4096, &g_tab1k.slot[e].re, &g_tab1k.slot[e].im);
+      for (uint32_t k = 0; k < 16; k++)
+        for (uint32_t L = 0; L < 64; L++)
+          or_fft_twiddle((L * (1 + 4 * k)) % 4096, 4096, &g_tab1k.ta[k][L].re, &g_tab1k.ta[k][L].im);
+      for (uint32_t m = 0; m < 4; m++)
+        for (uint32_t l = 0; l < 16; l++)
+          or_fft_twiddle((64 * l * m) % 4096, 4096, &g_tab1k.tb[m][l].re, &g_tab1k.tb[m][l].im);
+      __atomic_store_n(&g_tab1k_ready, 1, __ATOMIC_RELEASE);
+    }
+  }
+  return &g_tab1k;
+}
+
+static inline or_c64 cmulc(or_c64 z, or_c64 w) { return cmul(z, w.re, -w.im); }
+
+static void radix4(or_c64* x, int i0, int st, int inv) {
+  const or_c64 a = x[i0], b = x[i0 + st], c = x[i0 + 2 * st], d = x[i0 + 3 * st];
+  const or_c64 t0 = cadd(a, c), t1 = csub(a, c), t2 = cadd(b, d), t3 = csub(b, d);
+  x[i0] = cadd(t0, t2);
+  x[i0 + 2 * st] = csub(t0, t2);
+  const or_c64 p = {t1.re - t3.im, t1.im + t3.re}, q = {t1.re + t3.im, t1.im - t3.re}; /* t1 + i t3, t1 - i t3 */
+  x[i0 + st] = inv ? q : p;
+  x[i0 + 3 * st] = inv ? p : q;
+}
+
+/* t * W16^k (inv: conj), k in {1, 2, 3, 4, 6, 9} */
+static inline or_c64 w16(or_c64 t, int k, int inv) {
+  const double p = t.re, q = t.im;
+  or_c64 r;
+  switch (k) {
+    case 1: return inv ? cmul(t, C16, -S16) : cmul(t, C16, S16);
+    case 3: return inv ? cmul(t, S16, -C16) : cmul(t, S16, C16);
+    case 9: return inv ? cmul(t, -C16, S16) : cmul(t, -C16, -S16);
+    case 2: return w8(t, 1, inv);
+    case 6: return w8(t, 3, inv);
+    default: /* 4: i */
+      if (!inv) { r.re = -q; r.im = p; } else { r.re = q; r.im = -p; }
+      return r;
+  }
+}
+
+static void dft16(or_c64 x[16], int inv) {
+  static const int K[16] = {0, 0, 0, 0, 0, 1, 2, 3, 0, 2, 4, 6, 0, 3, 6, 9}; /* n0 k0 at position n0 + 4 k0 */
+  for (int n0 = 0; n0 < 4; n0++) radix4(x, n0, 4, inv);
+  for (int pos = 5; pos < 16; pos++)
+    if ((pos & 3) && (pos >> 2)) x[pos] = w16(x[pos], K[(pos >> 2) * 4 + (pos & 3)], inv);
+  for (int k0 = 0; k0 < 4; k0++) radix4(x, 4 * k0, 1, inv);
+  or_c64 y[16];
+  for (int k0 = 0; k0 < 4; k0++)
+    for (int k1 = 0; k1 < 4; k1++) y[k0 + 4 * k1] = x[4 * k0 + k1];
+  memcpy(x, y, sizeof(y));
+}
+
+static void fft1k_fwd(const double* a, or_c64* out) {
+  const fft1k_tab* T = tab1k();
+  static _Thread_local or_c64 X[64][16], Y[64][16];
+  for (int L = 0; L < 64; L++) {
+    or_c64* x = X[L];
+    for (int e = 0; e < 16; e++) {
+      const or_c64 v = {a[L + 64 * e], a[L + 64 * e + 1024]};
+      x[e] = e ? cmul(v, T->slot[e].re, T->slot[e].im) : v;
+    }
+    dft16(x, 0);
+    for (int k = 0; k < 16; k++) x[k] = cmul(x[k], T->ta[k][L].re, T->ta[k][L].im);
+  }
+  for (int Lp = 0; Lp < 64; Lp++) /* register exchange */
+    for (int sp = 0; sp < 16; sp++) Y[Lp][sp] = X[(Lp & 15) | ((sp >> 2) << 4)][(sp & 3) | ((Lp >> 4) << 2)];
+  for (int Lp = 0; Lp < 64; Lp++) { /* pass B */
+    or_c64* y = Y[Lp];
+    for (int g = 0; g < 4; g++) {
+      radix4(y, g, 4, 0);
+      for (int m = 1; m < 4; m++) y[g + 4 * m] = cmul(y[g + 4 * m], T->tb[m][Lp & 15].re, T->tb[m][Lp & 15].im);
+    }
+  }
+  for (int Lpp = 0; Lpp < 64; Lpp++) { /* transpose + pass C */
+    or_c64 z[16];
+    for (int r = 0; r < 16; r++) z[r] = Y[r + 16 * (Lpp >> 4)][Lpp & 15];
+    dft16(z, 0);
+    for (int m = 0; m < 16; m++) out[Lpp + 64 * m] = z[m];
+  }
+}
+
+static void fft1k_inv(const or_c64* in, double* a) {
+  const fft1k_tab* T = tab1k();
+  static _Thread_local or_c64 X[64][16], Y[64][16], Z[64][16];
+  for (int Lpp = 0; Lpp < 64; Lpp++) { /* pass C' */
+    for (int m = 0; m < 16; m++) Z[Lpp][m] = in[Lpp + 64 * m];
+    dft16(Z[Lpp], 1);
+  }
+  for (int Lp = 0; Lp < 64; Lp++) { /* transpose back, conj tb, inverse radix-4 */
+    or_c64* y = Y[Lp];
+    for (int sp = 0; sp < 16; sp++) y[sp] = Z[sp + 16 * (Lp >> 4)][Lp & 15];
+    for (int g = 0; g < 4; g++) {
+      for (int m = 1; m < 4; m++) y[g + 4 * m] = cmulc(y[g + 4 * m], T->tb[m][Lp & 15]);
+      radix4(y, g, 4, 1);
+    }
+  }
+  for (int L = 0; L < 64; L++) { /* exchange back, conj ta, pass A', untwist */
+    or_c64* x = X[L];
+    for (int k = 0; k < 16; k++) x[k] = cmulc(Y[(L & 15) | ((k >> 2) << 4)][(k & 3) | ((L >> 4) << 2)], T->ta[k][L]);
+    dft16(x, 1);
+    for (int e = 0; e < 16; e++) {
+      const or_c64 v = e ? cmulc(x[e], T->slot[e]) : x[e];
+      a[L + 64 * e] = v.re;
+      a[L + 64 * e + 1024] = v.im;
+    }
+  }
+}
+
 void or_fft_fwd(const double* a, uint32_t N, or_c64* out) {
-  if (N == 4 * FFT_M) { fft2k_fwd(a, out); return; }
+  if (N == 4 * FFT_M) { if (or_fft2k_legacy) fft2k_fwd(a, out); else fft1k_fwd(a, out); return; }
   if (N != 2 * FFT_M) abort();
   const fft_tab* T = tab();
   or_c64 z[FFT_M];
@@ -324,7 +469,7 @@ void or_fft_fwd(const double* a, uint32_t N, or_c64* out) {
 }
 
 void or_fft_inv(const or_c64* in, uint32_t N, double* out) {
-  if (N == 4 * FFT_M) { fft2k_inv(in, out); return; }
+  if (N == 4 * FFT_M) { if (or_fft2k_legacy) fft2k_inv(in, out); else fft1k_inv(in, out); return; }
   if (N != 2 * FFT_M) abort();
   const fft_tab* T = tab();
   or_c64 z[FFT_M];

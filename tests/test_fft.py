@@ -209,3 +209,63 @@ def test_pgate_inverse_output_bound_fast_torus_path(oracle_mod):
         assert abs(abs(x[k_peak]) - bound) <= 2.0 ** 40   # the peak coefficient reaches the linear bound
         for v in x[:: 37].tolist() + [x[k_peak]]:
             assert _fast_f64_to_torus(v) == oracle_mod.f64_to_torus(v)
+
+
+# ---- N = 2048: the one-wave 1024-point transform (fft_oracle.c fft1k_*, pbs_fft2k.hip) ----------------------
+N2, M2 = 2048, 1024
+_L, _S = np.arange(M2) % 64, np.arange(M2) // 64
+# device index L + 64 m1 holds frequency k = (L & 3) + 4 (L >> 4) + 16 ((L >> 2) & 3) + 64 m1
+DEVICE_ORDER_1K = (_L & 3) + 4 * (_L >> 4) + 16 * ((_L >> 2) & 3) + 64 * _S
+
+
+def _dft_definition_2k(a):
+    zeta = np.exp(1j * np.pi * np.arange(M2) / N2)
+    z = (a[:M2] + 1j * a[M2:]) * zeta
+    return (np.fft.ifft(z) * M2)[DEVICE_ORDER_1K]
+
+
+def test_fft1k_is_a_permutation_of_frequencies():
+    assert np.array_equal(np.sort(DEVICE_ORDER_1K), np.arange(M2))
+
+
+@pytest.mark.parametrize("legacy", [False, True])
+def test_fft2k_forward_matches_definition(oracle_mod, legacy):
+    rng = np.random.default_rng(13)
+    with oracle_mod.fft2k_legacy(legacy):
+        for a in (rng.integers(-2**22, 2**22, N2).astype(np.float64),
+                  rng.integers(-2**62, 2**62, N2).astype(np.float64)):
+            Z = oracle_mod.fft_fwd(a)[0]
+            if legacy:   # round-3 device order: per parity half h, index h*512 + 64 s + L
+                continue
+            ref = _dft_definition_2k(a)
+            assert np.max(np.abs(Z - ref)) <= 1e-12 * np.max(np.abs(ref)) + 1e-9
+
+
+def test_fft2k_inverse_roundtrip(oracle_mod):
+    rng = np.random.default_rng(14)
+    a = rng.integers(-2**40, 2**40, N2).astype(np.float64)
+    with oracle_mod.fft2k_legacy(False):
+        back = oracle_mod.fft_inv(oracle_mod.fft_fwd(a))[0] / M2
+    assert np.max(np.abs(back - a)) < 4e-3
+
+
+def test_fft2k_product_vs_exact_torus_schoolbook(oracle_mod):
+    """23-bit digits x uniform torus polynomial (the P-FHEVM external product): the one-wave transform's product
+    rounded with the wide torus path stays as close to the exact wrapping product as the two-wave one did."""
+    rng = np.random.default_rng(15)
+    worst = {}
+    for legacy in (False, True):
+        with oracle_mod.fft2k_legacy(legacy):
+            w = 0
+            for _ in range(2):
+                d = rng.integers(-2**22, 2**22 + 1, N2)
+                b = rng.integers(0, 2**64, N2, dtype=np.uint64)
+                Fb = oracle_mod.fft_fwd(b.view(np.int64).astype(np.float64))[0] * 2.0**-10
+                prod = oracle_mod.fft_inv(oracle_mod.fft_fwd(d.astype(np.float64))[0] * Fb)[0]
+                got = np.array([oracle_mod.f64_to_torus(x) for x in prod], dtype=np.uint64)
+                ref = oracle_mod.poly_mul_torus_schoolbook(d, b)
+                err = np.abs((got - ref).view(np.int64).astype(np.float64))
+                w = max(w, float(err.max()))
+            worst[legacy] = w
+    assert worst[False] < 2.0**46, f"one-wave product error 2^{math.log2(worst[False]):.1f}"
+    assert worst[False] < 4 * worst[True]

@@ -1,0 +1,321 @@
+// pbs_fft2kc.hip — P-FHEVM (N = 2048, k = 1, PBS 2^23 x 1) blind rotation with ONE wave per polynomial component
+// (round 4): the 1024-point transform of fft1k.h, restated in oracle/fft_oracle.c (fft1k_fwd / fft1k_inv).
+//
+// Workgroup = 8 waves, CTS ciphertexts (4 in the batch kernel, 1 in latency mode); waves w < 2 CTS are the transform
+// waves (p, c) = (w >> 1, w & 1), each holding component c of ciphertext p (2048 u64 = 32 per lane, registers).
+// Per CMUX i:
+//   transform waves: (X^a acc_c - acc_c) through the wave's LDS area (rotation by DS offsets), 23-bit digits, the
+//     forward transform (one LDS transpose), the spectrum D_c stored to the area [slot][lane]
+//   barrier
+//   MAC, all 8 waves: wave w owns slots 2w, 2w + 1 of every ciphertext of the workgroup,
+//     O_j = D_0 (.) K_{0,j} + D_1 (.) K_{1,j}  (the oracle's fma chain from (0, 0), c = 0 first)
+//     with the key words of those slots in registers (requested at the CMUX start: 8 complex per wave, shared by
+//     the CTS ciphertexts), O_j written over D_j in the areas
+//   barrier
+//   transform waves: O_c from the own area, the inverse transform, acc_c += rint mod 2^64 (two-split form: the
+//     23-bit digits give |x| up to 2^106)
+// Two barriers per CMUX (the two-wave kernel it replaces had five to six) and no wave waits for a partner
+// mid-transform.  LDS (CTS = 4): pass A table 16 KB (first, so an area's base minus 16 KB stays inside the block for
+// the rotation's wrapped reads) | 8 areas x 17 KB = 152 KB.
+#include "fft1k.h"
+#include "pbs_kernels.h"
+
+namespace tfhe {
+namespace fft1k {
+
+constexpr int N2 = 2048;
+constexpr int F1_THREADS = 512;  // 8 waves
+
+__device__ __forceinline__ int ms4096(u64 x) { return (int)((((x >> 51) + 1) >> 1) & 4095u); }
+// tfhe-rs SignedDecomposer 2^23 x 1 on the high word (pbs_fft2k.hip: decomp_23x1_hi; tests/test_fft.py)
+__device__ __forceinline__ int dig23(u32 hi) {
+  const u32 st = (hi + 256u) >> 9;
+  return (int)((st + 0x3FFFFFu) & 0x7FFFFFu) - 0x3FFFFF;
+}
+typedef __attribute__((address_space(3))) u64 lds_u64;
+
+template <int CTS>
+struct F1Shared {
+  double2 ta[M1];                 // pass A table (K_TA)
+  double2 area[2 * CTS][AREA_C64];
+};
+
+__device__ __forceinline__ void load_ta(double2* ta, const double2* __restrict__ tg) {
+  for (int q = threadIdx.x; q < M1; q += blockDim.x) ta[q] = tg[K_TA + q];
+}
+
+// (X^a v - v) through the area, then 23-bit digits as doubles: xr[e] <- coefficient L + 64 e, xi[e] <- + 1024
+__device__ __forceinline__ void rotate_digits(const u64 (&v)[32], int a, int lane, double2* area, double (&xr)[16],
+                                              double (&xi)[16]) {
+  u64* Tu = (u64*)area;
+#pragma unroll
+  for (int e = 0; e < 32; e++) Tu[64 * e + lane] = v[e];
+  lds_order();
+  const int t0 = (lane - a) & 4095;  // a < 4096
+  const int u = t0 & 2047;
+  const bool neg0 = t0 >= 2048;
+  const u32 a0 = (u32)(uintptr_t)(lds_u64*)&Tu[u];
+  const u32 a1 = a0 - 16384u;        // wrapped reads: the image 16 KB lower
+#pragma unroll
+  for (int e = 0; e < 32; e++) {
+    const bool wrap = u >= 2048 - 64 * e;
+    const u64 x = ((const lds_u64*)(uintptr_t)(wrap ? a1 : a0))[64 * e];
+    const u64 m = 0ull - (u64)(neg0 != wrap);  // all ones iff negated
+    const u64 y = ((x ^ m) - m) - v[e];
+    const double d = (double)dig23((u32)(y >> 32));
+    if (e < 16) xr[e] = d;
+    else xi[e - 16] = d;
+  }
+  lds_order();
+}
+
+template <int CTS, bool WRITE_ACC, bool WRITE_BIG>
+__global__ __launch_bounds__(F1_THREADS, 1) void blind_rotate_fft1k_kernel(
+    const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
+    int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tg, u64* __restrict__ out_big,
+    u64* __restrict__ out_acc) {
+  __shared__ __attribute__((aligned(16))) F1Shared<CTS> sh;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const bool tw_wave = wave_s < 2 * CTS;
+  const int c = wave & 1, p = tw_wave ? wave >> 1 : 0;
+  const size_t b_raw = (size_t)blockIdx.x * CTS + p;
+  const bool live = tw_wave && b_raw < B;
+  const size_t b = b_raw < B ? b_raw : B - 1;  // padding waves run a copy of the last ciphertext, store nothing
+  const u64* ct = lwe_in + b * (size_t)(n + 1);
+  double2* area = sh.area[tw_wave ? wave : 0];
+
+  load_ta(sh.ta, tg);
+  TwB tb;
+  tb.load(tg, lane);
+  u64 acc[32];
+  if (tw_wave) {  // acc_c: A = 0, B = X^{-b~} * lut (LUT values in the Z_p encoding, mapped to the torus)
+    int li = lut_index ? (int)lut_index[b] : 0;
+    li = (li < 0 || li >= n_lut) ? 0 : li;
+    const u64* lut = luts + (size_t)li * N2;
+    const int s = (4096 - ms4096(ct[n])) & 4095;
+#pragma unroll
+    for (int e = 0; e < 32; e++) {
+      int d = 64 * e + lane - s;
+      bool neg = false;
+      if (d < 0) { d += N2; neg = !neg; }
+      if (d < 0) { d += N2; neg = !neg; }
+      const u64 v = gl_to_torus(lut[d]);
+      acc[e] = c ? (neg ? 0 - v : v) : 0;
+    }
+  }
+  __syncthreads();
+
+  int a_next = tw_wave ? ms4096(ct[0]) : 0;
+  const int s0 = 2 * wave_s;  // MAC slots s0, s0 + 1
+  for (int i = 0; i < n; i++) {
+    // key words of this CMUX for the MAC phase: kv[t][cc][j] = K_{cc,j}[slot s0 + t][lane]
+    double2 kv[2][2][2];
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+#pragma unroll
+      for (int cc = 0; cc < 2; cc++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) kv[t][cc][j] = bsk[((size_t)(i * 2 + cc) * 2 + j) * M1 + 64 * (s0 + t) + lane];
+    const int a = a_next;
+    if (tw_wave && i + 1 < n) a_next = ms4096(ct[i + 1]);
+    if (tw_wave) {
+      double xr[16], xi[16];
+      rotate_digits(acc, a, lane, area, xr, xi);
+      fft1k_fwd(xr, xi, area, lane, sh.ta, tb);
+#pragma unroll
+      for (int s = 0; s < 16; s++) area[64 * s + lane] = make_double2(xr[s], xi[s]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < CTS; q++) {
+#pragma unroll
+      for (int t = 0; t < 2; t++) {
+        const int idx = 64 * (s0 + t) + lane;
+        const double2 d0 = sh.area[2 * q][idx], d1 = sh.area[2 * q + 1][idx];
+        double2 o[2];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          const double2 k0 = kv[t][0][j], k1 = kv[t][1][j];
+          double re = __builtin_fma(d0.x, k0.x, 0.0);
+          re = __builtin_fma(-d0.y, k0.y, re);
+          double im = __builtin_fma(d0.x, k0.y, 0.0);
+          im = __builtin_fma(d0.y, k0.x, im);
+          re = __builtin_fma(d1.x, k1.x, re);
+          re = __builtin_fma(-d1.y, k1.y, re);
+          im = __builtin_fma(d1.x, k1.y, im);
+          im = __builtin_fma(d1.y, k1.x, im);
+          o[j] = make_double2(re, im);
+        }
+        sh.area[2 * q][idx] = o[0];
+        sh.area[2 * q + 1][idx] = o[1];
+      }
+    }
+    __syncthreads();
+    if (tw_wave) {
+      double xr[16], xi[16];
+#pragma unroll
+      for (int s = 0; s < 16; s++) {
+        const double2 v = area[64 * s + lane];
+        xr[s] = v.x;
+        xi[s] = v.y;
+      }
+      fft1k_inv(xr, xi, area, lane, sh.ta, tb);
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        acc[e] += f64_to_torus_wide(xr[e]);
+        acc[e + 16] += f64_to_torus_wide(xi[e]);
+      }
+    }
+  }
+
+  if (!live) return;
+  if (WRITE_ACC) {
+    u64* oa = out_acc + b * (2 * N2) + c * N2;
+#pragma unroll
+    for (int e = 0; e < 32; e++) oa[64 * e + lane] = acc[e];
+  }
+  if (WRITE_BIG) {  // sample extraction at degree 0: a'_0 = A[0], a'_j = -A[N-j], b' = B[0]
+    u64* ob = out_big + b * (size_t)(N2 + 1);
+    if (c == 0) {
+#pragma unroll
+      for (int e = 0; e < 32; e++) {
+        const int t = 64 * e + lane;
+        if (t == 0) ob[0] = acc[e];
+        else ob[N2 - t] = 0 - acc[e];
+      }
+    } else if (lane == 0) {
+      ob[N2] = acc[0];
+    }
+  }
+}
+
+// one wave per polynomial: natural coefficients (int64 torus words) -> spectrum [slot][lane] x scale
+__global__ __launch_bounds__(64) void fwd1k_kernel(const u64* __restrict__ in, double2* __restrict__ out,
+                                                   const double2* __restrict__ tg, double scale) {
+  __shared__ __attribute__((aligned(16))) double2 ta[M1];
+  __shared__ __attribute__((aligned(16))) double2 area[AREA_C64];
+  const int lane = threadIdx.x;
+  load_ta(ta, tg);
+  TwB tb;
+  tb.load(tg, lane);
+  const u64* src = in + (size_t)blockIdx.x * N2;
+  double xr[16], xi[16];
+#pragma unroll
+  for (int e = 0; e < 16; e++) {
+    xr[e] = i64_to_f64(src[64 * e + lane]);
+    xi[e] = i64_to_f64(src[64 * e + lane + M1]);
+  }
+  __syncthreads();
+  fft1k_fwd(xr, xi, area, lane, ta, tb);
+  double2* dst = out + (size_t)blockIdx.x * M1;
+#pragma unroll
+  for (int s = 0; s < 16; s++) dst[64 * s + lane] = make_double2(xr[s] * scale, xi[s] * scale);
+}
+
+// inverse for the parity tests: spectrum [slot][lane] -> 2048 doubles (no 1/M, no rounding)
+__global__ __launch_bounds__(64) void inv1k_kernel(const double2* __restrict__ in, double* __restrict__ out,
+                                                   const double2* __restrict__ tg) {
+  __shared__ __attribute__((aligned(16))) double2 ta[M1];
+  __shared__ __attribute__((aligned(16))) double2 area[AREA_C64];
+  const int lane = threadIdx.x;
+  load_ta(ta, tg);
+  TwB tb;
+  tb.load(tg, lane);
+  const double2* src = in + (size_t)blockIdx.x * M1;
+  double xr[16], xi[16];
+#pragma unroll
+  for (int s = 0; s < 16; s++) {
+    const double2 v = src[64 * s + lane];
+    xr[s] = v.x;
+    xi[s] = v.y;
+  }
+  __syncthreads();
+  fft1k_inv(xr, xi, area, lane, ta, tb);
+  double* dst = out + (size_t)blockIdx.x * N2;
+#pragma unroll
+  for (int e = 0; e < 16; e++) {
+    dst[64 * e + lane] = xr[e];
+    dst[64 * e + lane + M1] = xi[e];
+  }
+}
+
+}  // namespace fft1k
+
+size_t fft1k_tables_len() { return 2 * fft1k::K_C64; }
+
+// ta[k][L] = zeta^{L (1 + 4 k)}, tb[m][l0] = zeta^{64 l0 m}, zeta = e^{2 pi i / 4096} (the oracle's tab1k)
+void make_fft1k_tables(double* t) {
+  using namespace fft1k;
+  for (uint32_t k = 0; k < 16; k++)
+    for (uint32_t L = 0; L < 64; L++) {
+      const int o = K_TA + 64 * k + L;
+      fft_twiddle((L * (1 + 4 * k)) % 4096, 4096, &t[2 * o], &t[2 * o + 1]);
+    }
+  for (uint32_t m = 0; m < 4; m++)
+    for (uint32_t l = 0; l < 16; l++) {
+      const int o = K_TB + 16 * m + l;
+      fft_twiddle((64 * l * m) % 4096, 4096, &t[2 * o], &t[2 * o + 1]);
+    }
+}
+
+// the compile-time slot constants equal the table generator's zeta^{64 e} bit for bit
+bool fft1k_slot_constants_ok() {
+  for (int e = 0; e < 16; e++) {
+    double c, s;
+    fft_twiddle(64u * e, 4096u, &c, &s);
+    if (c != fft1k::ctw16::SLOT[e].x || s != fft1k::ctw16::SLOT[e].y) return false;
+  }
+  return true;
+}
+
+hipError_t launch_bsk_to_fourier1k(const u64* bsk_std, double* bsk_f, size_t polys, const double* tw, hipStream_t s) {
+  if (polys == 0) return hipSuccess;
+  hipLaunchKernelGGL(fft1k::fwd1k_kernel, dim3((unsigned)polys), dim3(64), 0, s, bsk_std, (double2*)bsk_f,
+                     (const double2*)tw, 0x1p-10);
+  return hipGetLastError();
+}
+
+hipError_t launch_fft1k_fwd(const u64* in, size_t count, double* out, const double* tw, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(fft1k::fwd1k_kernel, dim3((unsigned)count), dim3(64), 0, s, in, (double2*)out,
+                     (const double2*)tw, 1.0);
+  return hipGetLastError();
+}
+
+hipError_t launch_fft1k_inv(const double* in, size_t count, double* out, const double* tw, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(fft1k::inv1k_kernel, dim3((unsigned)count), dim3(64), 0, s, (const double2*)in, out,
+                     (const double2*)tw);
+  return hipGetLastError();
+}
+
+template <int CTS>
+static hipError_t launch_br1k(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index, int n_lut,
+                              const double2* bk, const double2* t, u64* out_big, u64* out_acc, hipStream_t s) {
+  using namespace fft1k;
+  dim3 grid((unsigned)((B + CTS - 1) / CTS)), block(F1_THREADS);
+  if (out_acc && out_big)
+    hipLaunchKernelGGL((blind_rotate_fft1k_kernel<CTS, true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                       n_lut, bk, t, out_big, out_acc);
+  else if (out_acc)
+    hipLaunchKernelGGL((blind_rotate_fft1k_kernel<CTS, true, false>), grid, block, 0, s, lwe_in, n, B, luts,
+                       lut_index, n_lut, bk, t, out_big, out_acc);
+  else
+    hipLaunchKernelGGL((blind_rotate_fft1k_kernel<CTS, false, true>), grid, block, 0, s, lwe_in, n, B, luts,
+                       lut_index, n_lut, bk, t, out_big, out_acc);
+  return hipGetLastError();
+}
+
+// batches up to latency_max_batch: one ciphertext per workgroup (two transform waves, eight MAC waves); larger
+// batches: four per workgroup
+hipError_t launch_blind_rotate_fft1k(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
+                                     int n_lut, const double* bsk_f, const double* tw, u64* out_big, u64* out_acc,
+                                     hipStream_t s, size_t latency_max_batch) {
+  if (B == 0) return hipSuccess;
+  const double2 *bk = (const double2*)bsk_f, *t = (const double2*)tw;
+  if (B <= latency_max_batch) return launch_br1k<1>(lwe_in, B, n, luts, lut_index, n_lut, bk, t, out_big, out_acc, s);
+  return launch_br1k<4>(lwe_in, B, n, luts, lut_index, n_lut, bk, t, out_big, out_acc, s);
+}
+
+}  // namespace tfhe
