@@ -31,15 +31,8 @@
  *                    B': lane n0 + 8 k0 transforms k1 -> n1, x[n1] *= conj(w^{k0 (n0 + 8 n1)}) (all; the
  *                        merged tables also carry the lane part of the untwist)
  *                    A': lane n0 + 8 n1 transforms k0 -> n2 = z[L + 64 n2]
- *   N = 2048         (P-FHEVM, preset 3) two 512-point halves: z_j = (a_j + i a_{j+1024}) zeta^j,
- *                    zeta = e^{i pi/2048}; E_h = the 512-point DFT above of z_{2m+h} (h = 0, 1) with the
- *                    twist merged per parity (fft2k_tab.twA / twI: slot constant zeta^{128 e} before pass A,
- *                    zeta^{2 L + h} in pass A's table; the mirror image in the inverse), then
- *                    t = cmul(E_1[k'], w^k'), w = e^{2 pi i/1024}: Z[k'] = E_0 + t, Z[k'+512] = E_0 - t.
- *                    Device order of the spectrum (two waves per polynomial): index h*512 + 64 s + L
- *                    holds frequency k'(L, 4h + (s & 3)) + 512 (s >> 2), k'(L, e) = (L>>3) + 8 (L&7) + 64 e.
- *                    Inverse: E_0 = lo + hi, E_1 = cmul(lo - hi, conj(w^k')), the 512-point inverses,
- *                    untwist by conj(zeta^{2m+h}).  1/M = 2^-10 folded into the BSK.
+ *   N = 2048         (P-FHEVM, preset 3) one 1024-point transform per polynomial on the device's 64-lane x
+ *                    16-slot grid (round 4; the section "N = 2048, one wave per polynomial" below has the stages)
  *   N = 1024         the twist is merged into the passes (see fft_tab.twAm / twIm): z = v * zeta^{64 e} for
  *                    slot e > 0 before pass A, whose table is zeta^{L (1 + 4 e)} for all 8 slots; inverse pass
  *                    B' uses zeta^{(n0 + 8 n1)(4 k0 + 1)} and the output slot e > 0 gets conj(zeta^{64 e})
@@ -58,9 +51,6 @@
 #include "tfhe_oracle.h"
 
 #define FFT_M 512
-/* N = 2048: 1 = the round-1..3 two-wave transform (512-point halves + combine), 0 = the one-wave 1024-point
- * transform of round 4 (set by tests comparing the two; the device runs the round-4 one) */
-int or_fft2k_legacy = 1;
 
 /* ---- twiddles: fixed series in plain double (no libm), |x| <= pi/4 ------------------------ */
 static double fs_sin(double x) {
@@ -233,86 +223,6 @@ static void dft512_inv_tab(const or_c64* in, or_c64* out, const or_c64 (*twi)[64
 
 
 
-/* ---- N = 2048: two 512-point halves + one combine pass ------------------------------------ */
-typedef struct fft2k_tab {
-  or_c64 twist[2 * FFT_M];  /* zeta^j, zeta = e^{i pi / 2048} */
-  or_c64 wc[2][4][64];      /* w^{k'(L, 4h + p)}, w = e^{2 pi i / 1024} */
-  /* twist merged into the passes per parity h (pbs_fft2k.hip): zeta^{2 m + h} = zeta^{2 L + h} zeta^{128 e}
-   * for m = L + 64 e; the slot constant zeta^{128 e} multiplies before pass A, zeta^{2 L + h} rides in pass
-   * A's table; inverse: zeta^{2 (n0 + 8 n1) + h} in pass B''s table, conj(zeta^{128 e}) after pass A' */
-  or_c64 twA[2][8][64];     /* zeta^{L (8 e + 2) + h} */
-  or_c64 twI[2][8][64];     /* zeta^{(n0 + 8 e)(8 k0 + 2) + h}, L = n0 + 8 k0 */
-} fft2k_tab;
-static fft2k_tab g_tab2k;
-static int g_tab2k_ready = 0;
-
-static int kdev(int L, int e) { return (L >> 3) + 8 * (L & 7) + 64 * e; } /* device-order frequency */
-
-static const fft2k_tab* tab2k(void) {
-#pragma omp critical(or_fft_tab2k)
-  {
-    if (!g_tab2k_ready) {
-      for (uint32_t j = 0; j < 2 * FFT_M; j++) or_fft_twiddle(j, 4096, &g_tab2k.twist[j].re, &g_tab2k.twist[j].im);
-      for (int h = 0; h < 2; h++)
-        for (int q = 0; q < 4; q++)
-          for (int L = 0; L < 64; L++)
-            or_fft_twiddle((uint32_t)kdev(L, 4 * h + q), 1024, &g_tab2k.wc[h][q][L].re, &g_tab2k.wc[h][q][L].im);
-      for (uint32_t h = 0; h < 2; h++)
-        for (uint32_t e = 0; e < 8; e++)
-          for (uint32_t L = 0; L < 64; L++) {
-            or_fft_twiddle((L * (8 * e + 2) + h) % 4096, 4096, &g_tab2k.twA[h][e][L].re, &g_tab2k.twA[h][e][L].im);
-            or_fft_twiddle((((L & 7) + 8 * e) * (8 * (L >> 3) + 2) + h) % 4096, 4096, &g_tab2k.twI[h][e][L].re,
-                           &g_tab2k.twI[h][e][L].im);
-          }
-      __atomic_store_n(&g_tab2k_ready, 1, __ATOMIC_RELEASE);
-    }
-  }
-  return &g_tab2k;
-}
-
-static void fft2k_fwd(const double* a, or_c64* out) {
-  const fft2k_tab* T = tab2k();
-  or_c64 z[2][FFT_M], E[2][FFT_M];
-  for (int h = 0; h < 2; h++) {
-    for (int m = 0; m < FFT_M; m++) { /* m = L + 64 e: slot constant zeta^{128 e} (e > 0) */
-      const int j = 2 * m + h, e = m >> 6;
-      const or_c64 v = {a[j], a[j + 2 * FFT_M]};
-      z[h][m] = e ? cmul(v, T->twist[128 * e].re, T->twist[128 * e].im) : v;
-    }
-    dft512_fwd_tab(z[h], E[h], T->twA[h], 1);
-  }
-  for (int h = 0; h < 2; h++)
-    for (int q = 0; q < 4; q++)
-      for (int L = 0; L < 64; L++) {
-        const int d = L + 64 * (4 * h + q);
-        const or_c64 t = cmul(E[1][d], T->wc[h][q][L].re, T->wc[h][q][L].im);
-        out[h * FFT_M + 64 * q + L] = cadd(E[0][d], t);
-        out[h * FFT_M + 64 * (q + 4) + L] = csub(E[0][d], t);
-      }
-}
-
-static void fft2k_inv(const or_c64* in, double* out) {
-  const fft2k_tab* T = tab2k();
-  or_c64 E[2][FFT_M], z[2][FFT_M];
-  for (int h = 0; h < 2; h++)
-    for (int q = 0; q < 4; q++)
-      for (int L = 0; L < 64; L++) {
-        const or_c64 lo = in[h * FFT_M + 64 * q + L], hi = in[h * FFT_M + 64 * (q + 4) + L];
-        const int d = L + 64 * (4 * h + q);
-        E[0][d] = cadd(lo, hi);
-        E[1][d] = cmul(csub(lo, hi), T->wc[h][q][L].re, -T->wc[h][q][L].im);
-      }
-  for (int h = 0; h < 2; h++) {
-    dft512_inv_tab(E[h], z[h], T->twI[h]);
-    for (int m = 0; m < FFT_M; m++) { /* conj(zeta^{128 e}) after pass A' (e > 0) */
-      const int j = 2 * m + h, e = m >> 6;
-      const or_c64 v = e ? cmul(z[h][m], T->twist[128 * e].re, -T->twist[128 * e].im) : z[h][m];
-      out[j] = v.re;
-      out[j + 2 * FFT_M] = v.im;
-    }
-  }
-}
-
 /* ---- N = 2048, one wave per polynomial (round 4, pbs_fft2k.hip / fft1k.h) ------------------------
  * M = 1024 = 16 x 4 x 16 over the device's 64-lane x 16-slot grid, natural input n = L + 64 e:
  *   z_n = (a_n + i a_{n+1024}) zeta^n, zeta = e^{2 pi i / 4096}: the slot part zeta^{64 e} multiplies slot e > 0,
@@ -456,7 +366,7 @@ static void fft1k_inv(const or_c64* in, double* a) {
 }
 
 void or_fft_fwd(const double* a, uint32_t N, or_c64* out) {
-  if (N == 4 * FFT_M) { if (or_fft2k_legacy) fft2k_fwd(a, out); else fft1k_fwd(a, out); return; }
+  if (N == 4 * FFT_M) { fft1k_fwd(a, out); return; }
   if (N != 2 * FFT_M) abort();
   const fft_tab* T = tab();
   or_c64 z[FFT_M];
@@ -469,7 +379,7 @@ void or_fft_fwd(const double* a, uint32_t N, or_c64* out) {
 }
 
 void or_fft_inv(const or_c64* in, uint32_t N, double* out) {
-  if (N == 4 * FFT_M) { if (or_fft2k_legacy) fft2k_inv(in, out); else fft1k_inv(in, out); return; }
+  if (N == 4 * FFT_M) { fft1k_inv(in, out); return; }
   if (N != 2 * FFT_M) abort();
   const fft_tab* T = tab();
   or_c64 z[FFT_M];

@@ -305,23 +305,6 @@ def fft_inv(z) -> np.ndarray:
     return out
 
 
-class fft2k_legacy:
-    """Context manager: the oracle's N = 2048 transform is the round-1..3 two-wave one (512-point halves + combine)
-    inside, the round-4 one-wave 1024-point transform outside (fft_oracle.c: or_fft2k_legacy)."""
-
-    def __init__(self, on: bool = True):
-        self.on = on
-
-    def __enter__(self):
-        self._flag = ctypes.c_int.in_dll(lib(), "or_fft2k_legacy")
-        self._old = self._flag.value
-        self._flag.value = 1 if self.on else 0
-        return self
-
-    def __exit__(self, *exc):
-        self._flag.value = self._old
-
-
 def f64_to_torus(x: float) -> int:
     return int(lib().or_f64_to_torus(float(x)))
 

@@ -1,12 +1,9 @@
-"""GPU parity of the FFT64 engine at N = 2048 (P-FHEVM) against oracle/fft_oracle.c, bit-exact through the C
-ABI, for both device transforms: the two-wave one (pbs_fft2k.hip: 512-point halves + combine) and the one-wave
-1024-point one (pbs_fft2kc.hip, fft1k.h; TFHE_HIP_F2K=onewave), each against the oracle's restatement of the same
-operation sequence: the transform both ways, blind-rotation accumulators, the full KS -> MS noise reduction -> BR
--> SE PBS with multiple LUTs on ragged batches (padding in the last workgroup), and a 4096 batch by decryption
-plus a sampled bit-exact subset.
+"""GPU parity of the FFT64 engine at N = 2048 (P-FHEVM, the one-wave 1024-point transform of fft1k.h and
+pbs_fft2k.hip) against oracle/fft_oracle.c, bit-exact through the C ABI: the transform both ways, blind-rotation
+accumulators, the full KS -> MS noise reduction -> BR -> SE PBS with multiple LUTs on ragged batches (padding in the
+last workgroup), the latency (2 ciphertexts per workgroup) and batch (4) kernels against each other, and a 4096
+batch by decryption plus a sampled bit-exact subset.
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -25,20 +22,8 @@ def f2_keys():
     return tfhe_amd.gen_keys(tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM_FFT), KEY_SEED)
 
 
-@pytest.fixture(scope="module", params=["legacy", "onewave"])
-def f2_mode(request, oracle_mod):
-    old = os.environ.get("TFHE_HIP_F2K")
-    os.environ["TFHE_HIP_F2K"] = request.param
-    with oracle_mod.fft2k_legacy(request.param == "legacy"):
-        yield request.param
-    if old is None:
-        os.environ.pop("TFHE_HIP_F2K", None)
-    else:
-        os.environ["TFHE_HIP_F2K"] = old
-
-
 @pytest.fixture(scope="module")
-def f2_engine(f2_keys, f2_mode):
+def f2_engine(f2_keys):
     ck, sk = f2_keys
     eng = tfhe_amd.Engine(ck.params, 0)
     eng.load_keys(sk)
@@ -52,13 +37,12 @@ def f2_prm(oracle_mod):
 
 
 @pytest.fixture(scope="module")
-def f2_okeys(oracle_mod, f2_prm, f2_mode):
-    return oracle_mod.Keys(f2_prm, KEY_SEED)  # its Fourier BSK follows the oracle transform of f2_mode
+def f2_okeys(oracle_mod, f2_prm):
+    return oracle_mod.Keys(f2_prm, KEY_SEED)
 
 
-def test_fft2k_forward_inverse_bitexact(f2_engine, oracle_mod, f2_mode):
-    assert f2_engine.br_kernel(4096) == ("blind_rotate_fft1k_kernel" if f2_mode == "onewave" else
-                                         "blind_rotate_fft2k_kernel")
+def test_fft2k_forward_inverse_bitexact(f2_engine, oracle_mod):
+    assert f2_engine.br_kernel(4096) == "blind_rotate_fft2k_kernel"
     rng = np.random.default_rng(41)
     x = rng.integers(0, 2**64, size=(11, N), dtype=np.uint64)
     x[0] = 0
@@ -120,7 +104,7 @@ def test_pbs2k_batch_4096_decrypts_and_sampled_bitexact(f2_engine, f2_keys, orac
     assert np.array_equal(ck.decrypt(out2, MM), np.array([f(f(int(m))) for m in msgs[:512]], dtype=np.uint64))
 
 
-@pytest.mark.parametrize("B", [1, 7, 100])
+@pytest.mark.parametrize("B", [1, 7, 100, 513])
 def test_latency_and_batch_kernels_agree_2k(f2_engine, f2_keys, oracle_mod, f2_prm, f2_okeys, B):
     ck, _ = f2_keys
     rng = np.random.default_rng(B + 4096)

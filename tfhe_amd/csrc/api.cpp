@@ -167,7 +167,6 @@ struct tfhe_ctx {
   std::vector<tfhe_shard> sh;
   bool keys = false;
   bool ks_valu = false;  // TFHE_HIP_KS_VALU=1: the VALU keyswitch kernel instead (A/B runs)
-  bool f2_onewave = false;  // N = 2048 FFT64: the one-wave 1024-point transform (TFHE_HIP_F2K=onewave)
   size_t lat_max = 1024; // batches up to this size (per shard) use the latency blind-rotate kernel
   u64 ninv = 0;
   uint32_t ms_count = 0;
@@ -242,9 +241,6 @@ uint32_t io_dim(const tfhe_params& p) { return p.order == 0 ? p.n : p.k * p.N; }
 
 hipError_t launch_br(tfhe_ctx* c, shard& s, const u64* in, size_t B, const u64* luts, const u32* idx, size_t n_lut,
                      u64* out_big, u64* out_acc, hipStream_t st) {
-  if (is_fft(c->p) && c->p.N == 2048 && c->f2_onewave)
-    return tfhe::launch_blind_rotate_fft1k(in, B, (int)c->p.n, luts, idx, (int)n_lut, (const double*)s.d_bsk,
-                                           (const double*)s.d_tw, out_big, out_acc, st, c->lat_max);
   if (is_fft(c->p) && c->p.N == 2048)
     return tfhe::launch_blind_rotate_fft2k(in, B, (int)c->p.n, luts, idx, (int)n_lut, (const double*)s.d_bsk,
                                            (const double*)s.d_tw, out_big, out_acc, st, c->lat_max);
@@ -488,9 +484,7 @@ int convert_keys(tfhe_ctx* c, shard& s, const u64* std_bsk, size_t bsk_len) {
       HIP_TRY(hipMalloc(&s.d_ks_planes, tfhe::ks_planes_bytes(big_dim, (int)c->p.ks_level, (int)c->p.n)));
     HIP_TRY(tfhe::launch_ksk_planes(s.d_ksk, big_dim, (int)c->p.ks_level, (int)c->p.n, s.d_ks_planes, s.stream));
   }
-  if (is_fft(c->p) && c->p.N == 2048 && c->f2_onewave)
-    HIP_TRY(tfhe::launch_bsk_to_fourier1k(std_bsk, (double*)s.d_bsk, polys, (const double*)s.d_tw, s.stream));
-  else if (is_fft(c->p) && c->p.N == 2048)
+  if (is_fft(c->p) && c->p.N == 2048)
     HIP_TRY(tfhe::launch_bsk_to_fourier2k(std_bsk, (double*)s.d_bsk, polys, (const double*)s.d_tw, s.stream));
   else if (is_fft(c->p))
     HIP_TRY(tfhe::launch_bsk_to_fourier(std_bsk, (double*)s.d_bsk, polys, (const double*)s.d_tw, s.stream));
@@ -509,11 +503,10 @@ int shard_init(tfhe_ctx* c, shard& s) {
   const tfhe_params& p = c->p;
   using namespace tfhe;
   if (is_fft(p)) {  // FFT64: twist / pass tables (pbs_fft.hip: make_fft_tables)
-    std::vector<double> tw(p.N == 2048 ? (c->f2_onewave ? fft1k_tables_len() : fft2k_tables_len()) : fft_tables_len());
-    if (p.N == 2048 && c->f2_onewave) make_fft1k_tables(tw.data());
-    else if (p.N == 2048) make_fft2k_tables(tw.data());
+    std::vector<double> tw(p.N == 2048 ? fft2k_tables_len() : fft_tables_len());
+    if (p.N == 2048) make_fft2k_tables(tw.data());
     else make_fft_tables(tw.data());
-    if (!fft_slot_constants_ok() || !fft1k_slot_constants_ok())
+    if (!fft_slot_constants_ok() || !fft2k_slot_constants_ok())
       return fail(TFHE_HIP_EUNSUPPORTED, "FFT64: compile-time twist constants differ from the host tables");
     HIP_TRY(hipMalloc(&s.d_tw, tw.size() * 8));
     HIP_TRY(hipMemcpy(s.d_tw, tw.data(), tw.size() * 8, hipMemcpyHostToDevice));
@@ -578,15 +571,6 @@ int for_each_slice(tfhe_ctx* c, size_t B, F&& fn) {
 
 }  // namespace
 
-#if F2_STAMPS
-namespace tfhe {
-hipError_t read_fft2k_stamps(unsigned long long* out);
-}
-// diagnostic builds only (-DF2_STAMPS=1): the P-FHEVM batch kernel's phase stamps (tools/stamps.py)
-extern "C" int tfhe_hip_debug_fft2k_stamps(unsigned long long* out) {
-  return tfhe::read_fft2k_stamps(out) == hipSuccess ? 0 : TFHE_HIP_EDEVICE;
-}
-#endif
 
 // error slot shared with pks_api.cpp / sns_api.cpp
 int tfhe_hip_set_error(int code, const char* msg) {
@@ -741,12 +725,12 @@ int tfhe_hip_create(const tfhe_params* p, const int* devices, int ndev, tfhe_ctx
   // on, workgroups that start staggered stream the BSK from L2 at different CMUX indices)
   // round 3: the P-GATE FFT64 component-pair batch kernel runs any batch up to 1024 in one 6.7 ms round, the
   // latency kernel 3.5-3.7 ms up to 256 and 7.1 ms from 257 (profiles/r03_latsweep.json): crossover 256
+  // round 4: P-FHEVM FFT64 runs its one-wave kernel in latency mode (two ciphertexts per workgroup, one transform
+  // wave per SIMD) up to 512 ciphertexts (one round over 256 CUs), four per workgroup above
   c->lat_max = is_fft(*p) ? (p->N == 1024 ? 256 : 512) : p->N == 2048 ? 512 : 1024;
   {
     const char* e = getenv("TFHE_HIP_KS_VALU");
     c->ks_valu = e && e[0] == '1';
-    const char* f2 = getenv("TFHE_HIP_F2K");
-    c->f2_onewave = f2 && !strcmp(f2, "onewave");
   }
   if (!is_fft(*p)) c->ninv = tfhe::gl_pow(p->N, tfhe::GL_P - 2);
   c->sh.resize(ndev);
@@ -1049,12 +1033,10 @@ static int fft_impl(tfhe_ctx* c, const void* in, size_t count, double* out, bool
   RC_TRY(stage(s, {{in, bytes}}, d, bytes));
   const double* tw = (const double*)s.d_tw;
   if (!inverse) {
-    if (c->p.N == 2048 && c->f2_onewave) HIP_TRY(tfhe::launch_fft1k_fwd((const u64*)d[0], count, (double*)d[1], tw, s.stream));
-    else if (c->p.N == 2048) HIP_TRY(tfhe::launch_fft2k_fwd((const u64*)d[0], count, (double*)d[1], tw, s.stream));
+    if (c->p.N == 2048) HIP_TRY(tfhe::launch_fft2k_fwd((const u64*)d[0], count, (double*)d[1], tw, s.stream));
     else HIP_TRY(tfhe::launch_fft_fwd((const u64*)d[0], count, (double*)d[1], tw, s.stream));
   } else {
-    if (c->p.N == 2048 && c->f2_onewave) HIP_TRY(tfhe::launch_fft1k_inv((const double*)d[0], count, (double*)d[1], tw, s.stream));
-    else if (c->p.N == 2048) HIP_TRY(tfhe::launch_fft2k_inv((const double*)d[0], count, (double*)d[1], tw, s.stream));
+    if (c->p.N == 2048) HIP_TRY(tfhe::launch_fft2k_inv((const double*)d[0], count, (double*)d[1], tw, s.stream));
     else HIP_TRY(tfhe::launch_fft_inv((const double*)d[0], count, (double*)d[1], tw, s.stream));
   }
   HIP_TRY(hipMemcpyAsync(out, d[1], bytes, hipMemcpyDeviceToHost, s.stream));
@@ -1096,8 +1078,7 @@ int tfhe_hip_set_latency_batch(tfhe_ctx* c, size_t max_batch) {
 const char* tfhe_hip_br_kernel(const tfhe_ctx* c, size_t B) {
   if (!c) return nullptr;
   const bool lat = B <= c->lat_max;
-  if (is_fft(c->p) && c->p.N == 2048 && c->f2_onewave) return "blind_rotate_fft1k_kernel";
-  if (is_fft(c->p) && c->p.N == 2048) return lat ? "blind_rotate_fft2k_lat_kernel" : "blind_rotate_fft2k_kernel";
+  if (is_fft(c->p) && c->p.N == 2048) return "blind_rotate_fft2k_kernel";  // <2, ...> latency, <4, ...> batch
   if (is_fft(c->p)) return lat ? "blind_rotate_fft_lat_kernel" : "blind_rotate_fft_pair_kernel";
   if (c->p.N == 2048) return lat ? "blind_rotate2048_lat_kernel" : "blind_rotate2048_kernel";
   return lat ? "blind_rotate_lat_kernel" : "blind_rotate_kernel";

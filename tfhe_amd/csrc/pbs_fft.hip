@@ -333,6 +333,9 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
 #endif
 #if FFT_PRIO == 1
   if (wave_s >= 4) __builtin_amdgcn_s_setprio(1);
+#elif FFT_PRIO == 3
+  // A/B: with two workgroups per CU, one of them (by dispatch round) at the higher priority
+  if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_setprio(1);
 #endif
   for (int i = 0; i < n; i++) {
     // (X^a acc_c - acc_c), decomposed: the rotation image in this wave's own transpose area (its previous

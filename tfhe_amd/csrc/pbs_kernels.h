@@ -40,27 +40,18 @@ hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64
 hipError_t launch_sample_extract_torus(const u64* acc, size_t B, u64* out, hipStream_t s);
 hipError_t launch_fft_fwd(const u64* in, size_t count, double* out, const double* tw, hipStream_t s);
 hipError_t launch_fft_inv(const double* in, size_t count, double* out, const double* tw, hipStream_t s);
-// FFT64 transform, N = 2048 (pbs_fft2k.hip): table = 3072 complex (twist parity 0 | pass A | B | I |
-// twist parity 1 | combine); Fourier BSK = polys x 1024 complex in the two-wave device order
+// FFT64 transform, N = 2048, one wave per polynomial (pbs_fft2k.hip, fft1k.h): table = pass A [16][64] |
+// pass B [4][16] (complex)
 size_t fft2k_tables_len();  // doubles
 void make_fft2k_tables(double* tw);
+bool fft2k_slot_constants_ok();
 hipError_t launch_bsk_to_fourier2k(const u64* bsk_std, double* bsk_f, size_t polys, const double* tw, hipStream_t s);
 hipError_t launch_blind_rotate_fft2k(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
                                      int n_lut, const double* bsk_f, const double* tw, u64* out_big, u64* out_acc,
-                                     hipStream_t s, size_t latency_max_batch = 0);
+                                     hipStream_t s, size_t latency_max_batch);
 hipError_t launch_sample_extract_torus2k(const u64* acc, size_t B, u64* out, hipStream_t s);
 hipError_t launch_fft2k_fwd(const u64* in, size_t count, double* out, const double* tw, hipStream_t s);
 hipError_t launch_fft2k_inv(const double* in, size_t count, double* out, const double* tw, hipStream_t s);
-// FFT64, N = 2048, one wave per polynomial (pbs_fft2kc.hip, fft1k.h): table = pass A [16][64] | pass B [4][16]
-size_t fft1k_tables_len();  // doubles
-void make_fft1k_tables(double* tw);
-bool fft1k_slot_constants_ok();
-hipError_t launch_bsk_to_fourier1k(const u64* bsk_std, double* bsk_f, size_t polys, const double* tw, hipStream_t s);
-hipError_t launch_blind_rotate_fft1k(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
-                                     int n_lut, const double* bsk_f, const double* tw, u64* out_big, u64* out_acc,
-                                     hipStream_t s, size_t latency_max_batch);
-hipError_t launch_fft1k_fwd(const u64* in, size_t count, double* out, const double* tw, hipStream_t s);
-hipError_t launch_fft1k_inv(const double* in, size_t count, double* out, const double* tw, hipStream_t s);
 
 // N = 2048 (P-FHEVM, pbs_n2048.hip): tables = [1024-point tables of psi^2 (4096) | combine
 // twiddles psi^(2j+1) (2048) | inverses (2048)]
