@@ -18,16 +18,29 @@
  *                    (inverse transforms use w = (w.re, -w.im))
  *   dft8             radix-2 decimation in frequency, 3 stages, natural order in and out; the
  *                    internal rotations by e^{+-i pi/4 j} are the explicit forms in w8() below
- *   N = 1024         (P-GATE) M = 512 = 8 x 4 x 16 over the device's 64-lane x 8-slot grid with one LDS transpose
- *                    (round 4; section "N = 1024, the one-transpose 512-point transform" below); spectra are kept
- *                    in DEVICE ORDER (the BSK is converted by the same routine)
+ *   3 passes         M = 512 = 8 x 8 x 8 over a 64 x 8 grid (the device's lane x register grid),
+ *                    w = e^{2 pi i / M}, n = n0 + 8 n1 + 64 n2, k = k0 + 8 k1 + 64 k2:
+ *                    A: lane L = n0 + 8 n1 transforms n2, then x[k0] *= w^{L k0} (k0 > 0; with the twist
+ *                       merged, see N = 1024 / N = 2048 below, every k0 by the merged table)
+ *                    B: lane n0 + 8 k0 transforms n1, then x[k1] *= w^{8 n0 k1}            (k1 > 0)
+ *                    C: lane k1 + 8 k0 transforms n0 -> Z[k] in slot k2
+ *                    so spectra are kept in DEVICE ORDER: slot d = L + 64 e holds frequency
+ *                    k(d) = (L >> 3) + 8 (L & 7) + 64 e (the BSK is converted by the same routine)
+ *   inverse          the passes reversed (decimation in time), device order in, natural order out:
+ *                    C': lane k1 + 8 k0 transforms k2 -> n0, x[n0] *= conj(w^{8 n0 k1})   (n0 > 0)
+ *                    B': lane n0 + 8 k0 transforms k1 -> n1, x[n1] *= conj(w^{k0 (n0 + 8 n1)}) (all; the
+ *                        merged tables also carry the lane part of the untwist)
+ *                    A': lane n0 + 8 n1 transforms k0 -> n2 = z[L + 64 n2]
  *   N = 2048         (P-FHEVM, preset 3) one 1024-point transform per polynomial on the device's 64-lane x
  *                    16-slot grid (round 4; the section "N = 2048, one wave per polynomial" below has the stages)
- *   MAC              one fma chain per output and frequency, re = fma(D.re, K.re, re); re = fma(-D.im, K.im, re);
- *                    im = fma(D.re, K.im, im); im = fma(D.im, K.re, im), over the levels least significant
- *                    first (l = L-1 .. 0: the order the device produces digits, carry chain upward) and, within a
- *                    level, c = 0..k; N = 2048 starts from (0, 0), N = 1024 starts with re = D.re * K.re,
- *                    im = D.re * K.im (pbs_fft.hip mac_first; the two differ only in the sign of an exact zero)
+ *   N = 1024         the twist is merged into the passes (see fft_tab.twAm / twIm): z = v * zeta^{64 e} for
+ *                    slot e > 0 before pass A, whose table is zeta^{L (1 + 4 e)} for all 8 slots; inverse pass
+ *                    B' uses zeta^{(n0 + 8 n1)(4 k0 + 1)} and the output slot e > 0 gets conj(zeta^{64 e})
+ *   MAC              re = fma(D.re, K.re, re); re = fma(-D.im, K.im, re);
+ *                    im = fma(D.re, K.im, im); im = fma(D.im, K.re, im)   from (0, 0) (N = 1024: the first
+ *                    term of each component chain is re = D.re * K.re, im = D.re * K.im instead), over
+ *                    c = 0..k and, within c, the levels least significant first (l = L-1 .. 0:
+ *                    the order the device produces digits, carry chain upward)
  */
 #include <math.h>
 #include <stdlib.h>
@@ -85,9 +98,12 @@ void or_fft_twiddle(uint32_t t, uint32_t M, double* c, double* s) {
 
 typedef struct fft_tab {
   or_c64 twist[FFT_M];  /* zeta^j, zeta = e^{i pi / N} */
-  /* N = 1024 merged twist (fft512p.h): zeta^j = zeta^L zeta^{64 e} for j = L + 64 e; the slot constant zeta^{64 e}
-   * multiplies before stage A's DFT8, zeta^L rides in stage A's table (all 8 slots) */
+  or_c64 twB[8][64];    /* w^{8 (L & 7) k1}, w = e^{2 pi i / M} */
+  /* N = 1024 merged twist (pbs_fft.hip / fft512.h): zeta^j = zeta^L zeta^{64 e} for j = L + 64 e; the slot
+   * constant zeta^{64 e} multiplies before pass A, zeta^L rides in pass A's table (all 8 slots), and the
+   * inverse carries zeta^{n0 + 8 n1} in pass B''s table and conj(zeta^{64 e}) after pass A' */
   or_c64 twAm[8][64];   /* zeta^{L (1 + 4 e)} */
+  or_c64 twIm[8][64];   /* zeta^{(n0 + 8 e)(4 k0 + 1)}, L = n0 + 8 k0 */
 } fft_tab;
 
 static fft_tab g_tab;
@@ -100,7 +116,10 @@ static const fft_tab* tab(void) {
       for (uint32_t j = 0; j < FFT_M; j++) or_fft_twiddle(j, 2 * FFT_M * 2, &g_tab.twist[j].re, &g_tab.twist[j].im);
       for (uint32_t e = 0; e < 8; e++)
         for (uint32_t L = 0; L < 64; L++) {
+          or_fft_twiddle((8 * (L & 7) * e) % FFT_M, FFT_M, &g_tab.twB[e][L].re, &g_tab.twB[e][L].im);
           or_fft_twiddle((L * (1 + 4 * e)) % (4 * FFT_M), 4 * FFT_M, &g_tab.twAm[e][L].re, &g_tab.twAm[e][L].im);
+          or_fft_twiddle((((L & 7) + 8 * e) * (4 * (L >> 3) + 1)) % (4 * FFT_M), 4 * FFT_M, &g_tab.twIm[e][L].re,
+                         &g_tab.twIm[e][L].im);
         }
       __atomic_store_n(&g_tab_ready, 1, __ATOMIC_RELEASE);
     }
@@ -153,6 +172,57 @@ static void dft8(or_c64 x[8], int inv) {
   static const int brv3[8] = {0, 4, 2, 6, 1, 5, 3, 7};
   for (int k = 0; k < 8; k++) x[k] = u[brv3[k]];
 }
+
+/* forward 3-pass DFT: natural order in, device order out; pass A multiplies slots merged ? 0..7 : 1..7 by twa
+ * (the twist-merged tables multiply every slot) */
+static void dft512_fwd_tab(const or_c64* in, or_c64* out, const or_c64 (*twa)[64], int merged) {
+  const fft_tab* T = tab();
+  or_c64 A[64][8], Bv[64][8], x[8];
+  for (int L = 0; L < 64; L++) {
+    for (int e = 0; e < 8; e++) x[e] = in[L + 64 * e];
+    dft8(x, 0);
+    for (int e = merged ? 0 : 1; e < 8; e++) x[e] = cmul(x[e], twa[e][L].re, twa[e][L].im);
+    memcpy(A[L], x, sizeof(x));
+  }
+  for (int L = 0; L < 64; L++) { /* lane n0 + 8 k0 */
+    for (int e = 0; e < 8; e++) x[e] = A[(L & 7) + 8 * e][L >> 3];
+    dft8(x, 0);
+    for (int e = 1; e < 8; e++) x[e] = cmul(x[e], T->twB[e][L].re, T->twB[e][L].im);
+    memcpy(Bv[L], x, sizeof(x));
+  }
+  for (int L = 0; L < 64; L++) { /* lane k1 + 8 k0 */
+    for (int e = 0; e < 8; e++) x[e] = Bv[e + 8 * (L >> 3)][L & 7];
+    dft8(x, 0);
+    for (int e = 0; e < 8; e++) out[L + 64 * e] = x[e];
+  }
+}
+
+
+
+/* inverse 3-pass DFT (no 1/M): device order in, natural order out (merged: pass B' uses twIm) */
+static void dft512_inv_tab(const or_c64* in, or_c64* out, const or_c64 (*twi)[64]) {
+  const fft_tab* T = tab();
+  or_c64 S1[64][8], S2[64][8], x[8];
+  for (int L = 0; L < 64; L++) { /* lane k1 + 8 k0: k2 -> n0 */
+    for (int e = 0; e < 8; e++) x[e] = in[L + 64 * e];
+    dft8(x, 1);
+    for (int e = 1; e < 8; e++) x[e] = cmul(x[e], T->twB[e][L].re, -T->twB[e][L].im);
+    memcpy(S1[L], x, sizeof(x));
+  }
+  for (int L = 0; L < 64; L++) { /* lane n0 + 8 k0: k1 -> n1 */
+    for (int e = 0; e < 8; e++) x[e] = S1[e + 8 * (L >> 3)][L & 7];
+    dft8(x, 1);
+    for (int e = 0; e < 8; e++) x[e] = cmul(x[e], twi[e][L].re, -twi[e][L].im);
+    memcpy(S2[L], x, sizeof(x));
+  }
+  for (int L = 0; L < 64; L++) { /* lane n0 + 8 n1: k0 -> n2 */
+    for (int e = 0; e < 8; e++) x[e] = S2[(L & 7) + 8 * e][L >> 3];
+    dft8(x, 1);
+    for (int e = 0; e < 8; e++) out[L + 64 * e] = x[e];
+  }
+}
+
+
 
 /* ---- N = 2048, one wave per polynomial (round 4, pbs_fft2k.hip / fft1k.h) ------------------------
  * M = 1024 = 16 x 4 x 16 over the device's 64-lane x 16-slot grid, natural input n = L + 64 e:
@@ -296,83 +366,31 @@ static void fft1k_inv(const or_c64* in, double* a) {
   }
 }
 
-/* ---- N = 1024, the one-transpose 512-point transform (round 4, pbs_fft.hip / fft512p.h) ----------------------
- * M = 512 = 8 x 4 x 16 over the device's 64-lane x 8-slot grid, natural input n = L + 64 e, z_n = a_n + i a_{n+512}:
- *   A  lane L: x[e] *= zeta^{64 e} (e > 0), DFT8 over e -> k2, x[k2] *= twAm[k2][L] = zeta^{L (1 + 4 k2)}
- *   X  register exchange: lane L' = l0 + 16 (k2 >> 1) holds slot s' = (k2 & 1) + 2 l1        (L = l0 + 16 l1)
- *   B  per g = k2 & 1: radix-4 over l1 (slots g + 2 l1, stride 2) -> m0, x[g + 2 m0] *= tb[m0][l0]  (m0 > 0)
- *   T  LDS transpose: lane lam = s' + 8 (L' >> 5) + 16 ((L' >> 4) & 1) holds slot l0
- *   C  DFT16 over l0 -> m1, stored at device index lam + 32 m1:
- *      k = (lam & 1) + 2 ((lam >> 4) & 1) + 4 ((lam >> 3) & 1) + 8 ((lam >> 1) & 3) + 32 m1
- *   inverse: C' (inverse DFT16), T back, conj tb + inverse radix-4, X back, conj twAm, inverse DFT8, conj(zeta^{64 e})
- * (twAm is the round-2 merged pass-A table; tb the N = 2048 transform's e^{2 pi i l0 m / 64}.) */
-static void fft512p_fwd(const double* a, or_c64* out) {
-  const fft_tab* T = tab();
-  const fft1k_tab* T1 = tab1k();
-  or_c64 X[64][8], Y[64][8];
-  for (int L = 0; L < 64; L++) {
-    or_c64* x = X[L];
-    for (int e = 0; e < 8; e++) {
-      const or_c64 v = {a[L + 64 * e], a[L + 64 * e + FFT_M]};
-      x[e] = e ? cmul(v, T->twist[64 * e].re, T->twist[64 * e].im) : v;
-    }
-    dft8(x, 0);
-    for (int k = 0; k < 8; k++) x[k] = cmul(x[k], T->twAm[k][L].re, T->twAm[k][L].im);
-  }
-  for (int Lp = 0; Lp < 64; Lp++) /* register exchange */
-    for (int sp = 0; sp < 8; sp++) Y[Lp][sp] = X[(Lp & 15) | ((sp >> 1) << 4)][(sp & 1) | ((Lp >> 4) << 1)];
-  for (int Lp = 0; Lp < 64; Lp++) /* pass B */
-    for (int g = 0; g < 2; g++) {
-      radix4(Y[Lp], g, 2, 0);
-      for (int m = 1; m < 4; m++) Y[Lp][g + 2 * m] = cmul(Y[Lp][g + 2 * m], T1->tb[m][Lp & 15].re, T1->tb[m][Lp & 15].im);
-    }
-  for (int lam = 0; lam < 32; lam++) { /* transpose + pass C */
-    or_c64 z[16];
-    const int hi = (((lam >> 4) & 1) << 4) | (((lam >> 3) & 1) << 5);
-    for (int l0 = 0; l0 < 16; l0++) z[l0] = Y[l0 | hi][lam & 7];
-    dft16(z, 0);
-    for (int m = 0; m < 16; m++) out[lam + 32 * m] = z[m];
-  }
-}
-
-static void fft512p_inv(const or_c64* in, double* a) {
-  const fft_tab* T = tab();
-  const fft1k_tab* T1 = tab1k();
-  or_c64 Y[64][8];
-  for (int lam = 0; lam < 32; lam++) { /* pass C', transpose back */
-    or_c64 z[16];
-    for (int m = 0; m < 16; m++) z[m] = in[lam + 32 * m];
-    dft16(z, 1);
-    const int hi = (((lam >> 4) & 1) << 4) | (((lam >> 3) & 1) << 5);
-    for (int l0 = 0; l0 < 16; l0++) Y[l0 | hi][lam & 7] = z[l0];
-  }
-  for (int Lp = 0; Lp < 64; Lp++) /* conj tb, inverse radix-4 */
-    for (int g = 0; g < 2; g++) {
-      for (int m = 1; m < 4; m++) Y[Lp][g + 2 * m] = cmulc(Y[Lp][g + 2 * m], T1->tb[m][Lp & 15]);
-      radix4(Y[Lp], g, 2, 1);
-    }
-  for (int L = 0; L < 64; L++) { /* exchange back, conj twAm, inverse DFT8, conj slot twist */
-    or_c64 x[8];
-    for (int k = 0; k < 8; k++) x[k] = cmulc(Y[(L & 15) | ((k >> 1) << 4)][(k & 1) | ((L >> 4) << 1)], T->twAm[k][L]);
-    dft8(x, 1);
-    for (int e = 0; e < 8; e++) {
-      const or_c64 v = e ? cmul(x[e], T->twist[64 * e].re, -T->twist[64 * e].im) : x[e];
-      a[L + 64 * e] = v.re;
-      a[L + 64 * e + FFT_M] = v.im;
-    }
-  }
-}
-
 void or_fft_fwd(const double* a, uint32_t N, or_c64* out) {
   if (N == 4 * FFT_M) { fft1k_fwd(a, out); return; }
   if (N != 2 * FFT_M) abort();
-  fft512p_fwd(a, out);
+  const fft_tab* T = tab();
+  or_c64 z[FFT_M];
+  for (int j = 0; j < FFT_M; j++) { /* j = L + 64 e: slot constant zeta^{64 e} (e > 0), zeta^L in pass A */
+    const or_c64 v = {a[j], a[j + FFT_M]};
+    const int e = j >> 6;
+    z[j] = e ? cmul(v, T->twist[64 * e].re, T->twist[64 * e].im) : v;
+  }
+  dft512_fwd_tab(z, out, T->twAm, 1);
 }
 
 void or_fft_inv(const or_c64* in, uint32_t N, double* out) {
   if (N == 4 * FFT_M) { fft1k_inv(in, out); return; }
   if (N != 2 * FFT_M) abort();
-  fft512p_inv(in, out);
+  const fft_tab* T = tab();
+  or_c64 z[FFT_M];
+  dft512_inv_tab(in, z, T->twIm);
+  for (int j = 0; j < FFT_M; j++) { /* conj(zeta^{64 e}) after pass A' (e > 0); conj(zeta^L) rode in pass B' */
+    const int e = j >> 6;
+    const or_c64 v = e ? cmul(z[j], T->twist[64 * e].re, -T->twist[64 * e].im) : z[j];
+    out[j] = v.re;
+    out[j + FFT_M] = v.im;
+  }
 }
 
 /* round(x) (ties to even) mod 2^64; every step after rint is exact */
@@ -422,12 +440,12 @@ void or_blind_rotate_fft(const or_params* p, const or_c64* bsk_f, const uint64_t
   memset(acc, 0, (size_t)N * 8);
   const uint32_t bt = or_mod_switch(lwe_in[n], 2 * N);
   monomial_torus(acc + N, lt, N, (2 * N - bt) % (2 * N));
-  static _Thread_local double dig[2][8][4 * FFT_M]; /* [c][l][coefficient] */
-  or_c64 D[2 * FFT_M], O[2][2 * FFT_M];
-  /* MAC order (pbs_fft.hip one-wave-per-ciphertext and latency kernels, pbs_fft2k.hip): one fma chain per output j
-   * and frequency over the levels least significant first and, within a level, c = 0..k; N = 1024 starts the
-   * chain with a multiply (mac_first), N = 2048 from (0, 0) */
-  const int mul_first = N == 2 * FFT_M;
+  static _Thread_local double dig[8][4 * FFT_M];
+  or_c64 D[2 * FFT_M], O[2][2 * FFT_M], Oc[2][2 * FFT_M];
+  /* MAC order.  N = 1024 (pbs_fft.hip: component-pair and latency kernels): one fma chain per component,
+   * O_j = O_j^0 + O_j^1 with O_j^c = chain over the levels of D_(c,l) (.) BSK_i[(c, l)][j] from zero.
+   * N = 2048 (pbs_fft2k.hip): one chain over every (c, l) from zero. */
+  const int split = N == 2 * FFT_M;
   double res[4 * FFT_M];
   int64_t d[64];
   for (uint32_t i = 0; i < n; i++) {
@@ -438,33 +456,45 @@ void or_blind_rotate_fft(const or_params* p, const or_c64* bsk_f, const uint64_t
       monomial_torus(rot, acc + (size_t)c * N, N, a);
       for (uint32_t j = 0; j < N; j++) {
         or_decompose(rot[j] - acc[(size_t)c * N + j], p->pbs_base_log, L, d);
-        for (uint32_t l = 0; l < L; l++) dig[c][l][j] = (double)d[l];
+        for (uint32_t l = 0; l < L; l++) dig[l][j] = (double)d[l];
       }
-    }
-    for (int l = (int)L - 1; l >= 0; l--)
-      for (uint32_t c = 0; c <= k; c++) {
-        or_fft_fwd(dig[c][l], N, D);
+      or_c64 (*A)[2 * FFT_M] = split ? Oc : O; /* this component's chain (split) or the running one */
+      if (split) memset(Oc, 0, sizeof(Oc));
+      for (int l = (int)L - 1; l >= 0; l--) {
+        or_fft_fwd(dig[l], N, D);
         const or_c64* row = bsk_f + per_i * i + (size_t)(c * L + l) * (k + 1) * M;
-        const int first = mul_first && l == (int)L - 1 && c == 0;
+        /* N = 1024: each component chain's first term is a multiply (pbs_fft.hip mac_first: the chain does not
+         * start from a zeroed sum; the two forms differ only in the sign of an exact zero) */
+        const int first = split && l == (int)L - 1;
         for (uint32_t j = 0; j <= k; j++) {
           const or_c64* K = row + (size_t)j * M;
           if (first) {
             for (uint32_t f = 0; f < M; f++) {
-              O[j][f].re = D[f].re * K[f].re;
-              O[j][f].re = fma(-D[f].im, K[f].im, O[j][f].re);
-              O[j][f].im = D[f].re * K[f].im;
-              O[j][f].im = fma(D[f].im, K[f].re, O[j][f].im);
+              A[j][f].re = D[f].re * K[f].re;
+              A[j][f].re = fma(-D[f].im, K[f].im, A[j][f].re);
+              A[j][f].im = D[f].re * K[f].im;
+              A[j][f].im = fma(D[f].im, K[f].re, A[j][f].im);
             }
             continue;
           }
           for (uint32_t f = 0; f < M; f++) {
-            O[j][f].re = fma(D[f].re, K[f].re, O[j][f].re);
-            O[j][f].re = fma(-D[f].im, K[f].im, O[j][f].re);
-            O[j][f].im = fma(D[f].re, K[f].im, O[j][f].im);
-            O[j][f].im = fma(D[f].im, K[f].re, O[j][f].im);
+            A[j][f].re = fma(D[f].re, K[f].re, A[j][f].re);
+            A[j][f].re = fma(-D[f].im, K[f].im, A[j][f].re);
+            A[j][f].im = fma(D[f].re, K[f].im, A[j][f].im);
+            A[j][f].im = fma(D[f].im, K[f].re, A[j][f].im);
           }
         }
       }
+      if (split)
+        for (uint32_t j = 0; j <= k; j++)
+          for (uint32_t f = 0; f < M; f++) {
+            if (c == 0) O[j][f] = Oc[j][f];
+            else {
+              O[j][f].re = O[j][f].re + Oc[j][f].re;
+              O[j][f].im = O[j][f].im + Oc[j][f].im;
+            }
+          }
+    }
     for (uint32_t j = 0; j <= k; j++) {
       or_fft_inv(O[j], N, res);
       for (uint32_t f = 0; f < N; f++) acc[(size_t)j * N + f] += or_f64_to_torus(res[f]);

@@ -15,11 +15,9 @@ from conftest import KEY_SEED
 N, M = 1024, 512
 
 
-# device order (fft512p.h): index d = lam + 32 m1 holds frequency
-#   k = (lam & 1) + 2 ((lam >> 4) & 1) + 4 ((lam >> 3) & 1) + 8 ((lam >> 1) & 3) + 32 m1
+# device order: slot d = L + 64 e holds frequency k = (L >> 3) + 8 (L & 7) + 64 e
 _D = np.arange(M)
-_LAM, _M1 = _D % 32, _D // 32
-DEVICE_ORDER = (_LAM & 1) + 2 * ((_LAM >> 4) & 1) + 4 * ((_LAM >> 3) & 1) + 8 * ((_LAM >> 1) & 3) + 32 * _M1
+DEVICE_ORDER = (_D % 64 >> 3) + 8 * (_D % 8) + 64 * (_D // 64)
 
 
 def _dft_definition(a):

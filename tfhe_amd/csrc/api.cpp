@@ -1079,7 +1079,7 @@ const char* tfhe_hip_br_kernel(const tfhe_ctx* c, size_t B) {
   if (!c) return nullptr;
   const bool lat = B <= c->lat_max;
   if (is_fft(c->p) && c->p.N == 2048) return "blind_rotate_fft2k_kernel";  // <2, ...> latency, <4, ...> batch
-  if (is_fft(c->p)) return lat ? "blind_rotate_fft_lat_kernel" : "blind_rotate_fft_ct_kernel";
+  if (is_fft(c->p)) return lat ? "blind_rotate_fft_lat_kernel" : "blind_rotate_fft_pair_kernel";
   if (c->p.N == 2048) return lat ? "blind_rotate2048_lat_kernel" : "blind_rotate2048_kernel";
   return lat ? "blind_rotate_lat_kernel" : "blind_rotate_kernel";
 }

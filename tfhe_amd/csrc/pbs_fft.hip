@@ -2,21 +2,27 @@
 // PBS 2^7 x 3): the external product computed the way tfhe-rs computes it, with an f64 negacyclic
 // FFT over the native 2^64 torus, instead of the Goldilocks NTT of pbs_kernels.hip.
 //
-// Why: MI355X runs f64 add / mul / fma at the full VALU rate (4-5 cycles per wave-instruction, the same
-// as a 32-bit integer op), and a complex radix-2 butterfly is ~8 such instructions where a Goldilocks
-// butterfly is ~30 integer ones.  Same BSK bytes (N/2 complex doubles = N u64 per polynomial).
+// Why: MI355X runs f64 add / mul / fma at the full VALU rate (~6 cycles per wave-instruction, the
+// same as a 32-bit integer op, tools/microbench/f64_rates.hip), and a complex radix-2 butterfly is ~8
+// such instructions where a Goldilocks butterfly is ~30 integer ones.  Same BSK bytes (N/2 complex
+// doubles = N u64 per polynomial); the batch kernel walks the CMUX loop with 4 ciphertexts x 2 component
+// waves per workgroup in lockstep, the BSK level steps streamed once per workgroup into LDS by
+// global_load_lds, double-buffered.
 //
 // Arithmetic (one fixed f64 operation sequence, restated in oracle/fft_oracle.c, which this file
 // reproduces bit-for-bit — every product is written as an explicit fma or a lone multiply, and
 // contraction is off for the whole file):
 //   fold + twist  z_j = (a_j + i a_{j+512}) * zeta^j,   zeta = e^{i pi / 1024}
-//   DFT           Z_k = sum_j z_j e^{+2 pi i jk / 512}: fft512p.h (DFT8 over the slots, a register exchange,
-//                 radix-4, ONE LDS transpose, DFT16), natural order in, DEVICE ORDER out (fft512p.h); the
-//                 inverse runs the stages reversed, device order in, natural order out
-//   MAC           O_j = one fma chain per frequency over the levels least significant first and, within a level,
-//                 c = 0, 1 (each level's digits come off a running carry state, so the device BSK stores the
-//                 level rows least significant first: [i][q][c][j], q = 2 - l); the first term a multiply
-//   inverse       conjugate stages, untwist by conj(zeta^j), rint, mod 2^64, add to the accumulator
+//   DFT           Z_k = sum_j z_j e^{+2 pi i jk / 512}: 3 radix-8 passes over the wave's 64 lanes
+//                 x 8 registers, natural order in, DEVICE ORDER out (slot e of lane L holds
+//                 k = (L >> 3) + 8 (L & 7) + 64 e); the inverse runs the passes reversed (DIT), device
+//                 order in, natural order out.  Two LDS transposes each way with plain padded rows
+//                 (strides 72 and 65 complex): every ds_write_b128 / ds_read_b128 is conflict-free and
+//                 every address is a per-lane base plus an immediate offset
+//   MAC           O_j += D_(c,l) (.) BSK_i[(c,l)][j], 4 fma per complex; c ascending, levels least
+//                 significant first (each level's digits come off a running carry state, so the device
+//                 BSK stores the level rows of each component reversed)
+//   inverse       conjugate passes, untwist by conj(zeta^j), rint, mod 2^64, add to the accumulator
 // Coefficient 64 e + L of a u64 register polynomial (slot e of lane L, e < 16) meets coefficient
 // 64 (e + 8) + L in the same lane, so folding and unfolding move no data.
 #pragma clang fp contract(off)
@@ -24,13 +30,33 @@
 
 #include <type_traits>
 
-#include "fft512p.h"
+#include "fft512.h"
 #include "gl64.h"
 #include "ntt1024.h"
 #include "pbs_kernels.h"
 
 namespace tfhe {
 namespace fftk {
+
+// forward transform of a real polynomial held as 16 doubles per lane (slot e <-> coefficient 64 e + L)
+// (twist: slot constants here, the lane part inside pass A — fft512.h, "N = 1024 merged twist")
+__device__ __forceinline__ void fft_fwd_real(const double (&a)[16], double (&xr)[8], double (&xi)[8], double2* T,
+                                             int lane, const double2* tw) {
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    xr[e] = a[e];
+    xi[e] = a[e + 8];
+  }
+  twist_slots<false>(xr, xi);
+  dft512_fwd<true>(xr, xi, T, lane, TBase(lane), tw);
+}
+
+// inverse transform (no 1/M) + untwist: slot e -> coefficient 64 e + L (re), 64 (e + 8) + L (im)
+__device__ __forceinline__ void fft_inv_real(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
+                                             const double2* tw) {
+  dft512_inv(xr, xi, T, lane, tb, tw);
+  twist_slots<true>(xr, xi);  // the lane part of the untwist rode in pass B''s table
+}
 
 __device__ __forceinline__ int ms2048(u64 x) { return (int)((((x >> 52) + 1) >> 1) & 2047u); }
 
@@ -52,7 +78,7 @@ __device__ __forceinline__ int decomp_step(u32& st, u32 bmask) {
 // the top level (b = 0, no next state): 3 VALU per digit
 __device__ __forceinline__ int decomp_top(u32 st) { return (int)(st - ((st + 63u) & ~127u)); }
 
-// o = D (.) K as the first term of the fma chain: a multiply where the chain would add to +0 (the oracle's
+// o = D (.) K as the first term of an fma chain: a multiply where the chain would add to +0 (the oracle's
 // first term; the two differ only in the sign of an exact zero, which no later step can turn into a non-zero)
 __device__ __forceinline__ void mac_first(double& re, double& im, double dr, double di, double2 k) {
   re = dr * k.x;
@@ -67,185 +93,225 @@ __device__ __forceinline__ void mac_next(double& re, double& im, double dr, doub
   im = __builtin_fma(di, k.x, im);
 }
 
-}  // namespace fftk
-
-namespace fftp {
-using fftk::decomp_state;
-using fftk::decomp_step;
-using fftk::decomp_top;
-using fftk::mac_first;
-using fftk::mac_next;
-using fftk::ms2048;
-
 // ---------------------------------------------------------------------------------------------
-// BSK conversion: one wavefront per standard-layout polynomial [i][c * 3 + l][j] (l = 0 most significant) ->
-// device layout [i][q = 2 - l][c][j], 512 complex in device order, x 2^-9
+// BSK conversion: one wavefront per polynomial; [i][r][j] order kept, 512 complex natural, x 2^-9
 __global__ __launch_bounds__(64) void bsk_to_fourier_kernel(const u64* __restrict__ bsk_std,
                                                             double2* __restrict__ bsk_f,
-                                                            const double2* __restrict__ tab) {
-  __shared__ __attribute__((aligned(16))) double2 area[PS_C64];
+                                                            const double2* __restrict__ tw) {
+  __shared__ __attribute__((aligned(16))) double2 T[T_C64];
   const int lane = threadIdx.x;
-  TwP w;
-  w.load(tab, lane);
-  const size_t qs = blockIdx.x;
-  const u64* src = bsk_std + qs * N1K;
-  double ar[8], ai[8], xr[16], xi[16];
+  const size_t q = blockIdx.x;  // standard layout [i][c*3 + l][j]
+  const u64* src = bsk_std + q * N1K;
+  double a[16], xr[8], xi[8];
 #pragma unroll
-  for (int e = 0; e < 8; e++) {
-    ar[e] = i64_to_f64(src[64 * e + lane]);
-    ai[e] = i64_to_f64(src[64 * e + 512 + lane]);
-  }
-  fwd_single(ar, ai, xr, xi, area, TBaseP(lane, true), w);
-  const size_t j = qs % 2, r = (qs / 2) % 6, i = qs / 12, c = r / 3, q = 2 - r % 3;
-  double2* dst = bsk_f + ((i * 6 + 2 * q + c) * 2 + j) * MP;
-  if (lane < 32) {
+  for (int e = 0; e < 16; e++) a[e] = i64_to_f64(src[64 * e + lane]);
+  fft_fwd_real(a, xr, xi, T, lane, tw);
+  const size_t j = q % 2, r = (q / 2) % 6, i = q / 12;  // device layout [i][c*3 + (2 - l)][j]
+  double2* dst = bsk_f + ((i * 6 + (r / 3) * 3 + (2 - r % 3)) * 2 + j) * M;
 #pragma unroll
-    for (int m = 0; m < 16; m++) dst[lane + 32 * m] = make_double2(xr[m] * 0x1p-9, xi[m] * 0x1p-9);
-  }
+  for (int e = 0; e < 8; e++) dst[64 * e + lane] = make_double2(xr[e] * 0x1p-9, xi[e] * 0x1p-9);
 }
 
-// natural-order transforms for the parity tests (one wavefront per polynomial; spectra in device order)
+// natural-order transforms for the parity tests (one wavefront per polynomial)
 __global__ __launch_bounds__(64) void fft_fwd_kernel(const u64* __restrict__ in, double2* __restrict__ out,
-                                                     const double2* __restrict__ tab) {
-  __shared__ __attribute__((aligned(16))) double2 area[PS_C64];
+                                                     const double2* __restrict__ tw) {
+  __shared__ __attribute__((aligned(16))) double2 T[T_C64];
   const int lane = threadIdx.x;
-  TwP w;
-  w.load(tab, lane);
   const u64* src = in + (size_t)blockIdx.x * N1K;
-  double ar[8], ai[8], xr[16], xi[16];
+  double a[16], xr[8], xi[8];
 #pragma unroll
-  for (int e = 0; e < 8; e++) {
-    ar[e] = i64_to_f64(src[64 * e + lane]);
-    ai[e] = i64_to_f64(src[64 * e + 512 + lane]);
-  }
-  fwd_single(ar, ai, xr, xi, area, TBaseP(lane, true), w);
-  double2* dst = out + (size_t)blockIdx.x * MP;
-  if (lane < 32) {
+  for (int e = 0; e < 16; e++) a[e] = i64_to_f64(src[64 * e + lane]);
+  fft_fwd_real(a, xr, xi, T, lane, tw);
+  double2* dst = out + (size_t)blockIdx.x * M;
 #pragma unroll
-    for (int m = 0; m < 16; m++) dst[lane + 32 * m] = make_double2(xr[m], xi[m]);
-  }
+  for (int e = 0; e < 8; e++) dst[64 * e + lane] = make_double2(xr[e], xi[e]);
 }
 
 __global__ __launch_bounds__(64) void fft_inv_kernel(const double2* __restrict__ in, double* __restrict__ out,
-                                                     const double2* __restrict__ tab) {
-  __shared__ __attribute__((aligned(16))) double2 area[PS_C64];
+                                                     const double2* __restrict__ tw) {
+  __shared__ __attribute__((aligned(16))) double2 T[T_C64];
   const int lane = threadIdx.x;
-  TwP w;
-  w.load(tab, lane);
-  const double2* src = in + (size_t)blockIdx.x * MP;
-  double xr[16], xi[16], ar[8], ai[8];
+  const double2* src = in + (size_t)blockIdx.x * M;
+  double xr[8], xi[8];
 #pragma unroll
-  for (int m = 0; m < 16; m++) {
-    const double2 v = src[(lane & 31) + 32 * m];
-    xr[m] = v.x;
-    xi[m] = v.y;
+  for (int e = 0; e < 8; e++) {
+    const double2 v = src[64 * e + lane];
+    xr[e] = v.x;
+    xi[e] = v.y;
   }
-  inv_single(xr, xi, ar, ai, area, TBaseP(lane, true), w);
+  fft_inv_real(xr, xi, T, lane, TBase(lane), tw);
   double* dst = out + (size_t)blockIdx.x * N1K;
 #pragma unroll
   for (int e = 0; e < 8; e++) {
-    dst[64 * e + lane] = ar[e];
-    dst[64 * e + 512 + lane] = ai[e];
+    dst[64 * e + lane] = xr[e];
+    dst[64 * (e + 8) + lane] = xi[e];
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// One-wave-per-ciphertext batch kernel (round 4, the default above the latency range).  A workgroup is CTS
-// ciphertexts, one wave each; the wave holds both accumulator polynomials (32 u64 per lane).  Per CMUX i:
-//   rotate + decompose both components through the wave's LDS area (rotation by DS offsets)
-//   level steps q = 0, 1, 2 (least significant first): digits of BOTH components -> ONE pair transform
-//     (fft512p.h: one LDS round trip for two polynomials) -> lane 32 p + lam holds D_p at slots m1; one
-//     v_permlane32_swap per value then gives every lane D_0 and D_1 at the same 8 frequencies
-//     (m1 = i + 8 (lane >> 5), i = slot) -> MAC into O_0, O_1 (the oracle's chain: (q, c = 0), (q, c = 1), ...)
-//     against the level step's chunk (rows (c, j) of level q of BSK_i, 32 KB) streamed once per workgroup
-//     into LDS by global_load_lds
-//   a second permlane32 swap returns O_0 to lanes 0-31 and O_1 to lanes 32-63 (all 16 slots), ONE pair
-//   inverse transform, acc += rint mod 2^64
-// Against round 3's component-pair kernel (a wave per component, two 512-point transforms of two LDS round trips
-// each per level, a partial-sum exchange through LDS and two barriers): per ciphertext and CMUX 5 LDS round trips
-// instead of 20, 80 KB of LDS stores instead of 160 KB, no exchange.  Registers: accumulators 64, partial sums 64,
-// the pair in flight 64, digit states 32 — one wave per SIMD (512 registers), so CTS = 4 per CU.
-// LDS: CTS = 4: two 32 KB level-step buffers + the 9 KB twiddle table + 4 x 17 KB areas = 141 KB (one workgroup per
-//      CU); CTS = 2: one buffer + table + 2 areas = 75 KB (two workgroups per CU, FFT_CT_CTS=2 for A/B).
-#ifndef FFT_CT_CTS
-#define FFT_CT_CTS 4
-#endif
-// FFT_PRIO: s_setprio 1 for the upper half of the waves (round 1: the second-dispatched wave of a SIMD pair
-// otherwise loses VALU arbitration after every barrier); kept switchable for the one-wave-per-SIMD layout
+// FFT_PRIO: s_setprio 1 for waves 4-7 (the second-dispatched wave of each SIMD pair) for the whole
+// CMUX loop (round 1, measured on the 8-ciphertext kernel 29.36 -> 29.25 ms per 4096: both waves of a SIMD run the
+// same lockstep program, the younger one otherwise loses VALU arbitration after every barrier).
 #ifndef FFT_PRIO
-#define FFT_PRIO 0
+#define FFT_PRIO 1
 #endif
-constexpr int STEP_C64 = 4 * MP;  // rows (c, j) of one level, [c][j][512]
 
-template <int CTS, int NBUF>
-struct CtShared {
-  double2 K[NBUF][STEP_C64];  // first: an area's base minus 8 KB (the rotation's wrapped reads) stays in the block
-  double2 tab[P_C64];         // ta | tb (TwL reads them at each use)
-  double2 T[CTS][PA_C64];
+// Component-pair batch kernel (round 3, the default above the latency range): workgroup = CTS ciphertexts x 2
+// waves (CTS = 2 by default, 4 in round 3), wave (p, c) owns COMPONENT c of ciphertext p.  Per CMUX i:
+//   rotate + decompose acc_c (wave-local: the wave's own transpose area holds the rotation image)
+//   level steps q = 0, 1, 2 (least significant first): digits -> twist -> DFT -> MAC into BOTH outputs'
+//     partial sums  O_j^c = fma chain over q of D_(c,q) (.) BSK_i[(c, q)][j]      (j = 0, 1)
+//     one step's chunk = rows (0, q) and (1, q) of BSK_i (32 KB), streamed once per workgroup by
+//     global_load_lds (CTS = 4: double-buffered; CTS = 2: one buffer, loaded at the step's start)
+//   exchange: wave c publishes O_(1-c)^c in its transpose area and takes O_c^(1-c) from its partner's:
+//     O_c = O_c^c + O_c^(1-c)  (= O_c^0 + O_c^1: f64 addition commutes, the oracle's split order)
+//   ONE inverse transform: acc_c += rint(iFFT(O_c)) mod 2^64
+// Against round 2's 8-ciphertext kernel (one wave per ciphertext, retired in round 4): the same transforms per
+// ciphertext, half of them per wave, 1/2 the accumulator / partial-sum registers per wave, and twice the waves
+// per ciphertext -- a batch of 1024 fills all 256 CUs at 2 waves / SIMD.
+// The MAC order (per-component chains, then one add) is restated in oracle/fft_oracle.c.
+// LDS at CTS = 4: 8 x 9 KB transpose areas | 2 x 32 KB level steps | pass A, B, B' tables (24 KB) = 160 KB;
+// at CTS = 2: B' table (8 KB) | one 32 KB level step | 4 x 9 KB transpose areas = 76 KB, two workgroups per CU.
+// FFT_ROT_BATCH: the rotation's 16 image reads issued together before their first use (measured with the
+// first level peeled: 27.04 -> 27.55 ms per 4096, slower; kept for A/B runs)
+#ifndef FFT_ROT_BATCH
+#define FFT_ROT_BATCH 0
+#endif
+// FFT_PAIR_TWREG: pass A's twiddles held in registers across the CMUX loop (the round-2 ablation: -4 %)
+#ifndef FFT_PAIR_TWREG
+#define FFT_PAIR_TWREG 2
+#endif
+constexpr int STEP_C64 = 4 * M;                    // rows (0, q), (1, q), j = 0, 1
+// CTS = ciphertexts per workgroup.  2 (default since round 4): 4 waves, TWO independent workgroups per CU (76 KB
+// each: only the inverse's TW_I table in LDS, passes A / B from registers, one level-step buffer), so the two
+// workgroups drift apart and one's LDS phases overlap the other's VALU phases on every SIMD: 27.01 -> 26.63 ms per
+// 4096 on the same box (profiles/r04a_cts_ab.txt, two rounds).  4 (FFT_PAIR_CTS=4): 8 waves, one workgroup per CU,
+// all tables in LDS, level steps double-buffered (the round-3 kernel).
+template <int CTS>
+struct FpShared {
+  double2 tw[3 * M];                               // TW_A | TW_B | TW_I of the global table (no twist table)
+  double2 T[2 * CTS][T_C64];                       // after the tables: T - 8 KB is still inside the block
+  double2 K[2][STEP_C64];
 };
-
+template <>
+struct FpShared<2> {
+  double2 twI[M];                                  // TW_I only (passes A, B: registers, loaded from global)
+  double2 K[1][STEP_C64];
+  double2 T[4][T_C64];
+};
+#ifndef FFT_PAIR_CTS
+#define FFT_PAIR_CTS 2
+#endif
 typedef __attribute__((address_space(3))) u64 lds_u64;
 
-// level step g = 3 i + q: 32 KB in 1 KB blocks; wave w of CTS loads blocks (32 / CTS) w ..
-template <int CTS>
-__device__ __forceinline__ void load_step(const double2* __restrict__ bsk, int g, double2* dst, int wave_s, int lane) {
-  const char* src = (const char*)(bsk + (size_t)g * STEP_C64);
+// (X^a v - v), v = this wave's polynomial (slot e <-> coefficient 64 e + L), to decomposition states.  The
+// rotation image is the wave's transpose area.  Coefficient 64 e + L reads image entry (u + 64 e) mod 1024 with
+// u = (L - a) mod 1024, negated iff the negacyclic source index (L - a + 64 e) mod 2048 lies in [1024, 2048):
+// reads before the per-lane wrap use base u and DS offset 512 e, wrapped reads the base 8 KB lower (one compare
+// and one select per slot instead of the index arithmetic; the sign mask is an SGPR xor).
+__device__ __forceinline__ void rotate_states(const u64 (&v)[16], int a, int lane, double2* T, u32 (&st)[16]) {
+  u64* Tu = (u64*)T;
 #pragma unroll
-  for (int u = 0; u < 32 / CTS; u++) {
-    const int blk = wave_s * (32 / CTS) + u;
-    __builtin_amdgcn_global_load_lds((const void*)(src + blk * 1024 + lane * 16),
+  for (int e = 0; e < 16; e++) Tu[64 * e + lane] = v[e];
+  lds_order();
+  const int t0 = (lane - a) & 2047;        // a < 2048
+  const int u = t0 & 1023;
+  const bool neg0 = t0 >= 1024;
+  const u32 a0 = (u32)(uintptr_t)(lds_u64*)&Tu[u];
+  const u32 a1 = a0 - 8192u;
+#if FFT_ROT_BATCH
+  u64 x[16];
+#pragma unroll
+  for (int e = 0; e < 16; e++) {
+    const bool wrap = u >= 1024 - 64 * e;
+    x[e] = ((const lds_u64*)(uintptr_t)(wrap ? a1 : a0))[64 * e];
+  }
+  __builtin_amdgcn_sched_barrier(0);  // all 16 reads in flight before the first use
+#pragma unroll
+  for (int e = 0; e < 16; e++) {
+    const bool neg = neg0 != (u >= 1024 - 64 * e);
+    const u64 r = neg ? 0 - x[e] : x[e];
+    st[e] = decomp_state(r - v[e]);
+  }
+#else
+#pragma unroll
+  for (int e = 0; e < 16; e++) {
+    const bool wrap = u >= 1024 - 64 * e;
+    const u32 base = wrap ? a1 : a0;
+    const u64 x = ((const lds_u64*)(uintptr_t)base)[64 * e];
+    const bool neg = neg0 != wrap;
+    const u64 r = neg ? 0 - x : x;
+    st[e] = decomp_state(r - v[e]);
+  }
+#endif
+  lds_order();
+}
+
+// the partial-sum exchange of wave c (compile-time): publish O_(1-c)^c in this wave's area, add O_c^(1-c) from
+// the partner's (two workgroup barriers)
+template <int C>
+__device__ __forceinline__ void exchange_partials(const double (&o0r)[8], const double (&o0i)[8], const double (&o1r)[8],
+                                                  const double (&o1i)[8], double (&xr)[8], double (&xi)[8], double2* T,
+                                                  const double2* Tp, int lane) {
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    T[64 * e + lane] = C ? make_double2(o0r[e], o0i[e]) : make_double2(o1r[e], o1i[e]);
+    xr[e] = C ? o1r[e] : o0r[e];
+    xi[e] = C ? o1i[e] : o0i[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 w = Tp[64 * e + lane];
+    xr[e] = xr[e] + w.x;
+    xi[e] = xi[e] + w.y;
+  }
+  __syncthreads();  // the partner has read this wave's area before the inverse overwrites it
+}
+
+// level step g = 3 i + q: 32 KB in 1 KB blocks; wave w of NW loads blocks (32 / NW) w .. (16 per component row)
+template <int NW>
+__device__ __forceinline__ void load_step(const double2* __restrict__ bsk, int g, double2* dst, int wave_s, int lane) {
+  const int i = g / 3, q = g - 3 * (g / 3);
+#pragma unroll
+  for (int u = 0; u < 32 / NW; u++) {
+    const int blk = wave_s * (32 / NW) + u;
+    const int c = blk >> 4;
+    const char* src = (const char*)(bsk + ((size_t)i * 6 + c * 3 + q) * (2 * M)) + (blk & 15) * 1024;
+    __builtin_amdgcn_global_load_lds((const void*)(src + lane * 16),
                                      (__attribute__((address_space(3))) void*)((char*)dst + blk * 1024), 16, 0, 0);
   }
 }
 
-// (X^a v_c - v_c) for both components c (v[16 c + e] <-> coefficient 64 e + L of component c), to decomposition
-// states.  The rotation image is the wave's area (component c at u64 offset 1024 c).  Coefficient 64 e + L reads
-// image entry (u + 64 e) mod 1024 with u = (L - a) mod 1024, negated iff the negacyclic source index
-// (L - a + 64 e) mod 2048 lies in [1024, 2048): reads before the per-lane wrap use base u and DS offset 512 e,
-// wrapped reads the base 8 KB lower.
-__device__ __forceinline__ void rotate_states2(const u64 (&v)[32], int a, int lane, double2* T, u32 (&st)[32]) {
-  u64* Tu = (u64*)T;
-#pragma unroll
-  for (int e = 0; e < 32; e++) Tu[64 * e + lane] = v[e];
-  lds_order();
-  const int t0 = (lane - a) & 2047;  // a < 2048
-  const int u = t0 & 1023;
-  const bool neg0 = t0 >= 1024;
-  const u32 a0 = (u32)(uintptr_t)(lds_u64*)&Tu[u];
-#pragma unroll
-  for (int c = 0; c < 2; c++)
-#pragma unroll
-    for (int e = 0; e < 16; e++) {
-      const bool wrap = u >= 1024 - 64 * e;
-      const u32 base = (wrap ? a0 - 8192u : a0) + 8192u * c;
-      const u64 x = ((const lds_u64*)(uintptr_t)base)[64 * e];
-      const bool neg = neg0 != wrap;
-      const u64 r = neg ? 0 - x : x;
-      st[16 * c + e] = decomp_state(r - v[16 * c + e]);
-    }
-  lds_order();
-}
-
 template <int CTS, bool WRITE_ACC, bool WRITE_BIG>
-__global__ __launch_bounds__(64 * CTS, 1) void blind_rotate_fft_ct_kernel(
+__global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kernel(
     const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
-    int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tab, u64* __restrict__ out_big,
+    int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tw_g, u64* __restrict__ out_big,
     u64* __restrict__ out_acc) {
-  constexpr int NBUF = CTS >= 4 ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) CtShared<CTS, NBUF> sh;
+  constexpr int NW = 2 * CTS;
+  constexpr bool LDS_TW = CTS == 4;
+  __shared__ __attribute__((aligned(16))) FpShared<CTS> sh;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
-  const size_t b_raw = (size_t)blockIdx.x * CTS + wave;
+  const int c = wave & 1;
+  const size_t b_raw = (size_t)blockIdx.x * CTS + (wave >> 1);
   const bool live = b_raw < B;
-  const size_t b = live ? b_raw : B - 1;  // padding waves run a copy of the last ciphertext, store nothing
+  const size_t b = live ? b_raw : B - 1;  // padding pairs run a copy of the last ciphertext, store nothing
   const u64* ct = lwe_in + b * (size_t)(n + 1);
-  double2* T = sh.T[wave_s];
+  double2* T = sh.T[wave];
+  const double2* Tp = sh.T[wave ^ 1];
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const int c_s = wave_s & 1;
   const int n_steps = 3 * n;
-  if constexpr (NBUF == 2) load_step<CTS>(bsk, 0, sh.K[0], wave_s, lane);
-  for (int q = threadIdx.x; q < P_C64; q += 64 * CTS) sh.tab[q] = tab[q];
 
-  // acc: A = 0, B = X^{-b~} * lut (LUT values in the Z_p encoding, mapped to the torus first)
-  u64 acc[32];
+  if constexpr (LDS_TW) {
+    for (int q = threadIdx.x; q < 3 * M; q += 64 * NW) sh.tw[q] = tw_g[TW_A + q];
+    load_step<NW>(bsk, 0, sh.K[0], wave_s, lane);
+  } else {
+    for (int q = threadIdx.x; q < M; q += 64 * NW) sh.twI[q] = tw_g[TW_I + q];
+  }
+
+  // acc_c: A = 0, B = X^{-b~} * lut (LUT values in the Z_p encoding, mapped to the torus first)
+  u64 acc[16];
   {
     int li = lut_index ? (int)lut_index[b] : 0;
     li = (li < 0 || li >= n_lut) ? 0 : li;
@@ -258,128 +324,152 @@ __global__ __launch_bounds__(64 * CTS, 1) void blind_rotate_fft_ct_kernel(
       if (d < 0) { d += N1K; neg = !neg; }
       if (d < 0) { d += N1K; neg = !neg; }
       const u64 v = gl_to_torus(lut[d]);
-      acc[e] = 0;
-      acc[16 + e] = neg ? 0 - v : v;
+      acc[e] = c ? (neg ? 0 - v : v) : 0;
     }
   }
-  __syncthreads();  // the twiddle table is in LDS
-  const TwL w(sh.tab, lane);
-  const TBaseP tb(lane, false);
-  const int kb = (lane & 31) + 256 * (lane >> 5);  // this lane's 8 frequencies after the MAC swap: d = kb + 32 i
-#if FFT_PRIO
-  if (wave_s >= CTS / 2) __builtin_amdgcn_s_setprio(1);
-#endif
 
+  const TBase tb(lane);
+  const double2* twA = tw_g + TW_A;
+  const double2* twI;
+  if constexpr (LDS_TW) {
+    twA = sh.tw;
+    twI = sh.tw + 2 * M;
+  } else {
+    twI = sh.twI;
+  }
+  const double2* twB = twA + M;
+#if FFT_PAIR_TWREG
+  double2 wa[8];  // pass A's twiddles (twist merged) for the whole CMUX loop: 8 LDS reads fewer per transform
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 8; e++) wa[e] = twA[64 * e + lane];
+#endif
+#if FFT_PAIR_TWREG >= 2
+  double2 wb[8];  // and pass B's (the inverse's pass C' conjugates the same table): 7 more per forward, 7 per inverse
+#pragma unroll
+  for (int e = 1; e < 8; e++) wb[e] = twB[64 * e + lane];
+  wb[0] = make_double2(1.0, 0.0);
+#endif
+#if FFT_PRIO == 1
+  if (wave_s >= 4) __builtin_amdgcn_s_setprio(1);
+#elif FFT_PRIO == 3
+  // A/B: with two workgroups per CU, one of them (by dispatch round) at the higher priority
+  if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_setprio(1);
+#endif
   for (int i = 0; i < n; i++) {
-    u32 st[32];
-    rotate_states2(acc, ms2048(ct[i]), lane, T, st);
+    // (X^a acc_c - acc_c), decomposed: the rotation image in this wave's own transpose area (its previous
+    // user, the last inverse, is this wave: DS operations of a wave run in order)
+    u32 st[16];
+    rotate_states(acc, ms2048(ct[i]), lane, T, st);
     double o0r[8], o0i[8], o1r[8], o1i[8];
+    // level steps q = 0, 1, 2 (least significant first), each specialised at compile time: q = 0 starts the two
+    // fma chains with a multiply (no zeroed partial sums), q = 2 takes the top digit (no carry bit, no next state)
     auto level = [&](auto qc) {
       constexpr int q = decltype(qc)::value;
       const int g = 3 * i + q;
-      if constexpr (NBUF == 2) {
+      if constexpr (LDS_TW) {
         glds_barrier();  // step g's chunk is in K[g & 1]; every wave is done with K[(g + 1) & 1]
-        if (g + 1 < n_steps) load_step<CTS>(bsk, g + 1, sh.K[(g + 1) & 1], wave_s, lane);
+        if (g + 1 < n_steps) load_step<NW>(bsk, g + 1, sh.K[(g + 1) & 1], wave_s, lane);
       } else {
-        if (g > 0) __syncthreads();  // every wave is done with step g - 1's chunk
-        load_step<CTS>(bsk, g, sh.K[0], wave_s, lane);
+        // one buffer: every wave is done with step g - 1's chunk (the exchange's barriers order q = 0)
+        if (q > 0) __syncthreads();
+        load_step<NW>(bsk, g, sh.K[0], wave_s, lane);
       }
-      double xr[16], xi[16];
+      double xr[8], xi[8];
 #pragma unroll
-      for (int c = 0; c < 2; c++)
-#pragma unroll
-        for (int e = 0; e < 8; e++) {
-          if constexpr (q == 2) {
-            xr[8 * c + e] = (double)decomp_top(st[16 * c + e]);
-            xi[8 * c + e] = (double)decomp_top(st[16 * c + 8 + e]);
-          } else {
-            xr[8 * c + e] = (double)decomp_step(st[16 * c + e], 1u);
-            xi[8 * c + e] = (double)decomp_step(st[16 * c + 8 + e], 1u);
-          }
-        }
-      fwd_pair(xr, xi, T, tb, w);
-      // D_0 to slots 0-7, D_1 to slots 8-15, both at frequencies m1 = i + 8 (lane >> 5)
-#pragma unroll
-      for (int s = 0; s < 8; s++) {
-        swap32_d(xr[s], xr[s + 8]);
-        swap32_d(xi[s], xi[s + 8]);
-      }
-      if constexpr (NBUF == 1) glds_barrier();  // step g's chunk has landed (every wave's share)
-      const double2* K = sh.K[NBUF == 2 ? (g & 1) : 0] + kb;
-#pragma unroll
-      for (int s = 0; s < 8; s++) {
-        const double2 k00 = K[32 * s], k01 = K[MP + 32 * s], k10 = K[2 * MP + 32 * s], k11 = K[3 * MP + 32 * s];
-        if constexpr (q == 0) {
-          mac_first(o0r[s], o0i[s], xr[s], xi[s], k00);
-          mac_first(o1r[s], o1i[s], xr[s], xi[s], k01);
+      for (int e = 0; e < 8; e++) {
+        if constexpr (q == 2) {
+          xr[e] = (double)decomp_top(st[e]);
+          xi[e] = (double)decomp_top(st[e + 8]);
         } else {
-          mac_next(o0r[s], o0i[s], xr[s], xi[s], k00);
-          mac_next(o1r[s], o1i[s], xr[s], xi[s], k01);
+          xr[e] = (double)decomp_step(st[e], 1u);
+          xi[e] = (double)decomp_step(st[e + 8], 1u);
         }
-        mac_next(o0r[s], o0i[s], xr[s + 8], xi[s + 8], k10);
-        mac_next(o1r[s], o1i[s], xr[s + 8], xi[s + 8], k11);
+      }
+      twist_slots<false>(xr, xi);
+#if FFT_PAIR_TWREG >= 2
+      dft512_fwd_rab(xr, xi, T, lane, tb, wa, wb);
+#elif FFT_PAIR_TWREG
+      dft512_fwd_ra(xr, xi, T, lane, tb, wa, twB);
+#else
+      dft512_fwd_t<true>(xr, xi, T, lane, tb, twA, twB);
+#endif
+      if constexpr (!LDS_TW) glds_barrier();  // step g's chunk has landed
+      const double2* k0 = sh.K[LDS_TW ? (g & 1) : 0] + c * (2 * M) + lane;
+      const double2* k1 = k0 + M;
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const double2 u = k0[64 * e], v = k1[64 * e];
+        if constexpr (q == 0) {
+          mac_first(o0r[e], o0i[e], xr[e], xi[e], u);
+          mac_first(o1r[e], o1i[e], xr[e], xi[e], v);
+        } else {
+          mac_next(o0r[e], o0i[e], xr[e], xi[e], u);
+          mac_next(o1r[e], o1i[e], xr[e], xi[e], v);
+        }
       }
     };
     level(std::integral_constant<int, 0>{});
     level(std::integral_constant<int, 1>{});
     level(std::integral_constant<int, 2>{});
-    // O_0 to lanes 0-31, O_1 to lanes 32-63, all 16 slots
-    double yr[16], yi[16];
+    // exchange the partial sums: publish O_(1-c)^c, take O_c^(1-c) (c wave-uniform: a scalar branch, no selects)
+    double xr[8], xi[8];
+    if (c_s) exchange_partials<1>(o0r, o0i, o1r, o1i, xr, xi, T, Tp, lane);
+    else exchange_partials<0>(o0r, o0i, o1r, o1i, xr, xi, T, Tp, lane);
+#if FFT_PAIR_TWREG >= 2
+    dft512_inv_rb(xr, xi, T, lane, tb, wb, twI);
+#else
+    dft512_inv_t(xr, xi, T, lane, tb, twB, twI);
+#endif
+    twist_slots<true>(xr, xi);
 #pragma unroll
-    for (int s = 0; s < 8; s++) {
-      swap32_d(o0r[s], o1r[s]);
-      swap32_d(o0i[s], o1i[s]);
-      yr[s] = o0r[s];
-      yi[s] = o0i[s];
-      yr[s + 8] = o1r[s];
-      yi[s + 8] = o1i[s];
+    for (int e = 0; e < 8; e++) {
+      acc[e] += f64_to_torus(xr[e]);
+      acc[e + 8] += f64_to_torus(xi[e]);
     }
-    inv_pair(yr, yi, T, tb, w);
-#pragma unroll
-    for (int c = 0; c < 2; c++)
-#pragma unroll
-      for (int e = 0; e < 8; e++) {
-        acc[16 * c + e] += f64_to_torus(yr[8 * c + e]);
-        acc[16 * c + 8 + e] += f64_to_torus(yi[8 * c + e]);
-      }
   }
 
   if (!live) return;
   if (WRITE_ACC) {
-    u64* oa = out_acc + b * 2048;
+    u64* oa = out_acc + b * 2048 + c * N1K;
 #pragma unroll
-    for (int e = 0; e < 32; e++) oa[64 * e + lane] = acc[e];
+    for (int e = 0; e < 16; e++) oa[64 * e + lane] = acc[e];
   }
   if (WRITE_BIG) {
     // sample extraction at degree 0 (computations.rs:109-132): a'_0 = A[0], a'_j = -A[N-j], b' = B[0]
     u64* ob = out_big + b * (size_t)(N1K + 1);
+    if (c == 0) {
 #pragma unroll
-    for (int e = 0; e < 16; e++) {
-      const int idx = 64 * e + lane;
-      if (idx == 0) ob[0] = acc[e];
-      else ob[N1K - idx] = 0 - acc[e];
+      for (int e = 0; e < 16; e++) {
+        const int idx = 64 * e + lane;
+        if (idx == 0) ob[0] = acc[e];
+        else ob[N1K - idx] = 0 - acc[e];
+      }
+    } else if (lane == 0) {
+      ob[N1K] = acc[0];
     }
-    if (lane == 0) ob[N1K] = acc[16];
   }
 }
 
 // ---------------------------------------------------------------------------------------------
 // Latency-mode blind rotation (small batches): ONE ciphertext per workgroup of 8 waves.  Per CMUX:
-//   A  waves 0..5: wave r = 2 q + c (level q least significant first, component c) rotates + decomposes
-//      accumulator polynomial c, keeps level q's digits and runs the single-polynomial transform -> F[r]
-//   B  all 8 waves: O_j = the oracle's chain over r = 0..5 of F[r] (.) BSK_i[q][c][j] on 128 of the 512
-//      frequencies each (j = wave >> 2); the key words come straight from L2 into registers, requested one CMUX
-//      ahead
-//   C  waves 0, 1: single inverse transform of O_j, acc_j += rint mod 2^64
-// Three barriers per CMUX.  LDS: acc 16 KB | F 48 KB | 6 transpose areas 51 KB (O_0, O_1 alias areas 2, 3, dead
-// after phase A) | rotation amounts 2 KB | twiddle table 9 KB = 126 KB.
+//   A  waves 0..5: wave r = chain position (c, q) (c = r / 3; q = 0, 1, 2: levels least significant
+//      first) rotates + decomposes accumulator polynomial c, keeps step q's digits and transforms
+//      them -> F[r]                                                     (6 transforms in parallel)
+//   B  all 8 waves: O_j = O_j^0 + O_j^1, O_j^c = fma chain over r = 3c .. 3c + 2 of F[r] (.) BSK_i[r][j]
+//      (the oracle's split order) on 2 of the 8 slots each (j = wave >> 2); the BSK words come straight from L2, loaded into
+//      registers before phase A so their latency hides behind the transforms
+//   C  waves 0, 1: inverse transform of O_j, acc_j += rint mod 2^64      (2 transforms in parallel)
+// Three barriers per CMUX; the critical path is 1 forward + 1 inverse transform + 1/4 of the MAC
+// instead of 6 + 2 + all of it.  LDS (tables first: small DS immediates): tw 32 KB | acc 16 KB |
+// F 48 KB | 6 transpose areas 54 KB (O_0, O_1 alias areas 2, 3, dead after phase A) = 150 KB.
 constexpr int FL_THREADS = 512;
 constexpr int FL_MAXN = 1024;  // rotation amounts staged in LDS up to this LWE dimension (global reads above)
 struct FftLatShared {
-  double2 tab[P_C64];
+  double2 tw[TW_C64];
   u64 A[2][N1K];
-  double2 F[6][MP];
-  double2 T[6][PS_C64];
+  double2 F[6][M];
+  double2 T[6][T_C64];
   unsigned short ab[FL_MAXN];  // ms2048(ct[i]) for every CMUX
 };
 
@@ -391,15 +481,15 @@ __device__ __forceinline__ void lat_load_key(const double2* __restrict__ bsk, in
 #pragma unroll
   for (int r = 0; r < 6; r++)
 #pragma unroll
-    for (int t = 0; t < 2; t++) kv[r][t] = bsk[((size_t)(i * 6 + r) * 2 + j) * MP + 64 * (s0 + t) + lane];
+    for (int t = 0; t < 2; t++) kv[r][t] = bsk[((size_t)(i * 6 + r) * 2 + j) * M + 64 * (s0 + t) + lane];
 }
 
 // one CMUX of the latency kernel (phases A, B, C and their three barriers)
 __device__ __forceinline__ void lat_cmux(FftLatShared& sh, const u64* __restrict__ ct, int i, int wave, int lane,
-                                         const TwL& w, int j, int s0, const double2 (&kv)[6][2]) {
+                                         TBase tb, int j, int s0, const double2 (&kv)[6][2]) {
   const int a = i < FL_MAXN ? (int)sh.ab[i] : ms2048(ct[i]);
   if (wave < 6) {  // phase A
-    const int q = wave >> 1, c = wave & 1;
+    const int c = wave / 3, q = wave % 3;
     const u64* acc = sh.A[c];
     u32 st[16];
 #pragma unroll
@@ -415,50 +505,50 @@ __device__ __forceinline__ void lat_cmux(FftLatShared& sh, const u64* __restrict
 #pragma unroll
       for (int e = 0; e < 16; e++) dg[e] = decomp_step(st[e], bmask);
     }
-    double ar[8], ai[8], xr[16], xi[16];
+    double xr[8], xi[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) {
-      ar[e] = (double)dg[e];
-      ai[e] = (double)dg[e + 8];
+      xr[e] = (double)dg[e];
+      xi[e] = (double)dg[e + 8];
     }
-    fwd_single(ar, ai, xr, xi, sh.T[wave], TBaseP(lane, true), w);
-    if (lane < 32) {
+    twist_slots<false>(xr, xi);
+    dft512_fwd<true>(xr, xi, sh.T[wave], lane, tb, sh.tw);
 #pragma unroll
-      for (int m = 0; m < 16; m++) sh.F[wave][lane + 32 * m] = make_double2(xr[m], xi[m]);
-    }
+    for (int e = 0; e < 8; e++) sh.F[wave][64 * e + lane] = make_double2(xr[e], xi[e]);
   }
   __syncthreads();
   {  // phase B
     double2* O = sh.T[2 + j];
 #pragma unroll
     for (int t = 0; t < 2; t++) {
-      const int d = 64 * (s0 + t) + lane;
-      double re, im;
+      const int e = s0 + t;
+      double re[2], im[2];  // per-component chains (the first term a multiply), then one add (oracle order)
 #pragma unroll
       for (int r = 0; r < 6; r++) {
-        const double2 D = sh.F[r][d], K = kv[r][t];
-        if (r == 0) mac_first(re, im, D.x, D.y, K);
-        else mac_next(re, im, D.x, D.y, K);
+        const double2 D = sh.F[r][64 * e + lane], K = kv[r][t];
+        const int cc = r / 3;
+        if (r % 3 == 0) mac_first(re[cc], im[cc], D.x, D.y, K);
+        else mac_next(re[cc], im[cc], D.x, D.y, K);
       }
-      O[d] = make_double2(re, im);
+      O[64 * e + lane] = make_double2(re[0] + re[1], im[0] + im[1]);
     }
   }
   __syncthreads();
   if (wave < 2) {  // phase C
     const double2* O = sh.T[2 + wave];
-    double xr[16], xi[16], ar[8], ai[8];
+    double xr[8], xi[8];
 #pragma unroll
-    for (int m = 0; m < 16; m++) {
-      const double2 v = O[(lane & 31) + 32 * m];
-      xr[m] = v.x;
-      xi[m] = v.y;
+    for (int e = 0; e < 8; e++) {
+      const double2 v = O[64 * e + lane];
+      xr[e] = v.x;
+      xi[e] = v.y;
     }
-    inv_single(xr, xi, ar, ai, sh.T[wave], TBaseP(lane, true), w);
+    fft_inv_real(xr, xi, sh.T[wave], lane, tb, sh.tw);
     u64* acc = sh.A[wave];
 #pragma unroll
     for (int e = 0; e < 8; e++) {
-      acc[64 * e + lane] += f64_to_torus(ar[e]);
-      acc[64 * (e + 8) + lane] += f64_to_torus(ai[e]);
+      acc[64 * e + lane] += f64_to_torus(xr[e]);
+      acc[64 * (e + 8) + lane] += f64_to_torus(xi[e]);
     }
   }
   __syncthreads();
@@ -467,15 +557,15 @@ __device__ __forceinline__ void lat_cmux(FftLatShared& sh, const u64* __restrict
 template <bool WRITE_ACC, bool WRITE_BIG>
 __global__ __launch_bounds__(FL_THREADS, 1) void blind_rotate_fft_lat_kernel(
     const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
-    int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tab, u64* __restrict__ out_big,
+    int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tw_g, u64* __restrict__ out_big,
     u64* __restrict__ out_acc) {
   __shared__ __attribute__((aligned(16))) FftLatShared sh;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t b = blockIdx.x;
   const u64* ct = lwe_in + b * (size_t)(n + 1);
-  const TwL w(sh.tab, lane);
+  const TBase tb(lane);
 
-  for (int q = threadIdx.x; q < P_C64; q += FL_THREADS) sh.tab[q] = tab[q];
+  for (int q = threadIdx.x; q < TW_C64; q += FL_THREADS) sh.tw[q] = tw_g[q];
   for (int q = threadIdx.x; q < n && q < FL_MAXN; q += FL_THREADS) sh.ab[q] = (unsigned short)ms2048(ct[q]);
   {
     int li = lut_index ? (int)lut_index[b] : 0;
@@ -494,7 +584,7 @@ __global__ __launch_bounds__(FL_THREADS, 1) void blind_rotate_fft_lat_kernel(
   }
   __syncthreads();
 
-  const int j = wave >> 2, s0 = (wave & 3) * 2;  // phase B: output j, frequencies 64 (s0 + t) + lane
+  const int j = wave >> 2, s0 = (wave & 3) * 2;  // phase B: output j, slots s0, s0 + 1
 #if FFT_LAT_PREFETCH
   // key words one CMUX ahead (two register sets, the loop unrolled by two): a CMUX's row arrives while the
   // previous CMUX runs instead of behind this CMUX's phase A
@@ -502,16 +592,16 @@ __global__ __launch_bounds__(FL_THREADS, 1) void blind_rotate_fft_lat_kernel(
   lat_load_key(bsk, 0, j, s0, lane, kva);
   for (int i = 0; i < n; i += 2) {
     if (i + 1 < n) lat_load_key(bsk, i + 1, j, s0, lane, kvb);
-    lat_cmux(sh, ct, i, wave, lane, w, j, s0, kva);
+    lat_cmux(sh, ct, i, wave, lane, tb, j, s0, kva);
     if (i + 1 >= n) break;
     if (i + 2 < n) lat_load_key(bsk, i + 2, j, s0, lane, kva);
-    lat_cmux(sh, ct, i + 1, wave, lane, w, j, s0, kvb);
+    lat_cmux(sh, ct, i + 1, wave, lane, tb, j, s0, kvb);
   }
 #else
   for (int i = 0; i < n; i++) {
     double2 kv[6][2];  // phase-B key words of this CMUX, requested now, consumed after phase A
     lat_load_key(bsk, i, j, s0, lane, kv);
-    lat_cmux(sh, ct, i, wave, lane, w, j, s0, kv);
+    lat_cmux(sh, ct, i, wave, lane, tb, j, s0, kv);
   }
 #endif
 
@@ -535,9 +625,6 @@ __global__ void sample_extract_torus_kernel(const u64* __restrict__ acc, size_t 
   out[gid] = j == N1K ? A[N1K] : j == 0 ? A[0] : 0 - A[N1K - j];
 }
 
-}  // namespace fftp
-
-namespace fftk {
 // ---------------------------------------------------------------------------------------------
 // host: tables (fixed series in plain double, octant-reduced — the oracle's or_fft_twiddle)
 static double fs_sin(double x) {
@@ -586,21 +673,20 @@ static void twiddle(uint32_t t, uint32_t m, double* c, double* s) {
 
 void fft_twiddle(uint32_t t, uint32_t m, double* c, double* s) { fftk::twiddle(t, m, c, s); }
 
-size_t fft_tables_len() { return 2 * fftp::P_C64; }
+size_t fft_tables_len() { return 2 * fftk::TW_C64; }
 
-// N = 1024 tables (fft512p.h): ta[k][L] = zeta^(L (1 + 4 k)), zeta = e^(2 pi i / 2048) (the twist's lane part merged
-// into stage A), tb[m][l] = e^(2 pi i l m / 64) (the oracle's twAm and tb)
+// N = 1024 tables with the twist merged into the passes (fft512.h, "N = 1024 merged twist"):
+//   TW_A[e][L] = zeta^(L (1 + 4 e)),  TW_B as before,  TW_I[e][L] = zeta^((n0 + 8 e)(4 k0 + 1)) (L = n0 + 8 k0),
+// zeta = e^(2 pi i / 2048); TW_TWIST keeps zeta^j (the slot constants are its entries j = 64 e)
 void make_fft_tables(double* t) {
-  using namespace fftp;
-  for (uint32_t k = 0; k < 8; k++)
+  using namespace fftk;
+  for (uint32_t j = 0; j < (uint32_t)M; j++) twiddle(j, 4 * M, &t[2 * (TW_TWIST + j)], &t[2 * (TW_TWIST + j) + 1]);
+  for (uint32_t e = 0; e < 8; e++)
     for (uint32_t L = 0; L < 64; L++) {
-      const int o = P_TA + 64 * k + L;
-      fftk::twiddle((L * (1 + 4 * k)) % 2048, 2048, &t[2 * o], &t[2 * o + 1]);
-    }
-  for (uint32_t m = 0; m < 4; m++)
-    for (uint32_t l = 0; l < 16; l++) {
-      const int o = P_TB + 16 * m + l;
-      fftk::twiddle((64 * l * m) % 4096, 4096, &t[2 * o], &t[2 * o + 1]);
+      twiddle((L * (1 + 4 * e)) % (4 * M), 4 * M, &t[2 * (TW_A + 64 * e + L)], &t[2 * (TW_A + 64 * e + L) + 1]);
+      twiddle((8 * (L & 7) * e) % M, M, &t[2 * (TW_B + 64 * e + L)], &t[2 * (TW_B + 64 * e + L) + 1]);
+      twiddle((((L & 7) + 8 * e) * (4 * (L >> 3) + 1)) % (4 * M), 4 * M, &t[2 * (TW_I + 64 * e + L)],
+              &t[2 * (TW_I + 64 * e + L) + 1]);
     }
 }
 
@@ -616,7 +702,7 @@ bool fft_slot_constants_ok() {
 }
 
 hipError_t launch_bsk_to_fourier(const u64* bsk_std, double* bsk_f, size_t polys, const double* tw, hipStream_t s) {
-  hipLaunchKernelGGL(fftp::bsk_to_fourier_kernel, dim3((unsigned)polys), dim3(64), 0, s, bsk_std, (double2*)bsk_f,
+  hipLaunchKernelGGL(fftk::bsk_to_fourier_kernel, dim3((unsigned)polys), dim3(64), 0, s, bsk_std, (double2*)bsk_f,
                      (const double2*)tw);
   return hipGetLastError();
 }
@@ -624,7 +710,7 @@ hipError_t launch_bsk_to_fourier(const u64* bsk_std, double* bsk_f, size_t polys
 hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
                                    int n_lut, const double* bsk_f, const double* tw, u64* out_big, u64* out_acc,
                                    hipStream_t s, size_t latency_max_batch) {
-  using namespace fftp;
+  using namespace fftk;
   if (B == 0) return hipSuccess;
   const double2 *bk = (const double2*)bsk_f, *t = (const double2*)tw;
   if (B <= latency_max_batch) {
@@ -640,16 +726,16 @@ hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64
                          n_lut, bk, t, out_big, out_acc);
     return hipGetLastError();
   }
-  constexpr int CTS = FFT_CT_CTS;
-  dim3 grid((unsigned)((B + CTS - 1) / CTS)), block(64 * CTS);
+  constexpr int CTS = FFT_PAIR_CTS;
+  dim3 grid((unsigned)((B + CTS - 1) / CTS)), block(128 * CTS);
   if (out_acc && out_big)
-    hipLaunchKernelGGL((blind_rotate_fft_ct_kernel<CTS, true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
-                       n_lut, bk, t, out_big, out_acc);
+    hipLaunchKernelGGL((blind_rotate_fft_pair_kernel<CTS, true, true>), grid, block, 0, s, lwe_in, n, B, luts,
+                       lut_index, n_lut, bk, t, out_big, out_acc);
   else if (out_acc)
-    hipLaunchKernelGGL((blind_rotate_fft_ct_kernel<CTS, true, false>), grid, block, 0, s, lwe_in, n, B, luts,
+    hipLaunchKernelGGL((blind_rotate_fft_pair_kernel<CTS, true, false>), grid, block, 0, s, lwe_in, n, B, luts,
                        lut_index, n_lut, bk, t, out_big, out_acc);
   else
-    hipLaunchKernelGGL((blind_rotate_fft_ct_kernel<CTS, false, true>), grid, block, 0, s, lwe_in, n, B, luts,
+    hipLaunchKernelGGL((blind_rotate_fft_pair_kernel<CTS, false, true>), grid, block, 0, s, lwe_in, n, B, luts,
                        lut_index, n_lut, bk, t, out_big, out_acc);
   return hipGetLastError();
 }
@@ -657,21 +743,21 @@ hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64
 hipError_t launch_sample_extract_torus(const u64* acc, size_t B, u64* out, hipStream_t s) {
   if (B == 0) return hipSuccess;
   const size_t total = B * (N1K + 1);
-  hipLaunchKernelGGL(fftp::sample_extract_torus_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, acc, B,
+  hipLaunchKernelGGL(fftk::sample_extract_torus_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, acc, B,
                      out);
   return hipGetLastError();
 }
 
 hipError_t launch_fft_fwd(const u64* in, size_t count, double* out, const double* tw, hipStream_t s) {
   if (count == 0) return hipSuccess;
-  hipLaunchKernelGGL(fftp::fft_fwd_kernel, dim3((unsigned)count), dim3(64), 0, s, in, (double2*)out,
+  hipLaunchKernelGGL(fftk::fft_fwd_kernel, dim3((unsigned)count), dim3(64), 0, s, in, (double2*)out,
                      (const double2*)tw);
   return hipGetLastError();
 }
 
 hipError_t launch_fft_inv(const double* in, size_t count, double* out, const double* tw, hipStream_t s) {
   if (count == 0) return hipSuccess;
-  hipLaunchKernelGGL(fftp::fft_inv_kernel, dim3((unsigned)count), dim3(64), 0, s, (const double2*)in, out,
+  hipLaunchKernelGGL(fftk::fft_inv_kernel, dim3((unsigned)count), dim3(64), 0, s, (const double2*)in, out,
                      (const double2*)tw);
   return hipGetLastError();
 }
