@@ -106,6 +106,30 @@ int tfhe_hip_ms_zeros_keygen_k(const tfhe_params* p, const tfhe_rng_key* rk, con
                                uint64_t* zeros);
 int tfhe_hip_ms_zeros_keygen(const tfhe_params* p, uint64_t seed, const uint64_t* lwe_key, uint32_t count,
                              uint64_t* zeros);
+/* ---- compressed (seeded) server keys, SURVEY §8f f3 ---------------------------------------------
+ * Replaces tfhe-rs core_crypto decompress_seeded_lwe_bootstrap_key / decompress_seeded_lwe_keyswitch_key /
+ * decompress_seeded_lwe_ciphertext_list behind CompressedServerKey::decompress, the step by which the fhEVM
+ * coprocessor turns a tenant's stored key into evaluation keys (tests/fhevm-suite/fhevm/docker-compose/
+ * coprocessor-docker-compose.yml:96, --tenant-key-cache-size).  Masks come from the AES-128-CTR stream of a
+ * 128-bit seed (seed[0] = low 64 bits) restated from tfhe-csprng (tfhe_amd/csrc/seeded.cpp has the byte order);
+ * bodies are in tfhe-rs order:
+ *   BSK bodies [i < n][l < L][c <= k][N]   (GGSW i, decomposition level l most significant first, GLWE row c)
+ *   KSK bodies [j < k N][l < ks_level]     (input key element j; P-FHEVM: big key -> small key)
+ *   list bodies [z < count]                (e.g. the modulus-switch zeros)
+ * Decompressed keys land in this engine's standard layouts (tfhe_hip_load_keys, tfhe_hip_load_ms_key).  FFT64
+ * presets only (native 2^64 torus).  PARITY UNPINNED at the byte level: the reference holds no server-key file. */
+int tfhe_hip_aes128_block(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]); /* FIPS-197 check */
+int tfhe_hip_csprng_words(const uint64_t seed[2], uint64_t first_word, size_t count, uint64_t* out);
+int tfhe_hip_seeded_server_keygen_k(const tfhe_params* p, const tfhe_rng_key* rk, const uint64_t bsk_seed[2],
+                                    const uint64_t ksk_seed[2], const uint64_t* lwe_key, const uint64_t* glwe_key,
+                                    uint64_t* bsk_bodies /* nullable */, uint64_t* ksk_bodies /* nullable */);
+int tfhe_hip_seeded_lwe_list_k(uint32_t dim, uint32_t count, const uint64_t* key, int32_t noise_log2,
+                               const tfhe_rng_key* rk, uint64_t stream0, const uint64_t seed[2],
+                               const uint64_t* msgs /* nullable: encryptions of zero */, uint64_t* bodies);
+int tfhe_hip_decompress_bsk(const tfhe_params* p, const uint64_t seed[2], const uint64_t* bodies, uint64_t* bsk);
+int tfhe_hip_decompress_ksk(const tfhe_params* p, const uint64_t seed[2], const uint64_t* bodies, uint64_t* ksk);
+int tfhe_hip_decompress_lwe_list(uint32_t dim, uint32_t count, const uint64_t seed[2], const uint64_t* bodies,
+                                 uint64_t* out /* count x (dim + 1) */);
 /* Encrypt count torus messages; ciphertext q uses ChaCha stream (stream0 + q) of the rng key (a fresh
  * entropy key per call, or one key with non-overlapping stream ranges).
  * Replaces the encrypt path of packages/luxfhejs/src/index.ts:127-141 (server-side /encrypt). */

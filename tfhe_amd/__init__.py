@@ -111,7 +111,9 @@ ABI_SYMBOLS = (
     "tfhe_hip_sns_squash_async", "tfhe_hip_sns_blind_rotate", "tfhe_hip_sns_phase", "tfhe_hip_fft_fwd",
     "tfhe_hip_fft_inv", "tfhe_hip_rng_key_entropy", "tfhe_hip_rng_key_from_seed", "tfhe_hip_keygen_k",
     "tfhe_hip_server_keygen_k", "tfhe_hip_ms_zeros_keygen_k", "tfhe_hip_lwe_encrypt_k", "tfhe_hip_ndev",
-    "tfhe_hip_device_at", "tfhe_hip_key_bcast_mode", "tfhe_hip_br_kernel",
+    "tfhe_hip_device_at", "tfhe_hip_key_bcast_mode", "tfhe_hip_br_kernel", "tfhe_hip_aes128_block",
+    "tfhe_hip_csprng_words", "tfhe_hip_seeded_server_keygen_k", "tfhe_hip_seeded_lwe_list_k", "tfhe_hip_decompress_bsk",
+    "tfhe_hip_decompress_ksk", "tfhe_hip_decompress_lwe_list",
 )
 
 # P-FHEVM modulus-switch noise reduction key (include/tfhe_hip.h TFHE_HIP_MS_FHEVM_*)
@@ -169,6 +171,14 @@ def lib():
         L.tfhe_hip_keygen_k.argtypes = [ctypes.c_void_p, _RKP, _U64P, _U64P, _U64P, _U64P]
         L.tfhe_hip_server_keygen_k.argtypes = [ctypes.c_void_p, _RKP, _U64P, _U64P, _U64P, _U64P]
         L.tfhe_hip_ms_zeros_keygen_k.argtypes = [ctypes.c_void_p, _RKP, _U64P, ctypes.c_uint32, _U64P]
+        L.tfhe_hip_aes128_block.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p]
+        L.tfhe_hip_csprng_words.argtypes = [_U64P, ctypes.c_uint64, ctypes.c_size_t, _U64P]
+        L.tfhe_hip_seeded_server_keygen_k.argtypes = [ctypes.c_void_p, _RKP, _U64P, _U64P, _U64P, _U64P, _U64P, _U64P]
+        L.tfhe_hip_seeded_lwe_list_k.argtypes = [ctypes.c_uint32, ctypes.c_uint32, _U64P, ctypes.c_int32, _RKP,
+                                                 ctypes.c_uint64, _U64P, _U64P, _U64P]
+        L.tfhe_hip_decompress_bsk.argtypes = [ctypes.c_void_p, _U64P, _U64P, _U64P]
+        L.tfhe_hip_decompress_ksk.argtypes = [ctypes.c_void_p, _U64P, _U64P, _U64P]
+        L.tfhe_hip_decompress_lwe_list.argtypes = [ctypes.c_uint32, ctypes.c_uint32, _U64P, _U64P, _U64P]
         L.tfhe_hip_lwe_encrypt_k.argtypes = [ctypes.c_uint32, _U64P, ctypes.c_int32, _RKP, ctypes.c_uint64, _U64P,
                                              ctypes.c_size_t, _U64P]
         L.tfhe_hip_destroy.argtypes = [ctypes.c_void_p]

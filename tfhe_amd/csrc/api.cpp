@@ -662,6 +662,62 @@ int tfhe_hip_ms_zeros_keygen_k(const tfhe_params* p, const tfhe_rng_key* rk, con
   return 0;
 }
 
+// ---- compressed (seeded) server keys (seeded.cpp)
+static bool native_torus(const tfhe_params* p) { return params_valid(p) && p->transform == TFHE_HIP_TRANSFORM_FFT64; }
+
+int tfhe_hip_aes128_block(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]) {
+  if (!key || !in || !out) return fail(TFHE_HIP_EINVAL, "aes128_block: null argument");
+  tfhe::seeded::aes128_block(key, in, out);
+  return 0;
+}
+
+int tfhe_hip_csprng_words(const uint64_t seed[2], uint64_t first_word, size_t count, uint64_t* out) {
+  if (!seed || (count && !out)) return fail(TFHE_HIP_EINVAL, "csprng_words: null argument");
+  tfhe::seeded::csprng_words(seed, first_word, count, out);
+  return 0;
+}
+
+int tfhe_hip_seeded_server_keygen_k(const tfhe_params* p, const tfhe_rng_key* rk, const uint64_t bsk_seed[2],
+                                    const uint64_t ksk_seed[2], const uint64_t* lwe_key, const uint64_t* glwe_key,
+                                    uint64_t* bsk_bodies, uint64_t* ksk_bodies) {
+  if (!native_torus(p) || !rk || !lwe_key || !glwe_key || (bsk_bodies && !bsk_seed) || (ksk_bodies && !ksk_seed))
+    return fail(TFHE_HIP_EINVAL, "seeded_server_keygen: bad arguments (FFT64 presets only)");
+  RC_TRY(check_binary(lwe_key, p->n, "seeded_server_keygen: lwe_key"));
+  RC_TRY(check_binary(glwe_key, (size_t)p->k * p->N, "seeded_server_keygen: glwe_key"));
+  tfhe::seeded::seeded_server_keygen(*p, *rk, bsk_seed, ksk_seed, lwe_key, glwe_key, bsk_bodies, ksk_bodies);
+  return 0;
+}
+
+int tfhe_hip_seeded_lwe_list_k(uint32_t dim, uint32_t count, const uint64_t* key, int32_t noise_log2,
+                               const tfhe_rng_key* rk, uint64_t stream0, const uint64_t seed[2], const uint64_t* msgs,
+                               uint64_t* bodies) {
+  if (!dim || !key || !rk || !seed || (count && !bodies)) return fail(TFHE_HIP_EINVAL, "seeded_lwe_list: bad arguments");
+  RC_TRY(check_binary(key, dim, "seeded_lwe_list: key"));
+  tfhe::seeded::seeded_lwe_list(dim, count, key, noise_log2, *rk, stream0, seed, msgs, bodies);
+  return 0;
+}
+
+int tfhe_hip_decompress_bsk(const tfhe_params* p, const uint64_t seed[2], const uint64_t* bodies, uint64_t* bsk) {
+  if (!native_torus(p) || !seed || !bodies || !bsk)
+    return fail(TFHE_HIP_EINVAL, "decompress_bsk: bad arguments (FFT64 presets only)");
+  tfhe::seeded::decompress_bsk(*p, seed, bodies, bsk);
+  return 0;
+}
+
+int tfhe_hip_decompress_ksk(const tfhe_params* p, const uint64_t seed[2], const uint64_t* bodies, uint64_t* ksk) {
+  if (!native_torus(p) || !seed || !bodies || !ksk)
+    return fail(TFHE_HIP_EINVAL, "decompress_ksk: bad arguments (FFT64 presets only)");
+  tfhe::seeded::decompress_ksk(*p, seed, bodies, ksk);
+  return 0;
+}
+
+int tfhe_hip_decompress_lwe_list(uint32_t dim, uint32_t count, const uint64_t seed[2], const uint64_t* bodies,
+                                 uint64_t* out) {
+  if (!dim || !seed || (count && (!bodies || !out))) return fail(TFHE_HIP_EINVAL, "decompress_lwe_list: bad arguments");
+  tfhe::seeded::decompress_lwe_list(dim, count, seed, bodies, out);
+  return 0;
+}
+
 int tfhe_hip_ms_zeros_keygen(const tfhe_params* p, uint64_t seed, const uint64_t* lwe_key, uint32_t count,
                              uint64_t* zeros) {
   const tfhe_rng_key rk = tfhe::client::rng_key_from_seed(seed);

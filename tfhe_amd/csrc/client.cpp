@@ -249,6 +249,12 @@ void ms_zeros_keygen(const tfhe_params& p, const tfhe_rng_key& rk, const uint64_
   });
 }
 
+// count Gaussian noise words of ChaCha stream `stream` (the seeded keys' noise, seeded.cpp)
+void noise_words(const tfhe_rng_key& rk, uint64_t stream, int32_t log2_sigma, size_t count, int64_t* out) {
+  ChaCha r(rk, stream);
+  for (size_t i = 0; i < count; i++) out[i] = r.gauss(log2_sigma);
+}
+
 void lwe_encrypt(uint32_t dim, const uint64_t* key, int32_t noise_log2, const tfhe_rng_key& rk, uint64_t stream0,
                  const uint64_t* msgs, size_t count, uint64_t* out) {
   auto one = [&](int64_t q) {

@@ -18,8 +18,14 @@
 namespace tfhe {
 namespace {
 
-constexpr int MS_CT = 8;     // ciphertexts per workgroup
-constexpr int MS_ZT = 32;    // zeros per scan step
+#ifndef MS_CT_N
+#define MS_CT_N 8
+#endif
+#ifndef MS_ZT_N
+#define MS_ZT_N 32
+#endif
+constexpr int MS_CT = MS_CT_N;  // ciphertexts per workgroup
+constexpr int MS_ZT = MS_ZT_N;  // zeros per scan step
 constexpr int MS_IC = 128;   // elements per LDS chunk
 constexpr int MS_THREADS = MS_CT * MS_ZT;
 
@@ -60,9 +66,9 @@ __global__ void __launch_bounds__(MS_THREADS) ms_reduce_kernel(u64* __restrict__
   const int b0 = blockIdx.x * MS_CT;
   const size_t dim = (size_t)n + 1;
 
-  // measure of each ciphertext alone: wave w takes ciphertexts 2w, 2w+1
-  for (int cc = 0; cc < 2; cc++) {
-    const int c = 2 * wave + cc, b = b0 + c;
+  // measure of each ciphertext alone: wave w takes ciphertexts w, w + (waves), ...
+  for (int c = wave; c < MS_CT; c += MS_THREADS / 64) {
+    const int b = b0 + c;
     i64 s1 = 0;
     u128 s2 = 0;
     if (b < B) {
