@@ -64,6 +64,30 @@ def test_c5_auction_max_tree_256(request, transform):
     print(f"C5 {transform}: {time.time() - t0:.2f} s, {c.pbs_count} PBS in {c.launches} launches")
 
 
+def test_c5_device_resident_equals_host(gate_fft_engine, gate_fft_keys):
+    """C5 on the device-resident circuit (Circuit(device=...): int64 tensors on the GPU, every level one
+    pbs_async on torch's stream): the same winner, the same launches and PBS count, and every output bit of the
+    max equal to the host-array circuit's (same keys, same encryptions, deterministic kernels)."""
+    import torch
+    ck, _ = gate_fft_keys
+    v = np.random.default_rng(6).integers(0, 2**32, 256, dtype=np.uint64)
+    out = []
+    for dev in (None, "cuda:0"):
+        c = I.Circuit(gate_fft_engine, device=dev)
+        bids = I.FheUint.encrypt(c, ck, v, 32, seed=0xB1E, stream0=0)
+        t0 = time.time()
+        mx, idx = max_tree(c, bids)
+        if dev:
+            torch.cuda.synchronize()
+        wall = time.time() - t0
+        bits = mx.bits.cpu().numpy().view(np.uint64) if dev else mx.bits
+        out.append((bits, c.launches, c.pbs_count, int(mx.decrypt(ck)[0]), int(idx.decrypt(ck)[0])))
+        print(f"C5 fft64 {'device' if dev else 'host'}: {wall:.3f} s")
+    assert out[0][3:] == out[1][3:] == (int(v.max()), int(np.argmax(v)))
+    assert out[0][1:3] == out[1][1:3]
+    assert np.array_equal(out[0][0], out[1][0])
+
+
 @pytest.mark.parametrize("transform", ["ntt", "fft64"])
 def test_c2_batch_1024(request, transform, oracle_mod):
     """C2: batch = 1024 independent P-GATE PBS on one GPU (the exact config size: the FFT64 engine runs

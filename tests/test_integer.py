@@ -202,3 +202,37 @@ def test_operator_errors():
         c.run(I.fhevm_op(c, "add", 1, 2))
     with pytest.raises(ValueError):
         c.run(I.fhevm_op(c, "div", A, A))
+
+
+# ---- the device-resident circuit (Circuit(device=...)): the same circuits on torch int64 tensors ---------------
+class CleartextTorchEngine(CleartextEngine):
+    """pbs_device of the cleartext double on torch CPU tensors (the device path's array code on CPU)."""
+
+    def pbs_device(self, d_in, d_lut):
+        import torch
+        out = self.pbs(d_in.numpy().view(np.uint64), d_lut)
+        return torch.from_numpy(out.view(np.int64))
+
+
+def test_device_resident_circuit_matches_host(kats):
+    """Every operator of a KAT sample and the C5 max tree give the same bits on torch tensors as on numpy
+    arrays, through the same number of launches."""
+    import torch
+    for kat in kats[::25]:
+        res = []
+        for dev in (None, "cpu"):
+            c = I.Circuit(CleartextTorchEngine(), device=dev)
+            out = c.run(build_kat_op(c, kat))
+            bits = out.bits if isinstance(out, I.FheUint) else out
+            if isinstance(bits, torch.Tensor):
+                bits = bits.numpy().view(np.uint64)
+            res.append((bits.copy(), c.launches, c.pbs_count))
+        assert np.array_equal(res[0][0], res[1][0]) and res[0][1:] == res[1][1:], kat
+        assert check_result(ClearKey(), kat, I.FheUint(None, res[1][0]) if res[1][0].ndim == 3 else res[1][0])
+    from tfhe_amd.auction import max_tree
+    v = np.random.default_rng(11).integers(0, 2**32, 100, dtype=np.uint64)
+    c = I.Circuit(CleartextTorchEngine(), device="cpu")
+    mx, idx = max_tree(c, I.FheUint.trivial(c, v, 32))
+    ck = ClearKey()
+    assert isinstance(mx.bits, torch.Tensor)
+    assert (int(mx.decrypt(ck)[0]), int(idx.decrypt(ck)[0])) == (int(v.max()), int(np.argmax(v)))

@@ -518,6 +518,14 @@ class Engine:
                                         ctypes.c_void_p(d_lut_index.data_ptr()) if d_lut_index is not None else None,
                                         ctypes.c_void_p(d_out.data_ptr()), ctypes.c_void_p(stream)))
 
+    def pbs_device(self, d_in, d_luts, d_lut_index=None):
+        """pbs_async into a fresh tensor: (B, dim+1) int64 on this device -> the same shape, queued on torch's
+        current stream (no host synchronisation)."""
+        d_out = d_in.new_empty(d_in.shape)
+        if d_in.shape[0]:
+            self.pbs_async(d_in.contiguous(), d_luts, d_out, d_lut_index)
+        return d_out
+
     def blind_rotate(self, cts: np.ndarray, luts: np.ndarray, lut_index=None) -> np.ndarray:
         p = self.params
         cts = _c_u64(cts).reshape(-1, p.n + 1)

@@ -21,7 +21,7 @@ from typing import List, Tuple
 
 import numpy as np
 
-from .integer import NOT, Circuit, FheUint, g_ge, g_select
+from .integer import NOT, Circuit, FheUint, _cat, _contig, _is_t, _stack, _where, g_ge, g_select
 
 # an index bit column over the current candidates: ("pub", bool values (m,)) or ("enc", ciphertexts (m, dim))
 Col = Tuple[str, np.ndarray]
@@ -32,13 +32,13 @@ def _level_op(c: Circuit, lhs: np.ndarray, rhs: np.ndarray, w: int):
     selected columns, then the condition ge = lhs >= rhs."""
     ge = yield from g_ge(c, lhs[:, :w], rhs[:, :w])
     sel = yield from g_select(ge, lhs, rhs)
-    return np.concatenate([sel, ge[:, None]], axis=1)
+    return _cat([sel, ge[:, None]], axis=1)
 
 
 def _run_level(c: Circuit, pairs: np.ndarray, w: int) -> np.ndarray:
     if pairs.shape[0] == 0:
-        return np.zeros((0, pairs.shape[2] + 1, pairs.shape[3]), dtype=np.uint64)
-    return c.run(_level_op(c, np.ascontiguousarray(pairs[:, 0]), np.ascontiguousarray(pairs[:, 1]), w))
+        return c.trivial(np.zeros((0, pairs.shape[2] + 1), dtype=bool))
+    return c.run(_level_op(c, _contig(pairs[:, 0]), _contig(pairs[:, 1]), w))
 
 
 def _index_level(c: Circuit, cols: List[Col], enc_sel: np.ndarray, ge: np.ndarray, P: int) -> List[Col]:
@@ -48,7 +48,7 @@ def _index_level(c: Circuit, cols: List[Col], enc_sel: np.ndarray, ge: np.ndarra
     out, e = [], 0
     for kind, v in cols:
         if kind == "enc":
-            out.append(("enc", np.concatenate([enc_sel[:, e], v[2 * P:]], axis=0)))
+            out.append(("enc", _cat([enc_sel[:, e], v[2 * P:]], axis=0)))
             e += 1
             continue
         vl, vr = v[0:2 * P:2], v[1:2 * P:2]
@@ -56,8 +56,8 @@ def _index_level(c: Circuit, cols: List[Col], enc_sel: np.ndarray, ge: np.ndarra
             out.append(("pub", np.concatenate([vl, v[2 * P:]])))
             continue
         triv = c.trivial(vl)
-        col = np.where((vl & ~vr)[:, None], ge, np.where((~vl & vr)[:, None], NOT(ge), triv))
-        out.append(("enc", np.concatenate([col, c.trivial(v[2 * P:])], axis=0)))
+        col = _where((vl & ~vr)[:, None], ge, _where((~vl & vr)[:, None], NOT(ge), triv))
+        out.append(("enc", _cat([col, c.trivial(v[2 * P:])], axis=0)))
     return out
 
 
@@ -72,9 +72,9 @@ def max_tree(c: Circuit, bids: FheUint, group=None):
         m = cur.shape[0]
         P = m // 2
         enc = [v for kind, v in cols if kind == "enc"]
-        full = np.concatenate([cur] + [v[:, None] for v in enc], axis=1) if enc else cur   # (m, w + k, dim)
+        full = _cat([cur] + [v[:, None] for v in enc], axis=1) if enc else cur   # (m, w + k, dim)
         pairs = full[: 2 * P].reshape(P, 2, full.shape[1], dim)
-        if group is None:
+        if group is None or _is_t(pairs):
             res = _run_level(c, pairs, w)
         else:
             import torch
@@ -86,6 +86,6 @@ def max_tree(c: Circuit, bids: FheUint, group=None):
             res = res_t.numpy().view(np.uint64).reshape(P, full.shape[1] + 1, dim)
         win, ge = res[:, :-1], res[:, -1]
         cols = _index_level(c, cols, win[:, w:], ge, P)
-        cur = np.concatenate([win[:, :w], cur[2 * P:]], axis=0)                          # odd leftover advances
-    idx = np.stack([v[0] if kind == "enc" else c.trivial(v[:1])[0] for kind, v in cols], axis=0)[None]
+        cur = _cat([win[:, :w], cur[2 * P:]], axis=0)                          # odd leftover advances
+    idx = _stack([v[0] if kind == "enc" else c.trivial(v[:1])[0] for kind, v in cols], axis=0)[None]
     return FheUint(c, cur[:, :w]), FheUint(c, idx)

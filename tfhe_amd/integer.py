@@ -40,11 +40,71 @@ WIDTHS = (8, 16, 32, 64, 128, 160, 256)   # ebool / euint* / eaddress of fhEVM (
 
 
 # --------------------------------------------------------------------------------------------
+# arrays: host numpy uint64, or (a device-resident Circuit) torch int64 tensors holding the same bits
+# --------------------------------------------------------------------------------------------
+def _is_t(a) -> bool:
+    return type(a).__module__.startswith("torch")
+
+
+def _cat(seq, axis: int = 0):
+    seq = list(seq)
+    if seq and _is_t(seq[0]):
+        import torch
+        return torch.cat(seq, dim=axis)
+    return np.concatenate(seq, axis=axis)
+
+
+def _stack(seq, axis: int = 0):
+    seq = list(seq)
+    if seq and _is_t(seq[0]):
+        import torch
+        return torch.stack(seq, dim=axis)
+    return np.stack(seq, axis=axis)
+
+
+def _bcast(a, shape):
+    return a.expand(*shape) if _is_t(a) else np.broadcast_to(a, shape)
+
+
+def _roll(a, k: int, axis: int):
+    if _is_t(a):
+        import torch
+        return torch.roll(a, k, dims=axis)
+    return np.roll(a, k, axis=axis)
+
+
+def _where(mask: np.ndarray, x, y):
+    """mask: host bools broadcasting against x / y."""
+    if _is_t(x):
+        import torch
+        return torch.where(torch.as_tensor(np.ascontiguousarray(mask), device=x.device), x, y)
+    return np.where(mask, x, y)
+
+
+def _contig(a):
+    return a.contiguous() if _is_t(a) else np.ascontiguousarray(a)
+
+
+def _i64(v: int) -> int:
+    v %= _M64
+    return v - _M64 if v >= 1 << 63 else v
+
+
+# --------------------------------------------------------------------------------------------
 # linear combinations (all arithmetic mod 2^64, vectorised over any leading shape)
 # --------------------------------------------------------------------------------------------
-def _lin(terms, const: int = 0) -> np.ndarray:
+def _lin(terms, const: int = 0):
     """sum w * c + const on the body, mod 2^64, in one fresh array (weights +-1 as in-place adds / subtracts: the
-    circuits' levels are tens of MB, so the host time between launches is these passes)."""
+    circuits' levels are tens of MB, so the host time between launches is these passes).  Device tensors: the
+    same on int64 (two's-complement wrap-around = arithmetic mod 2^64)."""
+    if _is_t(terms[0][1]):
+        out = None
+        for w, c in terms:
+            w = _i64(w)
+            t = c if w == 1 else -c if w == -1 else c * w
+            out = (t.clone() if w == 1 else t) if out is None else out.add_(t)
+        out[..., -1] += _i64(const)
+        return out
     with np.errstate(over="ignore"):
         out = None
         for w, c in terms:
@@ -83,6 +143,8 @@ def XOR3(a, b, c):
 
 
 def NOT(a):
+    if _is_t(a):
+        return -a
     with np.errstate(over="ignore"):
         return np.subtract(np.uint64(0), a, dtype=np.uint64)
 
@@ -97,10 +159,17 @@ Op = Generator[Level, List[np.ndarray], object]
 class Circuit:
     """Runs operator coroutines on an Engine: every yielded level is one batched PBS launch."""
 
-    def __init__(self, engine: Engine, capacity: int = 2048, round_size: Optional[int] = None):
+    def __init__(self, engine: Engine, capacity: int = 2048, round_size: Optional[int] = None, device=None):
         self.engine = engine
         self.dim = engine.params.n + 1
         self.lut = engine.gate_lut()
+        # device-resident circuit (a torch device, e.g. "cuda:0"): ciphertexts are int64 tensors on it, every
+        # level is one Engine.pbs_device launch on torch's current stream and the linear combinations are torch
+        # ops queued behind it -- no host round trip per level (the host only walks the circuit's structure)
+        self.device = device
+        if device is not None:
+            import torch
+            self._lut_d = None if self.lut is None else torch.from_numpy(self.lut.view(np.int64).copy()).to(device)
         self.capacity = capacity      # PBS one launch completes in ~one PBS latency (8 x 256 CUs)
         # PBS per round of the engine's batch kernel (Engine.round_size: the FFT64 pair kernel holds 4
         # ciphertexts x 256 CUs per GPU); a launch of n PBS costs ~max(1, ceil(n / round_size)) rounds -- the
@@ -114,10 +183,19 @@ class Circuit:
         bits = np.asarray(bits, dtype=bool)
         out = np.zeros(bits.shape + (self.dim,), dtype=np.uint64)
         out[..., -1] = np.where(bits, np.uint64(MU), np.uint64(_M64 - MU))
-        return out
+        return out if self.device is None else self.to_device(out)
+
+    def to_device(self, a):
+        """Host uint64 array -> this circuit's arrays (a device tensor in device mode)."""
+        if self.device is None or _is_t(a):
+            return a
+        import torch
+        return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)).to(self.device)
 
     def bootstrap(self, lins: Sequence[np.ndarray]) -> List[np.ndarray]:
-        shapes = [l.shape[:-1] for l in lins]
+        shapes = [tuple(l.shape[:-1]) for l in lins]
+        if self.device is not None:
+            return self._bootstrap_device(lins, shapes)
         flat = np.concatenate([l.reshape(-1, self.dim) for l in lins], axis=0) if lins else \
             np.zeros((0, self.dim), np.uint64)
         if flat.shape[0]:
@@ -132,6 +210,25 @@ class Circuit:
         for s in shapes:
             cnt = int(np.prod(s, dtype=np.int64))
             res.append(out[off:off + cnt].reshape(s + (self.dim,)))
+            off += cnt
+        return res
+
+    def _bootstrap_device(self, lins, shapes):
+        import torch
+        flat = torch.cat([l.reshape(-1, self.dim) for l in lins], dim=0) if lins else \
+            torch.zeros((0, self.dim), dtype=torch.int64, device=self.device)
+        if flat.shape[0]:
+            outs = [self.engine.pbs_device(flat[o:o + MAX_LAUNCH], self._lut_d)
+                    for o in range(0, flat.shape[0], MAX_LAUNCH)]
+            out = outs[0] if len(outs) == 1 else torch.cat(outs, dim=0)
+            self.pbs_count += flat.shape[0]
+            self.launches += 1
+        else:
+            out = flat
+        res, off = [], 0
+        for sh in shapes:
+            cnt = int(np.prod(sh, dtype=np.int64))
+            res.append(out[off:off + cnt].reshape(sh + (self.dim,)))
             off += cnt
         return res
 
@@ -221,18 +318,18 @@ def g_add(c: Circuit, a: np.ndarray, b: np.ndarray, cin: bool = False, want_sum:
                 sums.append(out[-1])
             if need_carry:
                 carry = out[0]
-        return (np.stack(sums, axis=1) if want_sum else None), (carry if want_carry else None)
+        return (_stack(sums, axis=1) if want_sum else None), (carry if want_carry else None)
     # Kogge-Stone: inclusive prefixes (G, P)[0..i]
     G, P = yield [AND(a, b), OR(a, b)]
     d = 1
     while d < w:
         hi_G, hi_P = G[:, d:], P[:, d:]
         nG, nP = yield [MAJ(hi_G, hi_P, G[:, :-d]), MAJ(hi_G, hi_P, P[:, :-d])]
-        G = np.concatenate([G[:, :d], nG], axis=1)
-        P = np.concatenate([P[:, :d], nP], axis=1)
+        G = _cat([G[:, :d], nG], axis=1)
+        P = _cat([P[:, :d], nP], axis=1)
         d *= 2
     pref = P if cin else G
-    carries = np.concatenate([c.trivial(np.full((B, 1), cin, dtype=bool)), pref[:, :w - 1]], axis=1)
+    carries = _cat([c.trivial(np.full((B, 1), cin, dtype=bool)), pref[:, :w - 1]], axis=1)
     (s,) = yield [XOR3(a, b, carries)]
     return s, (pref[:, w - 1] if want_carry else None)
 
@@ -276,8 +373,8 @@ def _carry_out(c: Circuit, a: np.ndarray, b: np.ndarray, cin: bool, s: int) -> O
             if j == 0:
                 G, P = out[1], out[2]
             else:
-                G = np.concatenate([out[1], G[:, len(ks):]], axis=1)
-                P = np.concatenate([out[2], P[:, len(ks):]], axis=1)
+                G = _cat([out[1], G[:, len(ks):]], axis=1)
+                P = _cat([out[2], P[:, len(ks):]], axis=1)
     while G is not None and G.shape[1] > 0:
         # states: C (block 0), then (G, P) of blocks 1 .. n-1; merge (0, 1) and (2i, 2i+1)
         n = G.shape[1] + 1
@@ -294,8 +391,8 @@ def _carry_out(c: Circuit, a: np.ndarray, b: np.ndarray, cin: bool, s: int) -> O
         if n % 2:                                  # an odd block at the top passes through
             nG.append(G[:, n - 2:n - 1])
             nP.append(P[:, n - 2:n - 1])
-        G = np.concatenate(nG, axis=1) if nG else None
-        P = np.concatenate(nP, axis=1) if nP else None
+        G = _cat(nG, axis=1) if nG else None
+        P = _cat(nP, axis=1) if nP else None
     return C
 
 
@@ -315,7 +412,7 @@ def g_eq(c: Circuit, a, b) -> Op:
     B = a.shape[0]
     while cur.shape[1] > 1:
         if cur.shape[1] % 2:
-            cur = np.concatenate([cur, NOT(_zeros(c, B, 1))], axis=1)
+            cur = _cat([cur, NOT(_zeros(c, B, 1))], axis=1)
         (cur,) = yield [AND(cur[:, 0::2], cur[:, 1::2])]
     return cur[:, 0]
 
@@ -325,7 +422,7 @@ def g_select(cond: np.ndarray, x: np.ndarray, y: np.ndarray) -> Op:
     them is true, OR(t, f) = t + f + 1/8 holds exactly on the phases (-1/8 - 1/8 + 1/8 = -1/8, 1/8 - 1/8 + 1/8
     = 1/8): the OR needs no bootstrap.  The result carries the noise of two PBS outputs, still far inside
     the 1/8 decision margin of any gate it feeds."""
-    cw = np.broadcast_to(cond[:, None, :], x.shape)
+    cw = _bcast(cond[:, None, :], x.shape)
     t, f = yield [AND(cw, x), _lin([(-1, cw), (1, y)], -MU)]      # AND(cw, x), AND(NOT cw, y)
     return OR(t, f)
 
@@ -339,11 +436,11 @@ def g_mul(c: Circuit, a: np.ndarray, b: Union[np.ndarray, int], prefix=None) -> 
         k = int(b) % (1 << w)
         for j in range(w):
             if (k >> j) & 1:
-                rows.append(np.concatenate([_zeros(c, B, j), a[:, :w - j]], axis=1))
+                rows.append(_cat([_zeros(c, B, j), a[:, :w - j]], axis=1))
     else:
-        lvl = [AND(a[:, :w - j], np.broadcast_to(b[:, j:j + 1], (B, w - j, c.dim))) for j in range(w)]
+        lvl = [AND(a[:, :w - j], _bcast(b[:, j:j + 1], (B, w - j, c.dim))) for j in range(w)]
         pp = yield lvl
-        rows = [np.concatenate([_zeros(c, B, j), pp[j]], axis=1) for j in range(w)]
+        rows = [_cat([_zeros(c, B, j), pp[j]], axis=1) for j in range(w)]
     if not rows:
         return _zeros(c, B, w)
     while len(rows) > 2:
@@ -356,7 +453,7 @@ def g_mul(c: Circuit, a: np.ndarray, b: Union[np.ndarray, int], prefix=None) -> 
         nrows = []
         for t in range(ntrip):
             nrows.append(out[2 * t])
-            nrows.append(np.concatenate([_zeros(c, B, 1), out[2 * t + 1]], axis=1))
+            nrows.append(_cat([_zeros(c, B, 1), out[2 * t + 1]], axis=1))
         rows = nrows + rows[3 * ntrip:]
     if len(rows) == 1:
         return rows[0]
@@ -374,16 +471,16 @@ def g_div_rem_scalar(c: Circuit, a: np.ndarray, d: int) -> Op:
     q = _zeros(c, B, w)
     # after shifting in the top k bits, R = a[w-k:] ; while k < L, R < d so q bits are 0
     k0 = L - 1
-    R = a[:, w - k0:] if k0 > 0 else np.zeros((B, 0, c.dim), np.uint64)   # R has k0 bits
+    R = a[:, w - k0:] if k0 > 0 else _zeros(c, B, 0)   # R has k0 bits
     for i in range(w - L, -1, -1):
-        R = np.concatenate([a[:, i:i + 1], R], axis=1)         # (R << 1) | a_i  : L..w bits
+        R = _cat([a[:, i:i + 1], R], axis=1)         # (R << 1) | a_i  : L..w bits
         r = R.shape[1]
         dbits = c.trivial(np.broadcast_to(np.array([(d >> j) & 1 for j in range(r)], dtype=bool), (B, r)))
         t, ge = yield from g_add(c, R, NOT(dbits), True, want_sum=True, want_carry=True)
         q[:, i] = ge
         R = yield from g_select(ge, t, R)
         R = R[:, :max(L, 1)] if r > L else R                   # R < d < 2^L after the step
-    rem = np.concatenate([R, _zeros(c, B, w - R.shape[1])], axis=1) if R.shape[1] < w else R[:, :w]
+    rem = _cat([R, _zeros(c, B, w - R.shape[1])], axis=1) if R.shape[1] < w else R[:, :w]
     return q, rem
 
 
@@ -391,13 +488,13 @@ def _shift_clear(c: Circuit, a: np.ndarray, k: int, kind: str) -> np.ndarray:
     B, w = a.shape[0], a.shape[1]
     k %= w
     if kind == "shl":
-        return np.concatenate([_zeros(c, B, k), a[:, :w - k]], axis=1)
+        return _cat([_zeros(c, B, k), a[:, :w - k]], axis=1)
     if kind == "shr":
-        return np.concatenate([a[:, k:], _zeros(c, B, k)], axis=1)
+        return _cat([a[:, k:], _zeros(c, B, k)], axis=1)
     if kind == "rotl":
-        return np.roll(a, k, axis=1)
+        return _roll(a, k, 1)
     if kind == "rotr":
-        return np.roll(a, -k, axis=1)
+        return _roll(a, -k, 1)
     raise ValueError(kind)
 
 
@@ -444,7 +541,7 @@ class FheUint:
                 stream0: int = 0) -> "FheUint":
         b = cls._bits_of(values, width)
         ct = ck.encrypt_bool(b.reshape(-1), seed, stream0).reshape(b.shape[0], width, -1)
-        return cls(circuit, ct)
+        return cls(circuit, circuit.to_device(ct))
 
     @classmethod
     def trivial(cls, circuit: Circuit, values, width: int) -> "FheUint":
@@ -459,7 +556,7 @@ class FheUint:
             return self
         if width < self.width:
             return FheUint(self.c, self.bits[:, :width])
-        return FheUint(self.c, np.concatenate([self.bits, _zeros(self.c, self.batch, width - self.width)], 1))
+        return FheUint(self.c, _cat([self.bits, _zeros(self.c, self.batch, width - self.width)], 1))
 
     # synchronous operator sugar (each call runs its own levels; use Circuit.run_many + fhevm_op
     # to batch independent operations)
@@ -496,6 +593,8 @@ class FheUint:
 
 def decrypt_bits(ck: ClientKey, bits: np.ndarray) -> np.ndarray:
     """(B,) uint64 for w <= 64; an object array of Python ints for wider values."""
+    if _is_t(bits):
+        bits = bits.cpu().numpy().view(np.uint64)
     B, w = bits.shape[0], bits.shape[1]
     b = ck.decrypt_bool(bits.reshape(-1, bits.shape[-1])).reshape(B, w)
     if w <= 64:
