@@ -1,0 +1,19 @@
+#!/bin/bash
+# End-of-round evidence on the final tree: the whole -m gpu suite, then the profile set of both FFT64 presets
+# (tools/profile_round.sh: bench line with the CPU baseline, rocprofv3 kernel stats, SQ / FETCH / WRITE / mix
+# counter passes -> <TAG>_roofline.json tagged with this tree's source_id).  Stops at the first failure.
+#   TAG=r04z bash tools/gpu_final.sh
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-r04z}
+if [ "${SUITE:-1}" = "1" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 420 --timeout-method thread -p no:cacheprovider > gpurun_out/${TAG}_full.log 2>&1 || { echo "gpu tests failed"; grep -E "FAILED|Error|passed|failed" gpurun_out/${TAG}_full.log | tail -20; exit 1; }
+  grep -E "passed|C5 |C4 on" gpurun_out/${TAG}_full.log | tail -6
+fi
+TAG=${TAG} PRESET=gate_fft bash tools/profile_round.sh > gpurun_out/${TAG}_prof.log 2>&1 || { echo "gate profile failed"; tail -20 gpurun_out/${TAG}_prof.log; exit 1; }
+tail -3 gpurun_out/${TAG}_prof.log
+TAG=${TAG}_fhevm PRESET=fhevm_fft bash tools/profile_round.sh > gpurun_out/${TAG}_fhevm_prof.log 2>&1 || { echo "fhevm profile failed"; tail -20 gpurun_out/${TAG}_fhevm_prof.log; exit 1; }
+tail -3 gpurun_out/${TAG}_fhevm_prof.log
+echo FINAL_OK
