@@ -13,14 +13,23 @@
  * coefficients are Z_2^128 words stored as two u64 planes (lo, hi); the decomposition reads the word
  * directly (tfhe-rs SignedDecomposer, 72 bits as 3 digits of 24, gadget 2^(128 - 24 (l + 1))).
  *
- * The external product restates the device's precision contract (tfhe_amd/csrc/sns.hip): at load every
- * key coefficient is rounded to the nearest multiple of 2^16 (or_sns_bsk_round), so a key word is
- * 2^16 x a 112-bit signed integer = 2^16 sum_t l_t 2^(16 t) with seven balanced 16-bit limbs l_t; the
- * product digits x key is then sum_t 2^(16 + 16 t) (sum_r d_r (*) l_(r, t)) mod 2^128, and every limb
- * convolution is an integer of magnitude <= 9 * 2048 * 2^23 * 2^15 = 2^52.2.  The oracle computes each
- * limb convolution EXACTLY with the negacyclic NTT mod p = 2^64 - 2^32 + 1 (|value| < p / 2: the
- * signed lift of the residue is the integer) -- an independent method from the device's f64 FFT, which
- * must land on the same integers.
+ * The external product restates the device's precision contract (tfhe_amd/csrc/sns.hip, sns_fft.h): at
+ * load every key coefficient is rounded to the nearest multiple of 2^16 (or_sns_bsk_round), so a key word
+ * is 2^16 x a 112-bit signed integer = 2^16 (l_0 + sum_(t=1..4) l_t 2^(48 + 16 (t - 1))) with l_0 the
+ * balanced low 48 bits and l_1..l_4 balanced 16-bit limbs (round 4; seven 16-bit limbs before).  The
+ * product digits x key is sum_t 2^(16 + w_t) (sum_r d_r (*) l_(r, t)) mod 2^128 (w_0 = 0,
+ * w_t = 48 + 16 (t - 1)):
+ *  * limbs 1..4: every convolution is an integer of magnitude <= 9 * 2048 * 2^23 * 2^15 = 2^52.2; the
+ *    oracle computes it EXACTLY with the negacyclic NTT mod p = 2^64 - 2^32 + 1 (|value| < p / 2: the
+ *    signed lift of the residue is the integer) -- an independent method from the device's f64 FFT, which
+ *    must land on the same integers;
+ *  * limb 0: its products reach 2^84 and the device's f64 values are not the exact integers (the error,
+ *    <= 2^33.3 even for all-maximum operands, lands at weight 2^16 of a 2^128 torus whose output noise is
+ *    ~2^64).  The oracle RESTATES the
+ *    device's f64 computation for this limb operation by operation (sf_* below: the twisted fold, the
+ *    radix-4 DIF / DIT stages, explicit fused multiply-adds, the 9-term MAC order, the untwist, rint and
+ *    the conversion of the double's bits), as oracle/fft_oracle.c does for the FFT64 PBS; contraction is
+ *    off (Makefile).
  *
  * Key generation: body = sum_j mask_j (*) S_j + e + s_i g_l (mod 2^128); the binary-key products are
  * computed here by rotated additions (the product library uses exact NTTs of 32-bit quarters: any exact
@@ -29,6 +38,7 @@
  * Parity unpinned (no squashed ciphertext in the reference); message-level checks pin
  * decrypt(squash(ct)) == decrypt(ct).
  */
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -193,10 +203,73 @@ void or_sns_keygen(const or_sns_params* sp, uint64_t seed, const uint64_t* lwe_k
   }
 }
 
+/* ---- the device's f64 transform for the low limb (tfhe_amd/csrc/sns_fft.h, restated) ---------------- */
+#define SF_M 1024
+typedef struct { double x, y; } sf_cd;
+static inline sf_cd sf_add(sf_cd a, sf_cd b) { return (sf_cd){a.x + b.x, a.y + b.y}; }
+static inline sf_cd sf_sub(sf_cd a, sf_cd b) { return (sf_cd){a.x - b.x, a.y - b.y}; }
+static inline sf_cd sf_cmul(sf_cd a, sf_cd b) { return (sf_cd){fma(a.x, b.x, -(a.y * b.y)), fma(a.x, b.y, a.y * b.x)}; }
+static inline sf_cd sf_cmulc(sf_cd a, sf_cd b) { return (sf_cd){fma(a.x, b.x, a.y * b.y), fma(a.y, b.x, -(a.x * b.y))}; }
+static inline sf_cd sf_cmac(sf_cd acc, sf_cd a, sf_cd b) {
+  return (sf_cd){fma(-a.y, b.y, fma(a.x, b.x, acc.x)), fma(a.y, b.x, fma(a.x, b.y, acc.y))};
+}
+/* T[e] = e^{2 pi i e / M}, P[m] = e^{i pi m / N}: long-double cosl / sinl rounded once (make_sns_fft_const) */
+static void sf_tables(sf_cd* T, sf_cd* P, uint32_t N) {
+  const long double pi = 3.141592653589793238462643383279502884L;
+  for (int e = 0; e < SF_M; e++) {
+    T[e] = (sf_cd){(double)cosl(2 * pi * e / SF_M), (double)sinl(2 * pi * e / SF_M)};
+    P[e] = (sf_cd){(double)cosl(pi * e / (int)N), (double)sinl(pi * e / (int)N)};
+  }
+}
+/* radix-4 DIF stage s over the whole array (positions in place), twiddles on the outputs */
+static void sf_dif_stage(sf_cd* a, int s, const sf_cd* T) {
+  const int lq = 8 - 2 * s, q = 1 << lq;
+  for (int t = 0; t < SF_M / 4; t++) {
+    const int j = t & (q - 1), base = ((t >> lq) << (lq + 2)) + j, e = j << (2 * s);
+    sf_cd* x = a + base;
+    const sf_cd x0 = x[0], x1 = x[q], x2 = x[2 * q], x3 = x[3 * q];
+    const sf_cd a0 = sf_add(x0, x2), a1 = sf_sub(x0, x2), a2 = sf_add(x1, x3), d = sf_sub(x1, x3);
+    const sf_cd a3 = {-d.y, d.x};
+    x[0] = sf_add(a0, a2);
+    x[q] = sf_cmul(sf_add(a1, a3), T[e]);
+    x[2 * q] = sf_cmul(sf_sub(a0, a2), T[2 * e]);
+    x[3 * q] = sf_cmul(sf_sub(a1, a3), T[3 * e]);
+  }
+}
+/* its DIT inverse: conjugate twiddles on the inputs, then the butterfly with -i */
+static void sf_dit_stage(sf_cd* a, int s, const sf_cd* T) {
+  const int lq = 8 - 2 * s, q = 1 << lq;
+  for (int t = 0; t < SF_M / 4; t++) {
+    const int j = t & (q - 1), base = ((t >> lq) << (lq + 2)) + j, e = j << (2 * s);
+    sf_cd* x = a + base;
+    const sf_cd y0 = x[0], y1 = sf_cmulc(x[q], T[e]), y2 = sf_cmulc(x[2 * q], T[2 * e]), y3 = sf_cmulc(x[3 * q], T[3 * e]);
+    const sf_cd b0 = sf_add(y0, y2), b1 = sf_sub(y0, y2), b2 = sf_add(y1, y3), d = sf_sub(y1, y3);
+    const sf_cd b3 = {d.y, -d.x};
+    x[0] = sf_add(b0, b2);
+    x[q] = sf_add(b1, b3);
+    x[2 * q] = sf_sub(b0, b2);
+    x[3 * q] = sf_sub(b1, b3);
+  }
+}
+/* N = 2048 integer coefficients -> spectrum: fold + twist by P, 5 DIF stages */
+static void sf_forward(const double* v, sf_cd* z, const sf_cd* T, const sf_cd* P) {
+  for (int m = 0; m < SF_M; m++) z[m] = sf_cmul((sf_cd){v[m], v[m + SF_M]}, P[m]);
+  for (int s = 0; s < 5; s++) sf_dif_stage(z, s, T);
+}
+/* an integer-valued double (|v| < 2^127) as a word mod 2^128 (snsf::f64_int_to_w128) */
+static u128 sf_to_w128(double v) {
+  if (v < 0x1p62 && v > -0x1p62) return (u128)(__int128)(long long)v;
+  uint64_t bits;
+  memcpy(&bits, &v, 8);
+  const int e = (int)((bits >> 52) & 0x7FF) - 1075;
+  const u128 m = (u128)((bits & 0xFFFFFFFFFFFFFull) | 0x10000000000000ull) << e;
+  return (bits >> 63) ? (u128)0 - m : m;
+}
+
 /* Load-time rounding of the squashing key (the device's precision contract, tfhe_amd/csrc/sns.hip): every
  * coefficient, read as a signed 128-bit integer, is rounded to the nearest multiple of 2^16 (ties up).
  * The rounding error (< 2^15 per mask and body coefficient) adds ~2^20 of phase noise to a key whose own
- * noise is 2^30; the rounded key is 2^16 x a 112-bit integer: seven balanced 16-bit limbs. */
+ * noise is 2^30; the rounded key is 2^16 x a 112-bit integer: the five limbs above. */
 void or_sns_bsk_round(const or_sns_params* sp, const uint64_t* bsk, uint64_t* out) {
   const size_t N = sp->N, planes = or_sns_bsk_len(sp) / (2 * N);
 #pragma omp parallel for schedule(static)
@@ -208,13 +281,19 @@ void or_sns_bsk_round(const or_sns_params* sp, const uint64_t* bsk, uint64_t* ou
     }
 }
 
-/* rounded key -> limb spectra: [i][r][j][t][N] (t = limb 0..6), NTT mod p1 of the signed limb values */
+/* rounded key -> limb spectra: [i][r][j][t][N] words, t = limb 0..4.  Limb 0 (the balanced low 48 bits) is
+ * stored as the device's f64 spectrum / M (1024 complex doubles, their bits in the N words); limbs 1..4 as
+ * NTTs mod p1 of the signed 16-bit limb values. */
 size_t or_sns_limb_ntt_len(const or_sns_params* sp) { return or_sns_bsk_len(sp) / 2 * OR_SNS_LIMBS; }
 void or_sns_bsk_to_limb_ntt(const or_sns_params* sp, const uint64_t* rounded, uint64_t* out) {
   const size_t N = sp->N, planes = or_sns_bsk_len(sp) / (2 * N);
+  sf_cd T[SF_M], P[SF_M];
+  sf_tables(T, P, (uint32_t)N);
 #pragma omp parallel for schedule(dynamic, 1)
   for (size_t pp = 0; pp < planes; pp++) {
     uint64_t* o = out + pp * OR_SNS_LIMBS * N;
+    double* low = (double*)malloc(N * sizeof(double));
+    sf_cd* z = (sf_cd*)malloc(SF_M * sizeof(sf_cd));
     for (size_t t = 0; t < N; t++) {
       __int128 rr = (__int128)ld128(rounded + 2 * pp * N, N, t) >> 16; /* exact: a multiple of 2^16 */
       for (int l = 0; l < OR_SNS_LIMBS; l++) {
@@ -222,14 +301,24 @@ void or_sns_bsk_to_limb_ntt(const or_sns_params* sp, const uint64_t* rounded, ui
         if (l == OR_SNS_LIMBS - 1) {
           v = (int64_t)rr; /* the top limb keeps the remainder (|.| <= 2^15) */
         } else {
-          const __int128 lim = ((rr + 0x8000) & 0xFFFF) - 0x8000;
-          rr = (rr - lim) >> 16;
+          const int bits = l == 0 ? 48 : 16;
+          const __int128 half = (__int128)1 << (bits - 1), mask = ((__int128)1 << bits) - 1;
+          const __int128 lim = ((rr + half) & mask) - half;
+          rr = (rr - lim) >> bits;
           v = (int64_t)lim;
         }
-        o[(size_t)l * N + t] = from_i64(v, SP[0]);
+        if (l == 0) low[t] = (double)v; /* |v| <= 2^47: exact */
+        else o[(size_t)l * N + t] = from_i64(v, SP[0]);
       }
     }
-    for (int l = 0; l < OR_SNS_LIMBS; l++) or_sns_ntt_fwd(0, o + (size_t)l * N, (uint32_t)N);
+    sf_forward(low, z, T, P);
+    for (int f = 0; f < SF_M; f++) {
+      const double w[2] = {z[f].x * (1.0 / SF_M), z[f].y * (1.0 / SF_M)};
+      memcpy(o + 2 * f, w, 16);
+    }
+    for (int l = 1; l < OR_SNS_LIMBS; l++) or_sns_ntt_fwd(0, o + (size_t)l * N, (uint32_t)N);
+    free(low);
+    free(z);
   }
 }
 
@@ -255,6 +344,11 @@ void or_sns_blind_rotate(const or_sns_params* sp, const uint64_t* bsk_limb, cons
   u128* rot = (u128*)malloc((size_t)N * sizeof(u128));
   uint64_t* dig = (uint64_t*)malloc((size_t)R * N * 8);
   uint64_t* s = (uint64_t*)malloc((size_t)N * 8);
+  double* dv = (double*)malloc((size_t)N * sizeof(double));
+  sf_cd* Df = (sf_cd*)malloc((size_t)R * SF_M * sizeof(sf_cd)); /* the low limb's digit spectra (f64) */
+  sf_cd* z = (sf_cd*)malloc(SF_M * sizeof(sf_cd));
+  sf_cd T[SF_M], P[SF_M];
+  sf_tables(T, P, N);
   int64_t d[8];
   /* acc = X^{-b~} * (0, .., 0, lut) */
   memset(a, 0, (size_t)(k + 1) * N * sizeof(u128));
@@ -271,8 +365,8 @@ void or_sns_blind_rotate(const or_sns_params* sp, const uint64_t* bsk_limb, cons
   const size_t bsk_i = (size_t)R * (k + 1) * OR_SNS_LIMBS * N;
   for (uint32_t i = 0; i < sp->n; i++) {
     const uint32_t ai = or_mod_switch(lwe[i], twoN);
-    if (!ai) continue;
-    /* digits of X^{ai} acc_c - acc_c, NTT mod p */
+    if (!ai) continue; /* zero digits: every product is an exact zero, on the device too */
+    /* digits of X^{ai} acc_c - acc_c: NTT mod p (limbs 1..4) and the device's f64 spectrum (limb 0) */
     for (uint32_t c = 0; c <= k; c++) {
       const u128* ac = a + (size_t)c * N;
       for (uint32_t t = 0; t < N; t++) {
@@ -287,11 +381,19 @@ void or_sns_blind_rotate(const or_sns_params* sp, const uint64_t* bsk_limb, cons
         for (uint32_t l = 0; l < L; l++) dig[(size_t)(c * L + l) * N + t] = from_i64(d[l], p);
       }
     }
-    for (uint32_t r = 0; r < R; r++) or_sns_ntt_fwd(0, dig + (size_t)r * N, N);
-    /* acc_j += sum_t 2^(16 + 16 t) * (sum_r d_r (*) l_(r, j, t)) mod 2^128 */
+    for (uint32_t r = 0; r < R; r++) {
+      for (uint32_t t = 0; t < N; t++) {
+        const uint64_t w = dig[(size_t)r * N + t];
+        dv[t] = w > p / 2 ? -(double)(p - w) : (double)w;
+      }
+      sf_forward(dv, Df + (size_t)r * SF_M, T, P);
+      or_sns_ntt_fwd(0, dig + (size_t)r * N, N);
+    }
     const uint64_t* bi = bsk_limb + bsk_i * i;
-    for (uint32_t j = 0; j <= k; j++)
-      for (int l = 0; l < OR_SNS_LIMBS; l++) {
+    for (uint32_t j = 0; j <= k; j++) {
+      u128* aj = a + (size_t)j * N;
+      /* limbs 1..4: acc_j += 2^(64 + 16 (l - 1)) * (sum_r d_r (*) l_(r, j, l)), exact */
+      for (int l = 1; l < OR_SNS_LIMBS; l++) {
         for (uint32_t t = 0; t < N; t++) {
           uint64_t acc_t = 0;
           for (uint32_t r = 0; r < R; r++)
@@ -299,17 +401,33 @@ void or_sns_blind_rotate(const or_sns_params* sp, const uint64_t* bsk_limb, cons
           s[t] = acc_t;
         }
         or_sns_ntt_inv(0, s, N);
-        const int shift = 16 + 16 * l;
-        u128* aj = a + (size_t)j * N;
+        const int shift = 64 + 16 * (l - 1);
         for (uint32_t t = 0; t < N; t++) {
           const __int128 v = s[t] > p / 2 ? -(__int128)(p - s[t]) : (__int128)s[t]; /* exact: |value| < 2^53 */
           aj[t] += (u128)v << shift;
         }
       }
+      /* limb 0, the device's f64 order: 9-term MAC from zero, 5 DIT stages, untwist, rint; acc_j += v << 16 */
+      for (int f = 0; f < SF_M; f++) {
+        sf_cd o = {0.0, 0.0};
+        for (uint32_t r = 0; r < R; r++) {
+          sf_cd kk;
+          memcpy(&kk, bi + (((size_t)r * (k + 1) + j) * OR_SNS_LIMBS) * N + 2 * f, 16);
+          o = sf_cmac(o, Df[(size_t)r * SF_M + f], kk);
+        }
+        z[f] = o;
+      }
+      for (int st = 4; st >= 0; st--) sf_dit_stage(z, st, T);
+      for (int m = 0; m < SF_M; m++) {
+        const sf_cd y = sf_cmulc(z[m], P[m]);
+        aj[m] += sf_to_w128(rint(y.x)) << 16;
+        aj[m + SF_M] += sf_to_w128(rint(y.y)) << 16;
+      }
+    }
   }
   for (uint32_t j = 0; j <= k; j++)
     for (uint32_t t = 0; t < N; t++) st128(acc + (size_t)j * poly, N, t, a[(size_t)j * N + t]);
-  free(a); free(rot); free(dig); free(s);
+  free(a); free(rot); free(dig); free(s); free(dv); free(Df); free(z);
 }
 
 /* acc -> LWE over Z_2^128, dim k*N (+ body): (lo, hi) pairs; a'_(cN) = A_c[0], a'_(cN + t) = -A_c[N - t] */

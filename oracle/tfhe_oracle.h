@@ -194,7 +194,7 @@ typedef struct or_sns_params {
   uint32_t n, k, N, base_log, level;
   int32_t noise_log2; /* Gaussian integer noise round(N(0,1) * 2^(64 + x)) added to 128-bit bodies */
 } or_sns_params;
-#define OR_SNS_LIMBS 7 /* balanced 16-bit limbs of a rounded key word (2^16 x a 112-bit integer) */
+#define OR_SNS_LIMBS 5 /* limbs of a rounded key word (2^16 x a 112-bit integer): low 48 bits + four 16-bit */
 int or_sns_params_preset(int preset, or_sns_params* out); /* 0: n=918 (P-FHEVM small key) k=2 N=2048 2^24x3 */
 uint64_t or_sns_prime(int which);                        /* 0: 2^64-2^32+1 (the limb products), 1: 2^64-2^34+1 */
 uint64_t or_sns_psi(int which, uint32_t N);
@@ -205,7 +205,7 @@ void or_sns_keygen(const or_sns_params* sp, uint64_t seed, const uint64_t* lwe_k
                    uint64_t* bsk /* nullable */);
 /* load-time rounding of the squashing key to multiples of 2^16 (signed 128-bit words; sns_oracle.c) */
 void or_sns_bsk_round(const or_sns_params* sp, const uint64_t* bsk, uint64_t* out);
-/* rounded key -> NTTs (mod prime 0) of its 7 signed 16-bit limb polynomials: [i][r][j][limb][N] */
+/* rounded key -> limb spectra [i][r][j][limb][N]: limb 0 (low 48 bits) the f64 spectrum / M as bits, limbs 1..4 NTTs mod prime 0 */
 size_t or_sns_limb_ntt_len(const or_sns_params* sp);
 void or_sns_bsk_to_limb_ntt(const or_sns_params* sp, const uint64_t* rounded, uint64_t* out);
 void or_sns_lut_identity(const or_sns_params* sp, uint32_t msg_modulus, uint64_t* lut /* [lo, hi][N] */);

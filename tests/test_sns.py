@@ -73,11 +73,20 @@ def _words(a):
     return [[int(lo) | (int(hi) << 64) for lo, hi in zip(p[0], p[1])] for p in a]
 
 
+def _digitrev4(p, digits=5):
+    r = 0
+    for _ in range(digits):
+        r, p = 4 * r + (p & 3), p >> 2
+    return r
+
+
 def test_key_rounding_and_limbs(oracle_mod):
     """or_sns_bsk_round (the device's load-time rounding): every key word, read as a signed 128-bit
     integer, becomes the nearest multiple of 2^16 (moved by at most 2^15), so a rounded word is 2^16 x a
-    112-bit integer; the seven balanced 16-bit limbs of or_sns_bsk_to_limb_ntt recombine to it mod 2^128
-    (the inverse NTT of the limb spectra returns the signed limbs)."""
+    112-bit integer.  or_sns_bsk_to_limb_ntt splits it into the balanced low 48 bits (limb 0, stored as the
+    device's f64 spectrum / M: numpy's transform of the twisted fold, in base-4 digit-reversed order) and
+    four balanced 16-bit limbs (NTTs; the inverse NTT returns the signed limbs); they recombine to the
+    rounded word mod 2^128."""
     import ctypes
     osp = oracle_mod.sns_params(0)
     osp.n = 1
@@ -85,18 +94,28 @@ def test_key_rounding_and_limbs(oracle_mod):
     out = np.zeros_like(keys.bsk)
     oracle_mod.lib().or_sns_bsk_round(ctypes.byref(osp), oracle_mod._p(keys.bsk), oracle_mod._p(out))
     words, rounded = _words(keys.bsk.reshape(-1, 2, 2048)), _words(out.reshape(-1, 2, 2048))
-    limb = keys.bsk_limb.reshape(-1, 7, 2048)
+    limb = keys.bsk_limb.reshape(-1, 5, 2048)
     p1 = 0xFFFFFFFF00000001
     rng = np.random.default_rng(5)
     signed = lambda v: v - (1 << 128) if v >> 127 else v
+    order = np.array([_digitrev4(q) for q in range(1024)])
+    psi = np.exp(1j * np.pi * np.arange(1024) / 2048)
     for pp in rng.integers(0, len(words), 4):
-        lv = [oracle_mod.sns_ntt(0, limb[pp, t].copy(), inverse=True) for t in range(7)]
-        for t in list(rng.integers(0, 2048, 40)) + [0, 2047]:
+        lv = [oracle_mod.sns_ntt(0, limb[pp, t].copy(), inverse=True) for t in range(1, 5)]
+        low = np.zeros(2048)
+        for t in range(2048):
             x, y = signed(words[pp][t]), signed(rounded[pp][t])
             assert y % 65536 == 0 and abs(y - x) <= 32768 and abs(y >> 16) < 2 ** 111
-            ls = [int(lv[u][t]) - p1 if int(lv[u][t]) > p1 // 2 else int(lv[u][t]) for u in range(7)]
+            ls = [int(v[t]) - p1 if int(v[t]) > p1 // 2 else int(v[t]) for v in lv]
             assert all(abs(v) <= 32768 for v in ls)
-            assert sum(v << (16 + 16 * u) for u, v in enumerate(ls)) % (1 << 128) == rounded[pp][t]
+            up = sum(v << (64 + 16 * u) for u, v in enumerate(ls))
+            m = signed((rounded[pp][t] - up) % (1 << 128))
+            assert m % 65536 == 0 and abs(m >> 16) <= 2 ** 47
+            low[t] = m >> 16
+        spec = limb[pp, 0].view(np.float64).reshape(1024, 2)
+        spec = spec[:, 0] + 1j * spec[:, 1]
+        want = np.fft.ifft((low[:1024] + 1j * low[1024:]) * psi)   # sum_m z_m e^{+2 pi i m k / M} / M
+        assert np.max(np.abs(spec - want[order])) <= 2 ** -40 * np.max(np.abs(want))
 
 
 def test_lut_identity_native(oracle_mod):
@@ -115,13 +134,14 @@ def test_lut_identity_native(oracle_mod):
 
 def test_fft_limb_product_exactness(tmp_path):
     """tools/sns_fft_check.cpp runs the device's FFT stage functions (tfhe_amd/csrc/sns_fft.h) on the
-    host: 9-term digit x limb products at N = 2048 with uniform and extreme-magnitude random operands
+    host: 9-term digit x 16-bit limb products (limbs 1..4; the low 48-bit limb is inexact by design and
+    restated by the oracle) at N = 2048 with uniform and extreme-magnitude random operands
     land within 0.07 of the exact integers (rint() exact with margin), and the adversarial all-maximum
     operand (|value| = 2^52.2, no f64 headroom) is reported as the one inexact case."""
     import subprocess
     root = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
     exe = tmp_path / "sns_fft_check"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-I", f"{root}/tfhe_amd/csrc", f"{root}/tools/sns_fft_check.cpp",
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", f"{root}/tfhe_amd/csrc", f"{root}/tools/sns_fft_check.cpp",
                     "-o", str(exe)], check=True)
     for form in ("s", "w"):  # the 256-thread stage form (inverse, key conversion) and the one-wave form (step 1)
         out = subprocess.run([str(exe), "6", form], capture_output=True, text=True).stdout
@@ -130,19 +150,22 @@ def test_fft_limb_product_exactness(tmp_path):
                 if l.startswith("trial")]
         assert len(errs) == 6
         assert all(e < 0.07 for mode, e in errs if mode != 2)
+    out = subprocess.run([str(exe), "3", "s", "48"], capture_output=True, text=True)   # the low 48-bit limb
+    assert out.returncode == 0 and "OK: below 2^34" in out.stdout, out.stdout
 
 
 def test_device_arithmetic_replay_matches_oracle(tmp_path):
     """tools/sns_native_check.cpp replays the squash blind rotation on the host with the device's own
     shared code (sns_fft.h: key rounding + limb split, 128-bit decomposition, Horner recombination, the
     one-wave forward passes of step 1, the stage-form key / inverse transforms, the MAC order) and
-    compares every accumulator word with oracle/sns_oracle.c (exact Goldilocks limb NTTs): arbitrary
-    64-bit input words and a trivial-mask ciphertext at n = 24."""
+    compares every accumulator word with oracle/sns_oracle.c (exact Goldilocks NTTs for limbs 1..4, its own
+    restatement of the f64 operation order for the low limb): arbitrary 64-bit input words and a
+    trivial-mask ciphertext at n = 24."""
     import os
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     exe = tmp_path / "sns_native_check"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-I", f"{root}/tfhe_amd/csrc", "-I", f"{root}/oracle",
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", f"{root}/tfhe_amd/csrc", "-I", f"{root}/oracle",
                     f"{root}/tools/sns_native_check.cpp", "-L", f"{root}/oracle", "-loracle",
                     f"-Wl,-rpath,{root}/oracle", "-o", str(exe)], check=True)
     out = subprocess.run([str(exe), "24", "3"], capture_output=True, text=True)

@@ -71,7 +71,7 @@ void make_sns_fft_const(void* out);
 size_t sns_fft_key_len(size_t n);  // key limb spectra, in 16-byte complex
 size_t sns_digit_len(size_t B);    // digit spectra workspace, in 16-byte complex
 size_t sns_fft_prod_len(size_t B);  // MAC product workspace, in 16-byte complex
-constexpr size_t SNS_FFT_POLY_BYTES = 7 * 1024 * 16;  // limb spectra of one (i, r, j) key polynomial
+constexpr size_t SNS_FFT_POLY_BYTES = 5 * 1024 * 16;  // limb spectra of one (i, r, j) key polynomial (sns_fft.h SF_LIMBS)
 hipError_t launch_sns_bsk_to_fft(const u64* bsk_std, void* bsk_fft, size_t polys, const void* d_fconst,
                                  hipStream_t s);
 hipError_t launch_sns_blind_rotate(const u64* lwe, size_t B, int n, const u64* lut, const void* bsk_fft, u64* acc,

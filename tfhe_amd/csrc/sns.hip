@@ -5,15 +5,17 @@
 // an LWE over Z_2^128 (dim 4096) with ~2^-63 noise.  The GLWE ring is the native 2^128 torus, as in
 // tfhe-rs: a coefficient is one u128 word stored as two u64 planes, polynomial = [lo][N], [hi][N].
 //
-// The external product is exact and f64 (sns_fft.h): the key, rounded at load to multiples of 2^16, is
-// seven balanced 16-bit limbs; each 9-term digit x limb convolution is an integer below 2^52.2 that an
-// f64 FFT product returns exactly after rint(); the limbs recombine with 128-bit wrap-around shifts.
+// The external product is f64 (sns_fft.h): the key, rounded at load to multiples of 2^16, is five limbs --
+// the balanced low 48 bits and four balanced 16-bit limbs.  Each 9-term digit x 16-bit-limb convolution is
+// an integer below 2^52.2 that an f64 FFT product returns exactly after rint(); the low limb's products are
+// rounded f64 values whose error lands at weight 2^16, far below the output noise, and whose operation
+// order the oracle restates.  The limbs recombine with 128-bit wrap-around shifts.
 // Work shape per CMUX (accumulator, 96 KB per ciphertext, in HBM):
 //   sns_step1f (ciphertext, component c): X^{a_i} acc_c - acc_c, signed 2^24 x 3 digits, forward FFT
 //              of each digit polynomial (one per wave) -> Df
 //   sns_mac    key-stationary MAC: a 16-frequency tile of the CMUX's key in LDS, ciphertexts streamed
 //              through it -> O[ct][output j][limb t][M]
-//   sns_inv    (ciphertext, output j): 7 inverse FFTs, rint, Horner over the limbs, acc_j +=
+//   sns_inv    (ciphertext, output j): 5 inverse FFTs, rint, Horner over the limbs, acc_j +=
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdlib.h>
@@ -30,6 +32,8 @@ constexpr int SN = 2048, SK = 2, SL = 3, SR = (SK + 1) * SL, ST = 256;
 using snsf::cd;
 using snsf::SF_LIMBS;
 using snsf::SF_M;
+
+static_assert(SNS_FFT_POLY_BYTES == (size_t)SF_LIMBS * SF_M * sizeof(cd), "key polynomial stride (pbs_kernels.h)");
 
 struct SnsFftConst {
   cd T[SF_M];  // e^{2 pi i e / M}
@@ -71,7 +75,7 @@ __device__ __forceinline__ void fft_fwd_lds(cd* buf, const cd* __restrict__ T) {
   }
 }
 
-// BSK words (lo, hi planes) -> rounded key, 7 balanced 16-bit limbs, spectra / M (oracle:
+// BSK words (lo, hi planes) -> rounded key, its 5 limbs (snsf::key_limb), spectra / M (oracle:
 // or_sns_bsk_round + or_sns_bsk_to_limb_ntt: the same limbs).  One workgroup per (i, r, j) polynomial.
 __global__ void __launch_bounds__(ST) sns_bsk_to_fft_kernel(const u64* __restrict__ in, cd* __restrict__ out,
                                                             const SnsFftConst* __restrict__ Fc) {
@@ -90,7 +94,7 @@ __global__ void __launch_bounds__(ST) sns_bsk_to_fft_kernel(const u64* __restric
   for (int t = 0; t < SF_LIMBS; t++) {
     double lv[8];
 #pragma unroll
-    for (int e = 0; e < 8; e++) lv[e] = (double)snsf::key_limb(rr[e], t == SF_LIMBS - 1);
+    for (int e = 0; e < 8; e++) lv[e] = (double)snsf::key_limb(rr[e], t);
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const int m = threadIdx.x + 256 * u;
@@ -182,14 +186,14 @@ __global__ void __launch_bounds__(ST) sns_step1f_kernel(const u64* __restrict__ 
   }
 }
 
-// The MAC as a frequency-tiled kernel whose workgroup holds the CMUX's key for 16 frequencies x all 21
-// (output, limb) columns in LDS (48 KB) and streams 32 ciphertexts' digit spectra through it, writing the
-// products O[ct][j*7+t][M] to global memory (a one-kernel step 2 re-reads the ~1 MB per-output key slice
+// The MAC as a frequency-tiled kernel whose workgroup holds the CMUX's key for 16 frequencies x all 15
+// (output, limb) columns in LDS (34.6 KB) and streams 32 ciphertexts' digit spectra through it, writing the
+// products O[ct][j*5+t][M] to global memory (a one-kernel step 2 re-reads the ~1 MB per-output key slice
 // for every ciphertext: 6.3 GB of L2 traffic per CMUX, measured 497 us against 86).
 // Grid: (M / 16) frequency tiles x G ciphertext-group slots; slot g walks the groups g, g + G, ..., so a
 // slot stages its key tile once for all its groups.  The first group's digit spectra are requested before
 // the key tile is staged, so those loads overlap the LDS fill.
-constexpr int MAC_F = 16, MAC_CT = 32, MAC_JT = (SK + 1) * SF_LIMBS;  // 21 (output, limb) columns
+constexpr int MAC_F = 16, MAC_CT = 32, MAC_JT = (SK + 1) * SF_LIMBS;  // 15 (output, limb) columns
 constexpr int MAC_SLOTS = 8;
 
 __device__ __forceinline__ void mac_load(const cd* __restrict__ Df, int c0, int B, int f0, int f, int cl,
@@ -204,7 +208,7 @@ __device__ __forceinline__ void mac_load(const cd* __restrict__ Df, int c0, int 
 
 __global__ void __launch_bounds__(ST, 3) sns_mac_kernel(const cd* __restrict__ Df, const cd* __restrict__ kf_i,
                                                         cd* __restrict__ O, int B) {
-  __shared__ cd kt[SR * MAC_JT][MAC_F];  // [r * 21 + jt][f]
+  __shared__ cd kt[SR * MAC_JT][MAC_F];  // [r * 15 + jt][f]
   constexpr int FT = SF_M / MAC_F;
   const int f0 = (blockIdx.x % FT) * MAC_F;
   const int slots = gridDim.x / FT, groups = (B + MAC_CT - 1) / MAC_CT;
@@ -213,7 +217,7 @@ __global__ void __launch_bounds__(ST, 3) sns_mac_kernel(const cd* __restrict__ D
   int g = blockIdx.x / FT;
   cd da[SR], db[SR];
   mac_load(Df, g * MAC_CT, B, f0, f, cl, da, db);
-  // key tile: row (r, jt) of the CMUX's key = kf_i[(r * 21 + jt) * M + f0 .. + 16]
+  // key tile: row (r, jt) of the CMUX's key = kf_i[(r * 15 + jt) * M + f0 .. + 16]
   for (int x = threadIdx.x; x < SR * MAC_JT * MAC_F; x += ST) {
     const int row = x / MAC_F, fx = x % MAC_F;
     kt[row][fx] = kf_i[(size_t)row * SF_M + f0 + fx];
@@ -263,9 +267,12 @@ __device__ __forceinline__ void fft_inv_reg(const cd* __restrict__ o, cd* buf, c
   snsf::r4_dit(y[0], y[1], y[2], y[3], t, T);  // dit_stage(s = 0): base t, q 256, e = t
 }
 
-// (ciphertext, output j): the 7 inverse transforms one after another by all 256 threads, top limb first;
-// each thread untwists and rounds its 8 coefficients (|c| < 2^53: exact) and folds them into u128 Horner
-// sums h = (h << 16) + c, which wrap mod 2^128 like the torus: h = sum_t c_t 2^(16 t), acc_j += h << 16.
+// (ciphertext, output j): the 5 inverse transforms one after another by all 256 threads, top limb first;
+// each thread untwists and rounds its 8 coefficients (limbs 4..1: |c| < 2^53, exact) and folds them into u128
+// Horner sums h = (h << 16) + c, then h = (h << 48) + c_0 for the low limb (|c_0| < 2^85, converted from the
+// double's bits); the sums wrap mod 2^128 like the torus, acc_j += h << 16.
+// (A prefetch of the next limb's points and of the accumulator words measured slower: a barrier waits for
+// every outstanding global load, so the requests only lengthened each pass; profiles/r04g_sns_ab.txt.)
 __global__ void __launch_bounds__(ST, 3) sns_inv_kernel(const cd* __restrict__ O, u64* __restrict__ acc,
                                                         const SnsFftConst* __restrict__ Fc) {
   __shared__ cd buf[SF_M];
@@ -283,8 +290,13 @@ __global__ void __launch_bounds__(ST, 3) sns_inv_kernel(const cd* __restrict__ O
     for (int u = 0; u < 4; u++) {
       const int m = threadIdx.x + 256 * u;
       const cd y = snsf::cmulc(yr[u], F.P[m]);
-      h[2 * u] = snsf::horner16(h[2 * u], __builtin_rint(y.x));
-      h[2 * u + 1] = snsf::horner16(h[2 * u + 1], __builtin_rint(y.y));
+      if (t > 0) {
+        h[2 * u] = snsf::horner16(h[2 * u], __builtin_rint(y.x));
+        h[2 * u + 1] = snsf::horner16(h[2 * u + 1], __builtin_rint(y.y));
+      } else {
+        h[2 * u] = snsf::horner_low(h[2 * u], __builtin_rint(y.x));
+        h[2 * u + 1] = snsf::horner_low(h[2 * u + 1], __builtin_rint(y.y));
+      }
     }
     __syncthreads();
   }

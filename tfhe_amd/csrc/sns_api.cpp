@@ -55,7 +55,7 @@ struct DevGuard {
   }
 };
 
-// ciphertexts per pass (acc 96 KB + digit spectra 147 KB + MAC products 344 KB each);
+// ciphertexts per pass (acc 96 KB + digit spectra 147 KB + MAC products 246 KB each);
 // TFHE_HIP_SNS_CHUNK overrides
 size_t sns_chunk() {
   static const size_t v = [] {
@@ -73,11 +73,11 @@ struct tfhe_sns_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   void* d_fconst = nullptr;
-  void* d_bskf = nullptr;  // key limb spectra (n x 9 x 3 x 7 x 1024 complex f64)
+  void* d_bskf = nullptr;  // key limb spectra (n x 9 x 3 x 5 x 1024 complex f64)
   bool key = false;
   u64* d_acc = nullptr;    // chunk x 3 x (lo, hi) x N
   void* d_D = nullptr;     // digit spectra (chunk x 9 x 1024 complex)
-  void* d_O = nullptr;     // MAC products (chunk x 21 x 1024 complex)
+  void* d_O = nullptr;     // MAC products (chunk x 15 x 1024 complex)
   u64* d_lut = nullptr;
   uint32_t lut_mm = 0;
   size_t ws_cap = 0;

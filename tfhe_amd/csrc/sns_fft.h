@@ -2,13 +2,20 @@
 // native 2^128 word arithmetic around it, shared by the device kernels and the host checks
 // (tools/sns_fft_check.cpp: FFT accuracy; tools/sns_native_check.cpp: the whole CMUX vs the oracle).
 //
-// The squashing ring is the native 2^128 torus.  Its product digits x BSK is computed as EXACT integer
-// convolutions: every BSK word, read as a signed 128-bit integer and rounded to a multiple of 2^16 (the
-// load-time rounding; oracle: or_sns_bsk_round), is split into SF_LIMBS balanced 16-bit limbs, and each
-// digit-polynomial x limb-polynomial convolution (|value| <= 9 * 2048 * 2^23 * 2^15 = 2^52.2) is one f64
-// FFT product whose rounding error stays far below 1/2 (tools/sns_fft_check.cpp measures it), so rint()
-// returns the exact integer; the limbs recombine as sum_t c_t 2^(16 + 16 t) mod 2^128 -- bit-identical to
-// the oracle's exact NTT limb products.
+// The squashing ring is the native 2^128 torus.  Every BSK word, read as a signed 128-bit integer and
+// rounded to a multiple of 2^16 (the load-time rounding; oracle: or_sns_bsk_round), is 2^16 x a 112-bit
+// integer, split into SF_LIMBS = 5 limbs (round 4; seven 16-bit limbs before): limb 0 is the balanced
+// low 48 bits, limbs 1..4 are balanced 16-bit limbs (the top one keeps the remainder).
+//  * limbs 1..4: each digit-polynomial x limb-polynomial convolution (|value| <= 9 * 2048 * 2^23 * 2^15 =
+//    2^52.2) is one f64 FFT product whose rounding error stays far below 1/2 (tools/sns_fft_check.cpp
+//    measures it), so rint() returns the exact integer;
+//  * limb 0 (|l| <= 2^47): its products reach 2^84 and are NOT exact; their f64 rounding error (measured by
+//    tools/sns_fft_check.cpp: <= 2^28 for random operands, 2^33.3 for the all-maximum worst case) lands at
+//    weight 2^16 of the accumulator, <= 2^49.3 against the squashed ciphertext's ~2^64 noise.  Only the low limb can be inexact: an error in limb t > 0 is multiplied by 2^(64 + 16 (t - 1)).
+//    Its value is defined by THIS file's operation order -- explicit fma in cmul / cmulc / cmac,
+//    contraction off, the stage order below -- which oracle/sns_oracle.c restates word for word, so the
+//    device, the host replay and the oracle agree bit for bit.
+// The limbs recombine as h = ((c4 2^16 + c3) 2^16 + c2) 2^16 + c1) 2^48 + c0, acc += h << 16 mod 2^128.
 //
 // Transform: N = 2048 real coefficients folded to M = 1024 complex z_m = (a_m + i a_{m+1024}) psi^m,
 // psi = e^{i pi / 2048} (so the cyclic DFT of z evaluates a at the odd powers of psi), then a radix-4
@@ -17,6 +24,9 @@
 // M (the 1/M is folded into the key spectra).  Spectra stay in digit-reversed order: the MAC is
 // pointwise, so key and digits only need the same order.
 #pragma once
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
 
 #if defined(__HIPCC__)
 #define SF_HD __host__ __device__ __forceinline__
@@ -32,13 +42,18 @@ struct cd {
 };
 
 constexpr int SF_N = 2048, SF_M = 1024, SF_NT = 256;  // coefficients, complex points, threads per transform
-constexpr int SF_LIMBS = 7, SF_LIMB_BITS = 16, SF_DROP = 16;
+constexpr int SF_LIMBS = 5, SF_LIMB_BITS = 16, SF_LOW_BITS = 48, SF_DROP = 16;
 
+// complex arithmetic with explicit fused multiply-adds (oracle/sns_oracle.c: sf_cmul, sf_cmulc, sf_cmac)
 SF_HD cd cadd(cd a, cd b) { return {a.x + b.x, a.y + b.y}; }
 SF_HD cd csub(cd a, cd b) { return {a.x - b.x, a.y - b.y}; }
-SF_HD cd cmul(cd a, cd b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
-SF_HD cd cmulc(cd a, cd b) { return {a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y}; }  // a * conj(b)
-SF_HD cd cmac(cd acc, cd a, cd b) { return {acc.x + a.x * b.x - a.y * b.y, acc.y + a.x * b.y + a.y * b.x}; }
+SF_HD cd cmul(cd a, cd b) { return {__builtin_fma(a.x, b.x, -(a.y * b.y)), __builtin_fma(a.x, b.y, a.y * b.x)}; }
+SF_HD cd cmulc(cd a, cd b) {  // a * conj(b)
+  return {__builtin_fma(a.x, b.x, a.y * b.y), __builtin_fma(a.y, b.x, -(a.x * b.y))};
+}
+SF_HD cd cmac(cd acc, cd a, cd b) {
+  return {__builtin_fma(-a.y, b.y, __builtin_fma(a.x, b.x, acc.x)), __builtin_fma(a.y, b.x, __builtin_fma(a.x, b.y, acc.y))};
+}
 
 // Radix-4 DIF butterfly with output twiddles T[e k] (e = j * 4^s), and its DIT inverse (conjugate
 // input twiddles, then the butterfly with -i): dit(dif(x)) = 4 x.
@@ -133,12 +148,15 @@ typedef unsigned __int128 w128;
 // The add wraps mod 2^128, so a word within 2^15 of 2^127 rounds to -2^127: the same torus point.
 SF_HD __int128 key_round16(w128 w) { return (__int128)(w + ((w128)1 << 15)) >> 16; }
 
-// the next balanced 16-bit limb of a rounded key word (rr = word / 2^16, consumed from the bottom); the
-// top limb (t = SF_LIMBS - 1) keeps the remainder, |.| <= 2^15
-SF_HD long long key_limb(__int128& rr, bool top) {
-  if (top) return (long long)rr;
-  const __int128 l = ((rr + 0x8000) & 0xFFFF) - 0x8000;
-  rr = (rr - l) >> 16;
+// limb t of a rounded key word (rr = word / 2^16), consumed from the bottom (call t = 0, 1, .., 4 in order):
+// t = 0 the balanced low 48 bits (|.| <= 2^47, exact in a double), t = 1..3 balanced 16-bit limbs, t = 4 the
+// remainder (|.| <= 2^15)
+SF_HD long long key_limb(__int128& rr, int t) {
+  if (t == SF_LIMBS - 1) return (long long)rr;
+  const int bits = t == 0 ? SF_LOW_BITS : SF_LIMB_BITS;
+  const __int128 half = (__int128)1 << (bits - 1), mask = ((__int128)1 << bits) - 1;
+  const __int128 l = ((rr + half) & mask) - half;
+  rr = (rr - l) >> bits;
   return (long long)l;
 }
 
@@ -157,8 +175,19 @@ SF_HD void digits72(w128 y, int (&d)[3]) {
   }
 }
 
-// one Horner step over the limbs (top limb first): h = sum_t c_t 2^(16 t) mod 2^128; acc += h << 16
+// one Horner step over the exact limbs (top limb first): h = sum_(t >= 1) c_t 2^(16 (t - 1))
 SF_HD w128 horner16(w128 h, double c_rounded) { return (h << 16) + (w128)(__int128)(long long)c_rounded; }
+
+// an integer-valued double (|v| < 2^127) as a word mod 2^128: the low limb's products exceed 2^63
+SF_HD w128 f64_int_to_w128(double v) {
+  if (v < 0x1p62 && v > -0x1p62) return (w128)(__int128)(long long)v;
+  const unsigned long long bits = __builtin_bit_cast(unsigned long long, v);
+  const int e = (int)((bits >> 52) & 0x7FF) - 1075;  // >= 10 here
+  const w128 m = (w128)((bits & 0xFFFFFFFFFFFFFull) | 0x10000000000000ull) << e;
+  return (bits >> 63) ? (w128)0 - m : m;
+}
+// the last step: h = h 2^48 + c_0 (the low limb); acc += h << 16
+SF_HD w128 horner_low(w128 h, double c_rounded) { return (h << SF_LOW_BITS) + f64_int_to_w128(c_rounded); }
 
 }  // namespace snsf
 }  // namespace tfhe

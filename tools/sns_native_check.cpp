@@ -1,10 +1,10 @@
 // Host replay of the noise-squashing blind rotation exactly as the device computes it (tfhe_amd/csrc/sns.hip),
 // against the oracle (oracle/sns_oracle.c, linked as liboracle.so: this is a test tool).  Shared with the
 // device through sns_fft.h: the key rounding and limb split (key_round16 / key_limb), the 128-bit
-// decomposition (digits72), the Horner recombination (horner16) and the FFT passes -- the one-wave form of
+// decomposition (digits72), the Horner recombination (horner16, horner_low) and the FFT passes -- the one-wave form of
 // step 1 for the digit spectra, the 256-thread stage form for the key spectra and the inverse.  Run at a
 // reduced input dimension with arbitrary 64-bit input words; prints the accumulator words that differ.
-//   g++ -O2 -std=c++17 -I tfhe_amd/csrc -I oracle tools/sns_native_check.cpp -L oracle -loracle \
+//   g++ -O2 -std=c++17 -ffp-contract=off -I tfhe_amd/csrc -I oracle tools/sns_native_check.cpp -L oracle -loracle \
 //       -Wl,-rpath,$PWD/oracle -o /tmp/sns_native_check && /tmp/sns_native_check [n] [cts]
 #include <math.h>
 #include <stdint.h>
@@ -79,7 +79,7 @@ int main(int argc, char** argv) {
   or_sns_bsk_to_limb_ntt(&sp, rounded.data(), limb.data());
   or_sns_lut_identity(&sp, 16, lut.data());
 
-  // sns_bsk_to_fft_kernel: per (i, r, j) polynomial, 7 limb spectra / M (stage form)
+  // sns_bsk_to_fft_kernel: per (i, r, j) polynomial, 5 limb spectra / M (stage form)
   const size_t polys = bsk.size() / (2 * N);
   std::vector<cd> kf(polys * LIMBS * SF_M);
   std::vector<__int128> rr(N);
@@ -88,7 +88,7 @@ int main(int argc, char** argv) {
     for (int x = 0; x < N; x++) rr[x] = key_round16(ld(&bsk[p * 2 * N], x));
     for (int t = 0; t < LIMBS; t++) {
       std::vector<double> lv(N);
-      for (int x = 0; x < N; x++) lv[x] = (double)key_limb(rr[x], t == LIMBS - 1);
+      for (int x = 0; x < N; x++) lv[x] = (double)key_limb(rr[x], t);
       for (int m = 0; m < SF_M; m++) z[m] = cmul(cd{lv[m], lv[m + SF_M]}, P[m]);
       for (int s = 0; s < 5; s++)
         for (int th = 0; th < SF_NT; th++) dif_stage(z.data(), s, th, T);
@@ -142,8 +142,8 @@ int main(int argc, char** argv) {
             for (int th = 0; th < SF_NT; th++) dit_stage(z.data(), s, th, T);
           for (int m = 0; m < SF_M; m++) {
             const cd y = cmulc(z[m], P[m]);
-            h[m] = horner16(h[m], rint(y.x));
-            h[m + SF_M] = horner16(h[m + SF_M], rint(y.y));
+            h[m] = t ? horner16(h[m], rint(y.x)) : horner_low(h[m], rint(y.x));
+            h[m + SF_M] = t ? horner16(h[m + SF_M], rint(y.y)) : horner_low(h[m + SF_M], rint(y.y));
           }
         }
         uint64_t* a = &acc[(size_t)j * 2 * N];
