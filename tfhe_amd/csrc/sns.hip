@@ -120,6 +120,29 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// The rest of a one-wave forward transform after pass 01 (x in registers, pass-01 order): two exchanges
+// through the wave's padded buffer, passes 23 and 4, then the spectrum stored contiguously in DIF position order.
+__device__ __forceinline__ void wave_fwd_tail(cd (&x)[16], int t, const cd* __restrict__ T, cd* buf, cd* __restrict__ o) {
+#pragma unroll
+  for (int r = 0; r < 16; r++) buf[snsf::pad(snsf::pt01(t, r))] = x[r];
+  wave_sync();
+#pragma unroll
+  for (int r = 0; r < 16; r++) x[r] = buf[snsf::pad(snsf::pt23(t, r))];
+  snsf::dif_pass23(x, t, T);
+#pragma unroll
+  for (int r = 0; r < 16; r++) buf[snsf::pad(snsf::pt23(t, r))] = x[r];
+  wave_sync();
+#pragma unroll
+  for (int r = 0; r < 16; r++) x[r] = buf[snsf::pad(snsf::pt4(t, r))];
+  snsf::dif_pass4(x, T);
+  wave_sync();  // every lane has read its pass-4 inputs before the buffer takes the outputs
+#pragma unroll
+  for (int r = 0; r < 16; r++) buf[snsf::pad(snsf::pt4(t, r))] = x[r];
+  wave_sync();
+#pragma unroll
+  for (int r = 0; r < 16; r++) o[64 * r + t] = buf[snsf::pad(64 * r + t)];
+}
+
 // step 1 digits: coefficient t of X^{a_i} acc is +-acc[(t - a_i) mod 2N], read straight from global memory
 // (a shifted contiguous window, coalesced), minus acc[t], decomposed as a 128-bit word (tfhe-rs
 // SignedDecomposer: 72 bits, 3 digits of 24, gadget 2^(128 - 24 (l + 1)))
@@ -162,28 +185,7 @@ __global__ void __launch_bounds__(ST) sns_step1f_kernel(const u64* __restrict__ 
     snsf::dif_pass01(x, t, F.T);
   }
   __syncthreads();  // every digit read is done before the exchange buffers overwrite the digits
-  if (w < SL) {
-    cd* buf = xbuf + w * snsf::SF_PADDED;
-#pragma unroll
-    for (int r = 0; r < 16; r++) buf[snsf::pad(snsf::pt01(t, r))] = x[r];
-    wave_sync();
-#pragma unroll
-    for (int r = 0; r < 16; r++) x[r] = buf[snsf::pad(snsf::pt23(t, r))];
-    snsf::dif_pass23(x, t, F.T);
-#pragma unroll
-    for (int r = 0; r < 16; r++) buf[snsf::pad(snsf::pt23(t, r))] = x[r];
-    wave_sync();
-#pragma unroll
-    for (int r = 0; r < 16; r++) x[r] = buf[snsf::pad(snsf::pt4(t, r))];
-    snsf::dif_pass4(x, F.T);
-    wave_sync();  // every lane has read its pass-4 inputs before the buffer takes the outputs
-#pragma unroll
-    for (int r = 0; r < 16; r++) buf[snsf::pad(snsf::pt4(t, r))] = x[r];
-    wave_sync();
-    cd* o = Df + ((size_t)ct * SR + c * SL + w) * SF_M;  // spectra in DIF position order, stored contiguously
-#pragma unroll
-    for (int r = 0; r < 16; r++) o[64 * r + t] = buf[snsf::pad(64 * r + t)];
-  }
+  if (w < SL) wave_fwd_tail(x, t, F.T, xbuf + w * snsf::SF_PADDED, Df + ((size_t)ct * SR + c * SL + w) * SF_M);
 }
 
 // The MAC as a frequency-tiled kernel whose workgroup holds the CMUX's key for 16 frequencies x all 15
@@ -271,8 +273,10 @@ __device__ __forceinline__ void fft_inv_reg(const cd* __restrict__ o, cd* buf, c
 // each thread untwists and rounds its 8 coefficients (limbs 4..1: |c| < 2^53, exact) and folds them into u128
 // Horner sums h = (h << 16) + c, then h = (h << 48) + c_0 for the low limb (|c_0| < 2^85, converted from the
 // double's bits); the sums wrap mod 2^128 like the torus, acc_j += h << 16.
-// (A prefetch of the next limb's points and of the accumulator words measured slower: a barrier waits for
-// every outstanding global load, so the requests only lengthened each pass; profiles/r04g_sns_ab.txt.)
+// Measured slower (profiles/r04g_sns_ab.txt): a prefetch of the next limb's points and of the accumulator
+// words (a barrier waits for every outstanding global load, so the requests only lengthened each pass), and
+// the next CMUX's step 1 fused into this kernel (staged words in LDS, each transform wave decomposing its
+// own 32 points: 242.4 vs 235.3 ms per 1024).
 __global__ void __launch_bounds__(ST, 3) sns_inv_kernel(const cd* __restrict__ O, u64* __restrict__ acc,
                                                         const SnsFftConst* __restrict__ Fc) {
   __shared__ cd buf[SF_M];
