@@ -196,7 +196,10 @@ __global__ void __launch_bounds__(ST) sns_step1f_kernel(const u64* __restrict__ 
 // slot stages its key tile once for all its groups.  The first group's digit spectra are requested before
 // the key tile is staged, so those loads overlap the LDS fill.
 constexpr int MAC_F = 16, MAC_CT = 32, MAC_JT = (SK + 1) * SF_LIMBS;  // 15 (output, limb) columns
-constexpr int MAC_SLOTS = 8;
+#ifndef SNS_MAC_SLOTS
+#define SNS_MAC_SLOTS 8  // 16 / 32 measured slower (profiles/r04g_sns_ab.txt)
+#endif
+constexpr int MAC_SLOTS = SNS_MAC_SLOTS;
 
 __device__ __forceinline__ void mac_load(const cd* __restrict__ Df, int c0, int B, int f0, int f, int cl,
                                          cd (&da)[SR], cd (&db)[SR]) {
@@ -277,7 +280,10 @@ __device__ __forceinline__ void fft_inv_reg(const cd* __restrict__ o, cd* buf, c
 // words (a barrier waits for every outstanding global load, so the requests only lengthened each pass), and
 // the next CMUX's step 1 fused into this kernel (staged words in LDS, each transform wave decomposing its
 // own 32 points: 242.4 vs 235.3 ms per 1024).
-__global__ void __launch_bounds__(ST, 3) sns_inv_kernel(const cd* __restrict__ O, u64* __restrict__ acc,
+#ifndef SNS_INV_OCC
+#define SNS_INV_OCC 3  // 4 spills (92 B) and runs 25 % slower
+#endif
+__global__ void __launch_bounds__(ST, SNS_INV_OCC) sns_inv_kernel(const cd* __restrict__ O, u64* __restrict__ acc,
                                                         const SnsFftConst* __restrict__ Fc) {
   __shared__ cd buf[SF_M];
   const int j = blockIdx.x % (SK + 1), ct = blockIdx.x / (SK + 1);
