@@ -16,4 +16,10 @@ TAG=${TAG} PRESET=gate_fft bash tools/profile_round.sh > gpurun_out/${TAG}_prof.
 tail -3 gpurun_out/${TAG}_prof.log
 TAG=${TAG}_fhevm PRESET=fhevm_fft bash tools/profile_round.sh > gpurun_out/${TAG}_fhevm_prof.log 2>&1 || { echo "fhevm profile failed"; tail -20 gpurun_out/${TAG}_fhevm_prof.log; exit 1; }
 tail -3 gpurun_out/${TAG}_fhevm_prof.log
+if [ "${EXTRA:-1}" = "1" ]; then  # C2 (batch 1024), the squash bench + kernel stats, C5 timed
+  timeout -k 10 300 python -u bench.py --batch 1024 --steps 10 --warmup 3 --no-cpu > gpurun_out/${TAG}_c2_bench.json 2> gpurun_out/${TAG}_c2_bench.err || { echo "C2 bench failed"; tail gpurun_out/${TAG}_c2_bench.err; exit 1; }
+  TAG=${TAG}_sns bash tools/gpu_sns_prof.sh > gpurun_out/${TAG}_sns_prof.log 2>&1 || { echo "squash profile failed"; tail gpurun_out/${TAG}_sns_prof.log; exit 1; }
+  timeout -k 10 300 python -u tools/c5_bench.py > gpurun_out/${TAG}_c5_bench.json 2> gpurun_out/${TAG}_c5_bench.err || { echo "C5 bench failed"; tail gpurun_out/${TAG}_c5_bench.err; exit 1; }
+  tail -c 300 gpurun_out/${TAG}_c2_bench.json; head -c 300 gpurun_out/${TAG}_c5_bench.json; echo
+fi
 echo FINAL_OK
