@@ -421,7 +421,9 @@ def g_select(cond: np.ndarray, x: np.ndarray, y: np.ndarray) -> Op:
     """cond ? x : y bitwise in ONE level: t = AND(cond, x), f = AND(NOT cond, y), and since at most one of
     them is true, OR(t, f) = t + f + 1/8 holds exactly on the phases (-1/8 - 1/8 + 1/8 = -1/8, 1/8 - 1/8 + 1/8
     = 1/8): the OR needs no bootstrap.  The result carries the noise of two PBS outputs, still far inside
-    the 1/8 decision margin of any gate it feeds."""
+    the 1/8 decision margin of any gate it feeds.  Invariant: every consumer bootstraps it -- a select output
+    never enters another non-bootstrapped linear combination (tests/test_gpu_select_noise.py measures the
+    worst consumers, MAJ and XOR / XOR3 of select outputs, against their margins)."""
     cw = _bcast(cond[:, None, :], x.shape)
     t, f = yield [AND(cw, x), _lin([(-1, cw), (1, y)], -MU)]      # AND(cw, x), AND(NOT cw, y)
     return OR(t, f)
