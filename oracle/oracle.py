@@ -467,7 +467,8 @@ class SnsKeys:
     @property
     def bsk_limb(self) -> np.ndarray:
         """The key as the blind rotation consumes it: rounded to multiples of 2^16 at load (or_sns_bsk_round,
-        as the device does), then the NTTs of its seven 16-bit limb polynomials (2.8 GB at n = 918)."""
+        as the device does), then its five limb polynomials: the low 48-bit limb as the device's f64 spectrum
+        (bits in the u64 words), the four 16-bit limbs as NTTs (2.0 GB at n = 918)."""
         if self._bsk_limb is None:
             rounded = np.zeros_like(self.bsk)
             lib().or_sns_bsk_round(ctypes.byref(self.sp), _p(self.bsk), _p(rounded))
