@@ -8,7 +8,7 @@
 //   X  two register exchanges: v_permlane32_swap (slot bit 3 <-> lane bit 5), v_permlane16_swap (slot bit 2 <->
 //      lane bit 4) -- 64 cross-lane moves, no LDS
 //   B  radix-4 over the two slot bits that arrived (l1 -> m0), then x *= tb[m0][l0] = e^{2 pi i l0 m0 / 64}
-//   T  ONE LDS transpose of lane bits 0..3 with the 4 slot bits (row strides 17 / 272 complex: conflict-free)
+//   T  ONE LDS transpose of lane bits 0..3 with the 4 slot bits (XOR-swizzled or padded rows: conflict-free)
 //   C  DFT16 over the slots (l0 -> m1)
 // Device order out: slot m1 of lane L holds Z[k], k = (L & 3) + 4 (L >> 4) + 16 ((L >> 2) & 3) + 64 m1.  The inverse
 // runs the stages reversed with conjugate twiddles (no 1/M).  Against the two-wave form it replaces (two 512-point
@@ -26,9 +26,50 @@ constexpr int M1 = 1024;
 constexpr double C16 = 0.92387953251128675613, S16 = 0.38268343236508977173;  // cos, sin (pi / 8)
 // table (complex, global memory and LDS): ta [16][64] | tb [4][16]
 constexpr int K_TA = 0, K_TB = 1024, K_C64 = 1088;
-// per-wave LDS area: transpose at hi * AH + s * AS + l0 (hi = lane >> 4, l0 = lane & 15); also the 2048-u64
-// rotation image and the spectra [slot][lane]
+// per-wave LDS area: the transpose's element (hi, s, l0) (hi = lane >> 4, slot s, l0 = lane & 15); also the
+// 2048-u64 rotation image and the spectra [slot][lane].  Row side: lane (hi, l0) touches (hi, s, l0), s = 0..15;
+// column side: lane (hi, l0) touches (hi, l0, c), c = 0..15.  Layouts (all conflict-free for every 16-lane group):
+// F1_SWZ = 2 (round 4 default) skewed 16 KB rows, 1 XOR-swizzled 16 KB rows, 0 rows padded to 17 complex (17 KB).
+// 16 KB areas let a 2-ciphertext workgroup fit twice per CU (80 KB).
+#ifndef F1_SWZ
+#define F1_SWZ 2
+#endif
+#if F1_SWZ == 2
+// skewed rows: element (hi, s, l0) at 256 hi + 16 s + ((l0 + s) & 15).  Row side (lane l0, s = 0..15) and column
+// side (lane = row s, c = 0..15) are each "one of two lane bases + an immediate": the wrap picks the base.
+constexpr int AREA_C64 = 1024;
+struct TAddr {
+  int w1, w2, r1, r2, l0;  // row side: w1 + 17 s (s < 16 - l0) or w2 + 17 s; column side: r1 + c or r2 + c
+  __device__ __forceinline__ TAddr(int lane) {
+    const int hi = lane >> 4;
+    l0 = lane & 15;
+    w1 = 256 * hi + l0;
+    w2 = w1 - 16;
+    r1 = 256 * hi + 17 * l0;
+    r2 = r1 - 16;
+  }
+  __device__ __forceinline__ int row(int s) const { return (s < 16 - l0 ? w1 : w2) + 17 * s; }
+  __device__ __forceinline__ int col(int c) const { return (c < 16 - l0 ? r1 : r2) + c; }
+};
+#elif F1_SWZ == 1
+// XOR rows: element (hi, s, l0) at 256 hi + 16 s + (l0 ^ s)
+constexpr int AREA_C64 = 1024;
+struct TAddr {
+  int hi, l0;
+  __device__ __forceinline__ TAddr(int lane) : hi(lane >> 4), l0(lane & 15) {}
+  __device__ __forceinline__ int row(int s) const { return 256 * hi + 16 * s + (l0 ^ s); }
+  __device__ __forceinline__ int col(int c) const { return 256 * hi + 16 * l0 + (c ^ l0); }
+};
+#else
+// padded rows of 17 complex (17 KB areas)
 constexpr int AS = 17, AH = 272, AREA_C64 = 4 * AH;
+struct TAddr {
+  int w, r;
+  __device__ __forceinline__ TAddr(int lane) : w(AH * (lane >> 4) + (lane & 15)), r(AH * (lane >> 4) + AS * (lane & 15)) {}
+  __device__ __forceinline__ int row(int s) const { return w + AS * s; }
+  __device__ __forceinline__ int col(int c) const { return r + c; }
+};
+#endif
 
 // cos / sin (2 pi t / m) evaluated at compile time with the host table generator's series (fftk::twiddle)
 namespace ctw16 {
@@ -152,14 +193,13 @@ __device__ __forceinline__ void fft1k_fwd(double (&xr)[16], double (&xi)[16], do
 #pragma unroll
     for (int m = 1; m < 4; m++) cmul<false>(xr[g + 4 * m], xi[g + 4 * m], tb.w[m]);
   }
-  double2* wp = area + (lane >> 4) * AH + (lane & 15);
+  const TAddr ad(lane);
 #pragma unroll
-  for (int s = 0; s < 16; s++) wp[s * AS] = make_double2(xr[s], xi[s]);
+  for (int s = 0; s < 16; s++) area[ad.row(s)] = make_double2(xr[s], xi[s]);
   lds_order();
-  const double2* rp = area + (lane >> 4) * AH + (lane & 15) * AS;
 #pragma unroll
   for (int r = 0; r < 16; r++) {
-    const double2 v = rp[r];
+    const double2 v = area[ad.col(r)];
     xr[r] = v.x;
     xi[r] = v.y;
   }
@@ -171,14 +211,13 @@ __device__ __forceinline__ void fft1k_fwd(double (&xr)[16], double (&xi)[16], do
 __device__ __forceinline__ void fft1k_inv(double (&xr)[16], double (&xi)[16], double2* area, int lane,
                                           const double2* ta, const TwB& tb) {
   dft16<true>(xr, xi);
-  double2* wp = area + (lane >> 4) * AH + (lane & 15) * AS;
+  const TAddr ad(lane);
 #pragma unroll
-  for (int r = 0; r < 16; r++) wp[r] = make_double2(xr[r], xi[r]);
+  for (int r = 0; r < 16; r++) area[ad.col(r)] = make_double2(xr[r], xi[r]);
   lds_order();
-  const double2* rp = area + (lane >> 4) * AH + (lane & 15);
 #pragma unroll
   for (int s = 0; s < 16; s++) {
-    const double2 v = rp[s * AS];
+    const double2 v = area[ad.row(s)];
     xr[s] = v.x;
     xi[s] = v.y;
   }

@@ -76,8 +76,10 @@ __device__ __forceinline__ void rotate_digits(const u64 (&v)[32], int a, int lan
   lds_order();
 }
 
-template <int CTS, bool WRITE_ACC, bool WRITE_BIG>
-__global__ __launch_bounds__(F1_THREADS, 1) void blind_rotate_fft2k_kernel(
+// NW waves per workgroup: 8 (the MAC spread over 8 waves, 2 slots each) or 2 CTS (every wave a transform wave,
+// 16 / NW slots each; with CTS = 2 and 16 KB areas two workgroups share a CU)
+template <int CTS, int NW, bool WRITE_ACC, bool WRITE_BIG>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
     const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
     int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tg, u64* __restrict__ out_big,
     u64* __restrict__ out_acc) {
@@ -114,20 +116,26 @@ __global__ __launch_bounds__(F1_THREADS, 1) void blind_rotate_fft2k_kernel(
   __syncthreads();
 
   int a_next = tw_wave ? ms4096(ct[0]) : 0;
-  const int s0 = 2 * wave_s;  // MAC slots s0, s0 + 1
+  constexpr int SPW = 16 / NW;  // MAC slots per wave
+  static_assert(NW == 8 || NW == 2 * CTS, "waves: 8, or one per polynomial");
+  const int s0 = SPW * wave_s;  // MAC slots s0 .. s0 + SPW - 1
 #if F1_PRIO
   if (wave_s >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
-  // key words of CMUX i for the MAC phase: kv[t][cc][j] = K_{cc,j}[slot s0 + t][lane]
-  auto load_key = [&](int i, double2 (&kv)[2][2][2]) {
+  // key words of CMUX i for the MAC phase: kv[t][cc][j] = K_{cc,j}[slot s0 + t][lane].  The first KPRE slots are
+  // requested at the CMUX start (their latency hides behind the forward transform); with 4 slots per wave the
+  // other two are requested when the MAC phase starts (holding all four across the transform spills).
+  constexpr int KPRE = SPW < 2 ? SPW : 2;
+  auto load_key = [&](int i, double2 (&kv)[SPW][2][2], bool late) {
 #pragma unroll
-    for (int t = 0; t < 2; t++)
+    for (int t = 0; t < SPW; t++)
+      if ((t >= KPRE) == late)
 #pragma unroll
-      for (int cc = 0; cc < 2; cc++)
+        for (int cc = 0; cc < 2; cc++)
 #pragma unroll
-        for (int j = 0; j < 2; j++) kv[t][cc][j] = bsk[((size_t)(i * 2 + cc) * 2 + j) * M1 + 64 * (s0 + t) + lane];
+          for (int j = 0; j < 2; j++) kv[t][cc][j] = bsk[((size_t)(i * 2 + cc) * 2 + j) * M1 + 64 * (s0 + t) + lane];
   };
-  auto cmux = [&](int i, const double2 (&kv)[2][2][2]) {
+  auto cmux = [&](int i, double2 (&kv)[SPW][2][2]) {
     const int a = a_next;
     if (tw_wave && i + 1 < n) a_next = ms4096(ct[i + 1]);
     if (tw_wave) {
@@ -138,10 +146,11 @@ __global__ __launch_bounds__(F1_THREADS, 1) void blind_rotate_fft2k_kernel(
       for (int s = 0; s < 16; s++) area[64 * s + lane] = make_double2(xr[s], xi[s]);
     }
     __syncthreads();
+    if constexpr (SPW > KPRE) load_key(i, kv, true);
 #pragma unroll
     for (int q = 0; q < CTS; q++) {
 #pragma unroll
-      for (int t = 0; t < 2; t++) {
+      for (int t = 0; t < SPW; t++) {
         const int idx = 64 * (s0 + t) + lane;
         const double2 d0 = sh.area[2 * q][idx], d1 = sh.area[2 * q + 1][idx];
         double2 o[2];
@@ -180,19 +189,19 @@ __global__ __launch_bounds__(F1_THREADS, 1) void blind_rotate_fft2k_kernel(
     }
   };
 #if F1_KPF
-  double2 kva[2][2][2], kvb[2][2][2];  // one CMUX ahead
-  load_key(0, kva);
+  double2 kva[SPW][2][2], kvb[SPW][2][2];  // one CMUX ahead
+  load_key(0, kva, false);
   for (int i = 0; i < n; i += 2) {
-    if (i + 1 < n) load_key(i + 1, kvb);
+    if (i + 1 < n) load_key(i + 1, kvb, false);
     cmux(i, kva);
     if (i + 1 >= n) break;
-    if (i + 2 < n) load_key(i + 2, kva);
+    if (i + 2 < n) load_key(i + 2, kva, false);
     cmux(i + 1, kvb);
   }
 #else
   for (int i = 0; i < n; i++) {
-    double2 kv[2][2][2];  // requested at the CMUX start, consumed after the rotation and forward transform
-    load_key(i, kv);
+    double2 kv[SPW][2][2];  // requested at the CMUX start, consumed after the rotation and forward transform
+    load_key(i, kv, false);
     cmux(i, kv);
   }
 #endif
@@ -335,32 +344,40 @@ hipError_t launch_fft2k_inv(const double* in, size_t count, double* out, const d
   return hipGetLastError();
 }
 
-template <int CTS>
+template <int CTS, int NW>
 static hipError_t launch_br2k(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index, int n_lut,
                               const double2* bk, const double2* t, u64* out_big, u64* out_acc, hipStream_t s) {
   using namespace fft1k;
-  dim3 grid((unsigned)((B + CTS - 1) / CTS)), block(F1_THREADS);
+  dim3 grid((unsigned)((B + CTS - 1) / CTS)), block(64 * NW);
   if (out_acc && out_big)
-    hipLaunchKernelGGL((blind_rotate_fft2k_kernel<CTS, true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
-                       n_lut, bk, t, out_big, out_acc);
+    hipLaunchKernelGGL((blind_rotate_fft2k_kernel<CTS, NW, true, true>), grid, block, 0, s, lwe_in, n, B, luts,
+                       lut_index, n_lut, bk, t, out_big, out_acc);
   else if (out_acc)
-    hipLaunchKernelGGL((blind_rotate_fft2k_kernel<CTS, true, false>), grid, block, 0, s, lwe_in, n, B, luts,
+    hipLaunchKernelGGL((blind_rotate_fft2k_kernel<CTS, NW, true, false>), grid, block, 0, s, lwe_in, n, B, luts,
                        lut_index, n_lut, bk, t, out_big, out_acc);
   else
-    hipLaunchKernelGGL((blind_rotate_fft2k_kernel<CTS, false, true>), grid, block, 0, s, lwe_in, n, B, luts,
+    hipLaunchKernelGGL((blind_rotate_fft2k_kernel<CTS, NW, false, true>), grid, block, 0, s, lwe_in, n, B, luts,
                        lut_index, n_lut, bk, t, out_big, out_acc);
   return hipGetLastError();
 }
 
 // batches up to latency_max_batch: two ciphertexts per workgroup (four transform waves on four SIMDs, eight MAC
-// waves); larger batches: four per workgroup (two transform waves per SIMD)
+// waves); larger batches: F1_BATCH2 = 1 two per workgroup of four waves, two workgroups per CU (16 KB areas);
+// 0: four per workgroup of eight waves (two transform waves per SIMD)
+#ifndef F1_BATCH2
+#define F1_BATCH2 1
+#endif
 hipError_t launch_blind_rotate_fft2k(const u64* lwe_in, size_t B, int n, const u64* luts, const u32* lut_index,
                                      int n_lut, const double* bsk_f, const double* tw, u64* out_big, u64* out_acc,
                                      hipStream_t s, size_t latency_max_batch) {
   if (B == 0) return hipSuccess;
   const double2 *bk = (const double2*)bsk_f, *t = (const double2*)tw;
-  if (B <= latency_max_batch) return launch_br2k<2>(lwe_in, B, n, luts, lut_index, n_lut, bk, t, out_big, out_acc, s);
-  return launch_br2k<4>(lwe_in, B, n, luts, lut_index, n_lut, bk, t, out_big, out_acc, s);
+  if (B <= latency_max_batch) return launch_br2k<2, 8>(lwe_in, B, n, luts, lut_index, n_lut, bk, t, out_big, out_acc, s);
+#if F1_BATCH2 && F1_SWZ != 0
+  return launch_br2k<2, 4>(lwe_in, B, n, luts, lut_index, n_lut, bk, t, out_big, out_acc, s);
+#else
+  return launch_br2k<4, 8>(lwe_in, B, n, luts, lut_index, n_lut, bk, t, out_big, out_acc, s);
+#endif
 }
 
 }  // namespace tfhe
