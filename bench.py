@@ -374,10 +374,13 @@ def main() -> int:
             "roofline": dict(roofline(args.preset, br_kernel, B, br_avg, br_bytes,
                                       bsk_bytes + B * 8 * ((pd["n"] + 1) + (pd["k"] * pd["N"] + 1))),
                              # the reuse the kernel implements and the true minimum traffic
-                             bsk_reuse=(f"each BSK level-step chunk is streamed once per workgroup into LDS and shared "
-                                        f"by its {dict(gate=8, gate_fft=2).get(args.preset, 4)} ciphertexts; resident workgroups share it through L2"
-                                        if "lat" not in br_kernel else
-                                        "latency kernel: one ciphertext per workgroup, key words from L2"),
+                             bsk_reuse=("latency kernel: one ciphertext per workgroup, key words from L2"
+                                        if "lat" in br_kernel else
+                                        "each CMUX's key words are read from L2 into registers once per workgroup and "
+                                        "shared by its 2 ciphertexts (two workgroups per CU)"
+                                        if args.preset == "fhevm_fft" else
+                                        f"each BSK level-step chunk is streamed once per workgroup into LDS and shared "
+                                        f"by its {dict(gate=8, gate_fft=2).get(args.preset, 4)} ciphertexts; resident workgroups share it through L2"),
                              min_traffic_bytes_per_pbs=round((bsk_bytes + ksk_bytes) / B + io_bytes),
                              launches=br_n),
             "keyswitch_ms": round(ks_ms / max(ks_n, 1), 3),

@@ -1,23 +1,27 @@
 // pbs_fft2k.hip — P-FHEVM (N = 2048, k = 1, PBS 2^23 x 1) blind rotation with ONE wave per polynomial component
 // (round 4): the 1024-point transform of fft1k.h, restated in oracle/fft_oracle.c (fft1k_fwd / fft1k_inv).
 //
-// Workgroup = 8 waves, CTS ciphertexts (4 in the batch kernel, 2 in latency mode); waves w < 2 CTS are the transform
-// waves (p, c) = (w >> 1, w & 1), each holding component c of ciphertext p (2048 u64 = 32 per lane, registers).
+// Batch mode (round 4): workgroup = 4 waves = 2 ciphertexts x 2 components, TWO workgroups per CU (80 KB of LDS
+// each: the 16 KB pass-A table + 4 skewed 16 KB areas, fft1k.h), so the barriers of one workgroup overlap the other's
+// work; latency mode: 8 waves, CTS = 2 (below).  Waves w < 2 CTS are the transform waves (p, c) = (w >> 1, w & 1),
+// each holding component c of ciphertext p (2048 u64 = 32 per lane, registers).
 // Per CMUX i:
 //   transform waves: (X^a acc_c - acc_c) through the wave's LDS area (rotation by DS offsets), 23-bit digits, the
 //     forward transform (one LDS transpose), the spectrum D_c stored to the area [slot][lane]
 //   barrier
-//   MAC, all 8 waves: wave w owns slots 2w, 2w + 1 of every ciphertext of the workgroup,
+//   MAC, all waves: wave w owns 16 / NW slots of every ciphertext of the workgroup,
 //     O_j = D_0 (.) K_{0,j} + D_1 (.) K_{1,j}  (the oracle's fma chain from (0, 0), c = 0 first)
-//     with the key words of those slots in registers (requested at the CMUX start: 8 complex per wave, shared by
-//     the CTS ciphertexts), O_j written over D_j in the areas
+//     with the key words of those slots in registers (two slots requested at the CMUX start, the others when the
+//     MAC starts; shared by the CTS ciphertexts), O_j written over D_j in the areas
 //   barrier
 //   transform waves: O_c from the own area, the inverse transform, acc_c += rint mod 2^64 (two-split form: the
 //     23-bit digits give |x| up to 2^106)
 // Two barriers per CMUX (the round-1..3 two-wave kernel had five to six: 512-point halves + a combine exchange per
 // transform) and no wave waits for a partner mid-transform.  In latency mode (CTS = 2: four transform waves, one per
-// SIMD, and four MAC-only waves) a workgroup takes two ciphertexts at the per-CMUX latency of one.  LDS (CTS = 4): pass A table 16 KB (first, so an area's base minus 16 KB stays inside the block for
-// the rotation's wrapped reads) | 8 areas x 17 KB = 152 KB.
+// SIMD, and four MAC-only waves) a workgroup takes two ciphertexts at the per-CMUX latency of one.  LDS: pass A table
+// 16 KB (first, so an area's base minus 16 KB stays inside the block for the rotation's wrapped reads) | 2 CTS areas
+// x 16 KB.  (Rounds 1-3 / early round 4: 4 ciphertexts x 8 waves, 8 padded 17 KB areas = 152 KB, one workgroup per CU:
+// 45.8 ms per 4096 against 44.4 ms now, profiles/r04i_fhevm_2wg_ab.txt.)
 #include "fft1k.h"
 #include "pbs_kernels.h"
 
