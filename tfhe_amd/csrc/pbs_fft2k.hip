@@ -29,7 +29,6 @@ namespace tfhe {
 namespace fft1k {
 
 constexpr int N2 = 2048;
-constexpr int F1_THREADS = 512;  // 8 waves
 
 __device__ __forceinline__ int ms4096(u64 x) { return (int)((((x >> 51) + 1) >> 1) & 4095u); }
 // tfhe-rs SignedDecomposer 2^23 x 1 on the high word (pbs_fft2k.hip: decomp_23x1_hi; tests/test_fft.py)
