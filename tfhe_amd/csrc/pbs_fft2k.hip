@@ -40,8 +40,13 @@ typedef __attribute__((address_space(3))) u64 lds_u64;
 #ifndef F1_KPF
 #define F1_KPF 0
 #endif
+// F1_PRIO 3 (default since late round 4): in the two-workgroup batch kernel the workgroups of the second dispatch
+// half (blockIdx bit 8: with 256 CUs, the second workgroup each CU receives first) run at the higher wave
+// priority, so the two workgroups of a CU drift apart instead of reaching their barriers together:
+// 44.24 -> 43.35 ms per 4096 on the same box (profiles/r04i_fhevm_2wg_ab.txt).  1: the MAC-only waves of the
+// 8-wave form; 0: none.
 #ifndef F1_PRIO
-#define F1_PRIO 0
+#define F1_PRIO 3
 #endif
 
 template <int CTS>
@@ -122,8 +127,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
   constexpr int SPW = 16 / NW;  // MAC slots per wave
   static_assert(NW == 8 || NW == 2 * CTS, "waves: 8, or one per polynomial");
   const int s0 = SPW * wave_s;  // MAC slots s0 .. s0 + SPW - 1
-#if F1_PRIO
+#if F1_PRIO == 1
   if (wave_s >= 4) __builtin_amdgcn_s_setprio(1);
+#elif F1_PRIO == 3
+  if constexpr (NW == 2 * CTS)
+    if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_setprio(1);
 #endif
   // key words of CMUX i for the MAC phase: kv[t][cc][j] = K_{cc,j}[slot s0 + t][lane].  The first KPRE slots are
   // requested at the CMUX start (their latency hides behind the forward transform); with 4 slots per wave the
