@@ -21,7 +21,8 @@
 // SIMD, and four MAC-only waves) a workgroup takes two ciphertexts at the per-CMUX latency of one.  LDS: pass A table
 // 16 KB (first, so an area's base minus 16 KB stays inside the block for the rotation's wrapped reads) | 2 CTS areas
 // x 16 KB.  (Rounds 1-3 / early round 4: 4 ciphertexts x 8 waves, 8 padded 17 KB areas = 152 KB, one workgroup per CU:
-// 45.8 ms per 4096 against 44.4 ms now, profiles/r04i_fhevm_2wg_ab.txt.)
+// 45.8 ms per 4096; two workgroups per CU 44.4 ms, with the priority scheme below 42.8 ms,
+// profiles/r04i_fhevm_2wg_ab.txt.)
 #include "fft1k.h"
 #include "pbs_kernels.h"
 
@@ -47,6 +48,12 @@ typedef __attribute__((address_space(3))) u64 lds_u64;
 // 8-wave form; 0: none.
 #ifndef F1_PRIO
 #define F1_PRIO 3
+#endif
+// F1_MACPRIO 1 (default): every wave runs the short MAC phase at the top priority and then returns to its
+// workgroup's F1_PRIO level, so a CU's MAC phases are not stalled behind the other workgroup's transforms:
+// 43.43 -> 42.77 ms per 4096 on the same box (profiles/r04i_fhevm_2wg_ab.txt)
+#ifndef F1_MACPRIO
+#define F1_MACPRIO 1
 #endif
 
 template <int CTS>
@@ -160,6 +167,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
     // latency overlaps the wait (+0.3-0.5 %, profiles/r04i_fhevm_2wg_ab.txt)
     if constexpr (SPW > KPRE) load_key(i, kv, true);
     __syncthreads();
+#if F1_MACPRIO
+    __builtin_amdgcn_s_setprio(3);  // the short MAC phase ahead of the other workgroup's transforms
+#endif
 #pragma unroll
     for (int q = 0; q < CTS; q++) {
 #pragma unroll
@@ -185,6 +195,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
       }
     }
     __syncthreads();
+#if F1_MACPRIO  // back to the workgroup's level (F1_PRIO)
+    if (F1_PRIO == 3 && NW == 2 * CTS && ((blockIdx.x >> 8) & 1)) __builtin_amdgcn_s_setprio(1);
+    else if (F1_PRIO == 1 && wave_s >= 4) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#endif
     if (tw_wave) {
       double xr[16], xi[16];
 #pragma unroll
