@@ -202,6 +202,13 @@ struct FpShared<2> {
 #ifndef FFT_PAIR_CTS
 #define FFT_PAIR_CTS 2
 #endif
+// FFT_MACPRIO 1 (default since late round 4): each level step's MAC runs at the top wave priority (back to 0
+// when the next step starts and after the last), so the short MAC phase of one workgroup is not stalled behind
+// the other workgroup's transforms on the same SIMD: 26.62 -> 25.26 ms per 4096 on the same box, 152.2k ->
+// 160.4k PBS/s (profiles/r04k_pgate_macprio_ab.txt)
+#ifndef FFT_MACPRIO
+#define FFT_MACPRIO 1
+#endif
 typedef __attribute__((address_space(3))) u64 lds_u64;
 
 // (X^a v - v), v = this wave's polynomial (slot e <-> coefficient 64 e + L), to decomposition states.  The
@@ -367,6 +374,9 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
     auto level = [&](auto qc) {
       constexpr int q = decltype(qc)::value;
       const int g = 3 * i + q;
+#if FFT_MACPRIO
+      if (q > 0) __builtin_amdgcn_s_setprio(0);
+#endif
       if constexpr (LDS_TW) {
         glds_barrier();  // step g's chunk is in K[g & 1]; every wave is done with K[(g + 1) & 1]
         if (g + 1 < n_steps) load_step<NW>(bsk, g + 1, sh.K[(g + 1) & 1], wave_s, lane);
@@ -395,6 +405,9 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
       dft512_fwd_t<true>(xr, xi, T, lane, tb, twA, twB);
 #endif
       if constexpr (!LDS_TW) glds_barrier();  // step g's chunk has landed
+#if FFT_MACPRIO
+      __builtin_amdgcn_s_setprio(3);  // the short MAC ahead of the other workgroup's transforms
+#endif
       const double2* k0 = sh.K[LDS_TW ? (g & 1) : 0] + c * (2 * M) + lane;
       const double2* k1 = k0 + M;
 #pragma unroll
@@ -412,6 +425,9 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
     level(std::integral_constant<int, 0>{});
     level(std::integral_constant<int, 1>{});
     level(std::integral_constant<int, 2>{});
+#if FFT_MACPRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     // exchange the partial sums: publish O_(1-c)^c, take O_c^(1-c) (c wave-uniform: a scalar branch, no selects)
     double xr[8], xi[8];
     if (c_s) exchange_partials<1>(o0r, o0i, o1r, o1i, xr, xi, T, Tp, lane);
