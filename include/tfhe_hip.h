@@ -114,7 +114,9 @@ int tfhe_hip_ms_zeros_keygen(const tfhe_params* p, uint64_t seed, const uint64_t
  * 128-bit seed (seed[0] = low 64 bits) restated from tfhe-csprng (tfhe_amd/csrc/seeded.cpp has the byte order);
  * bodies are in tfhe-rs order:
  *   BSK bodies [i < n][l < L][c <= k][N]   (GGSW i, decomposition level l most significant first, GLWE row c)
- *   KSK bodies [j < k N][l < ks_level]     (input key element j; P-FHEVM: big key -> small key)
+ *   KSK bodies [j < k N][s < ks_level]     (input key element j, storage row s = decomposition level ks_level - s:
+ *                                           least significant first, as tfhe-rs's keygen walks (1..=levels).rev();
+ *                                           engine KSK row ks_level - 1 - s; P-FHEVM: big key -> small key)
  *   list bodies [z < count]                (e.g. the modulus-switch zeros)
  * Decompressed keys land in this engine's standard layouts (tfhe_hip_load_keys, tfhe_hip_load_ms_key).  FFT64
  * presets only (native 2^64 torus).  PARITY UNPINNED at the byte level: the reference holds no server-key file. */

@@ -430,8 +430,10 @@ static void monomial_torus(uint64_t* out, const uint64_t* in, uint32_t N, uint32
   }
 }
 
-void or_blind_rotate_fft(const or_params* p, const or_c64* bsk_f, const uint64_t* lwe_in, const uint64_t* lut,
-                         uint64_t* acc) {
+/* trace (nullable): (n + 1) x (k+1)N words, the accumulator before CMUX 0 and after every CMUX i (skipped CMUXes
+ * included), so tests can hand each state to the exact arbiter (exact_oracle.c) */
+static void blind_rotate_fft_impl(const or_params* p, const or_c64* bsk_f, const uint64_t* lwe_in, const uint64_t* lut,
+                                  uint64_t* acc, uint64_t* trace) {
   const uint32_t N = p->N, M = N / 2, k = p->k, L = p->pbs_level, n = p->n;
   if (k != 1 || (N != 2 * FFT_M && N != 4 * FFT_M) || L > 8) abort();
   const size_t per_i = (size_t)(k + 1) * L * (k + 1) * M;
@@ -448,9 +450,14 @@ void or_blind_rotate_fft(const or_params* p, const or_c64* bsk_f, const uint64_t
   const int split = N == 2 * FFT_M;
   double res[4 * FFT_M];
   int64_t d[64];
+  const size_t row = (size_t)(k + 1) * N;
+  if (trace) memcpy(trace, acc, row * 8);
   for (uint32_t i = 0; i < n; i++) {
     const uint32_t a = or_mod_switch(lwe_in[i], 2 * N);
-    if (a == 0) continue; /* (X^0 - 1) acc == 0: every double stays +-0, rounds to 0 */
+    if (a == 0) { /* (X^0 - 1) acc == 0: every double stays +-0, rounds to 0 */
+      if (trace) memcpy(trace + (i + 1) * row, acc, row * 8);
+      continue;
+    }
     memset(O, 0, sizeof(O));
     for (uint32_t c = 0; c <= k; c++) {
       monomial_torus(rot, acc + (size_t)c * N, N, a);
@@ -499,7 +506,20 @@ void or_blind_rotate_fft(const or_params* p, const or_c64* bsk_f, const uint64_t
       or_fft_inv(O[j], N, res);
       for (uint32_t f = 0; f < N; f++) acc[(size_t)j * N + f] += or_f64_to_torus(res[f]);
     }
+    if (trace) memcpy(trace + (i + 1) * row, acc, row * 8);
   }
+}
+
+void or_blind_rotate_fft(const or_params* p, const or_c64* bsk_f, const uint64_t* lwe_in, const uint64_t* lut,
+                         uint64_t* acc) {
+  blind_rotate_fft_impl(p, bsk_f, lwe_in, lut, acc, NULL);
+}
+
+void or_blind_rotate_fft_trace(const or_params* p, const or_c64* bsk_f, const uint64_t* lwe_in, const uint64_t* lut,
+                               uint64_t* trace) {
+  uint64_t* acc = (uint64_t*)malloc((size_t)(p->k + 1) * p->N * 8);
+  blind_rotate_fft_impl(p, bsk_f, lwe_in, lut, acc, trace);
+  free(acc);
 }
 
 void or_sample_extract_torus(const or_params* p, const uint64_t* acc, uint64_t* out) {

@@ -517,3 +517,71 @@ def sns_ntt(which: int, a: np.ndarray, inverse: bool = False) -> np.ndarray:
     f = lib().or_sns_ntt_inv if inverse else lib().or_sns_ntt_fwd
     f(ctypes.c_int(which), _p(a), ctypes.c_uint32(a.size))
     return a
+
+
+# ---- exact integer arithmetic over Z_2^64 (exact_oracle.c): the arbiter of the FFT64 path --------------------
+def poly_mul_torus_exact(a_small, b) -> np.ndarray:
+    """The limb / Goldilocks-NTT exact wrapping product (or_poly_mul_torus_exact)."""
+    a = np.ascontiguousarray(a_small, dtype=np.int64)
+    b = np.ascontiguousarray(b, dtype=np.uint64)
+    out = np.zeros(b.shape[0], dtype=np.uint64)
+    lib().or_poly_mul_torus_exact(_p(out), _p(a, I64P), _p(b), ctypes.c_uint32(b.shape[0]))
+    return out
+
+
+class ExactKey:
+    """or_exact_key: the standard-domain torus BSK as NTT-domain limb polynomials (3 x the BSK's size)."""
+
+    def __init__(self, prm: Params, bsk: np.ndarray):
+        L = lib()
+        L.or_exact_key_new.restype = ctypes.c_void_p
+        L.or_exact_key_free.argtypes = [ctypes.c_void_p]
+        self.prm = prm
+        self._bsk = np.ascontiguousarray(bsk, dtype=np.uint64)
+        self.h = L.or_exact_key_new(ctypes.byref(prm), _p(self._bsk))
+        assert self.h, "or_exact_key_new refused the parameters"
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_exact_key_free(ctypes.c_void_p(self.h))
+            self.h = None
+
+    def cmux(self, key_index, a_tilde, acc_in, threads: int = 0):
+        """-> (acc_out, s1, s2): acc_out[q] = acc_in[q] + ExtProd(BSK_i, X^a acc - acc) exactly, with the norm sums of
+        the FFT error bound (s1 = sum_r ||d_r|| ||w_r||, s2 = sum_r ||d_r||^2 ||w_r||^2, per output column)."""
+        prm = self.prm
+        row = (prm.k + 1) * prm.N
+        acc_in = np.ascontiguousarray(acc_in, dtype=np.uint64).reshape(-1, row)
+        cnt = acc_in.shape[0]
+        ki = np.ascontiguousarray(np.broadcast_to(np.asarray(key_index, dtype=np.uint32), (cnt,)))
+        at = np.ascontiguousarray(np.broadcast_to(np.asarray(a_tilde, dtype=np.uint32), (cnt,)))
+        assert int(ki.max(initial=0)) < prm.n and int(at.max(initial=0)) < 2 * prm.N
+        out = np.zeros_like(acc_in)
+        s1 = np.zeros((cnt, prm.k + 1), dtype=np.float64)
+        s2 = np.zeros((cnt, prm.k + 1), dtype=np.float64)
+        lib().or_cmux_exact_batch(ctypes.c_void_p(self.h), ctypes.c_size_t(cnt), _p(ki, U32P), _p(at, U32P),
+                                  _p(acc_in), _p(out), _p(s1, ctypes.c_void_p), _p(s2, ctypes.c_void_p),
+                                  ctypes.c_int(threads))
+        return out, s1, s2
+
+    def blind_rotate(self, lwe_in: np.ndarray, lut: np.ndarray) -> np.ndarray:
+        acc = np.zeros((self.prm.k + 1) * self.prm.N, dtype=np.uint64)
+        lib().or_blind_rotate_exact(ctypes.c_void_p(self.h), _p(np.ascontiguousarray(lwe_in, dtype=np.uint64)),
+                                    _p(np.ascontiguousarray(lut, dtype=np.uint64)), _p(acc))
+        return acc
+
+
+def blind_rotate_fft_trace(prm: Params, keys: Keys, lwe_in: np.ndarray, lut: np.ndarray) -> np.ndarray:
+    """(n + 1) x (k+1)N: the FFT64 oracle's accumulator before CMUX 0 and after each CMUX."""
+    tr = np.zeros((prm.n + 1, (prm.k + 1) * prm.N), dtype=np.uint64)
+    lib().or_blind_rotate_fft_trace(ctypes.byref(prm), _p(keys.bsk_fourier, ctypes.c_void_p),
+                                    _p(np.ascontiguousarray(lwe_in, dtype=np.uint64)),
+                                    _p(np.ascontiguousarray(lut, dtype=np.uint64)), _p(tr))
+    return tr
+
+
+def mod_switch(x, two_n: int) -> np.ndarray:
+    """round(x 2N / 2^64) mod 2N (or_mod_switch), vectorised."""
+    x = np.asarray(x, dtype=np.uint64)
+    lg = int(two_n).bit_length() - 1
+    return ((((x >> np.uint64(64 - lg - 1)) + np.uint64(1)) >> np.uint64(1)) & np.uint64(two_n - 1)).astype(np.uint32)

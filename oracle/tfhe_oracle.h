@@ -259,6 +259,24 @@ void or_pbs_batch_fft_ex(const or_params* p, const or_c64* bsk_f, const uint64_t
                          const uint32_t* lut_index, uint64_t* lwe_out, int threads);
 /* exact negacyclic product over Z_2^64 (wrapping): the independent arbiter of the FFT's rounding */
 void or_poly_mul_torus_schoolbook(uint64_t* out, const int64_t* a, const uint64_t* b, uint32_t N);
+/* the FFT64 blind rotation with every intermediate accumulator: trace = (n + 1) x (k+1)N words, row 0 the initial
+ * X^{-b~} LUT, row i + 1 the state after CMUX i */
+void or_blind_rotate_fft_trace(const or_params* p, const or_c64* bsk_f, const uint64_t* lwe_in, const uint64_t* lut,
+                               uint64_t* trace);
+
+/* ---- exact integer arithmetic over Z_2^64 (exact_oracle.c): the arbiter of the FFT64 path -----------------
+ * The external product computed with no floating point: BSK words split into three balanced base-2^22 limbs, each
+ * digit x limb product exact through the Goldilocks NTT (|value| <= 2^55 < p/2), recombined mod 2^64.  Equal to the
+ * reference's polynomial_wrapping_mul (ml/extensions/rust/src/computations.rs:50-54) by construction. */
+typedef struct or_exact_key or_exact_key;
+or_exact_key* or_exact_key_new(const or_params* p, const uint64_t* bsk /* standard-domain torus BSK */);
+void or_exact_key_free(or_exact_key* K);
+/* acc_out[q] = acc_in[q] + ExtProd(BSK_{key_index[q]}, X^{a_tilde[q]} acc_in[q] - acc_in[q]) for q < count.
+ * s1, s2 (nullable, count x (k+1)): sum_r ||d_r|| ||w_{r,j}|| and sum_r ||d_r||^2 ||w_{r,j}||^2 (w as signed int64) */
+void or_cmux_exact_batch(const or_exact_key* K, size_t count, const uint32_t* key_index, const uint32_t* a_tilde,
+                         const uint64_t* acc_in, uint64_t* acc_out, double* s1, double* s2, int threads);
+void or_poly_mul_torus_exact(uint64_t* out, const int64_t* a, const uint64_t* b, uint32_t N);
+void or_blind_rotate_exact(const or_exact_key* K, const uint64_t* lwe_in, const uint64_t* lut, uint64_t* acc);
 
 /* ---- LUT helpers --------------------------------------------------------------------- */
 void or_lut_constant(uint32_t N, uint64_t torus_value, uint64_t* lut); /* gate LUT: every coef = v */

@@ -128,3 +128,21 @@ def test_blind_rotate_ntt_equals_schoolbook_small(oracle_mod):
     a = O.blind_rotate(prm, keys, ct, lut, schoolbook=False)
     b = O.blind_rotate(prm, keys, ct, lut, schoolbook=True)
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("name", ["fft64_gate.npz", "fft64_fhevm.npz"])
+def test_golden_fft64(oracle_mod, name):
+    """The FFT64 oracle (fft_oracle.c, the device's bit-exact twin) against its committed fixtures
+    (tests/golden/make_golden_fft64.py): a lockstep edit of kernel and oracle changes these bytes."""
+    g = load_golden(name)
+    prm = oracle_mod.params(int(g["preset"]))
+    keys = oracle_mod.Keys(prm, int(g["key_seed"]))
+    bri = g["small"] if "small" in g else g["lwe_in"]
+    if "small" in g:
+        for i in range(bri.shape[0]):
+            assert np.array_equal(oracle_mod.keyswitch(prm, keys, g["lwe_in"][i]), bri[i])
+    for i in range(bri.shape[0]):
+        acc = oracle_mod.blind_rotate_fft(prm, keys, bri[i], g["luts"][g["lut_index"][i]])
+        assert np.array_equal(acc, g["acc"][i]), f"{name}: accumulator {i} drifted"
+    out = oracle_mod.pbs_batch_fft(prm, keys, g["lwe_in"], g["luts"], g["lut_index"])
+    assert np.array_equal(out, g["lwe_out"]), f"{name}: PBS output drifted"

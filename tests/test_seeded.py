@@ -79,6 +79,8 @@ def _rows_decrypt(p, ck, sk, csk, rows=((0, 0), (1, 0), (5, 1), (629, 1)), tol_l
             with np.errstate(over="ignore"):
                 ph = b - np.sum(a * ck.lwe_key, dtype=np.uint64) - (ck.glwe_key[j] << np.uint64(64 - p.ks_base_log * (l + 1)))
             assert abs(int(np.int64(ph.view(np.int64)))) < 2 ** (tol_log2 + 8)
+            # tfhe-rs stores a keyswitch block least significant level first: storage row s = engine row L - 1 - s
+            assert int(b) == int(csk.ksk_bodies[j, p.ks_level - 1 - l]), (j, l)
 
 
 @pytest.fixture(scope="module")

@@ -14,7 +14,11 @@
 //   native-modulus mask element is the next 8 bytes, little endian.  Forks hand out consecutive byte ranges, so
 //   the masks of a whole key are one contiguous run of the stream in the order the encryption walks them:
 //     bootstrapping key   GGSW i < n, level l < L (most significant first), row c <= k: k*N mask words
-//     keyswitching key    input key element j < k*N, level l: n mask words
+//     keyswitching key    input key element j < k*N, storage row s < ks_level: n mask words, where storage row s
+//                         holds decomposition level ks_level - s (tfhe-rs generate_lwe_keyswitch_key walks the
+//                         levels (1..=level_count).rev(), least significant first, so a block lines up with the
+//                         SignedDecomposer's low-to-high digit iterator); this engine's KSK row l is level l + 1
+//                         (most significant first), so storage row s <-> engine row ks_level - 1 - s
 //     ciphertext list     ciphertext z: dim mask words
 // A GGSW row c < k of tfhe-rs encrypts -m*g*S_c and row k encrypts m*g (g = 2^(64 - beta (l + 1))); this engine's
 // keygen adds m*g to mask c of an encryption of zero instead.  Both have the same phase, which is all the external
@@ -215,10 +219,10 @@ void seeded_server_keygen(const tfhe_params& p, const tfhe_rng_key& rk, const ui
       std::vector<uint64_t> mask(n);
       std::vector<int64_t> e(p.ks_level);
       client::noise_words(rk, 0x100000 + (uint64_t)j, p.lwe_noise_log2, e.size(), e.data());
-      for (uint32_t l = 0; l < p.ks_level; l++) {
-        const size_t row = (size_t)j * p.ks_level + l;
+      for (uint32_t s = 0; s < p.ks_level; s++) {  // storage row s = engine level ks_level - 1 - s
+        const size_t row = (size_t)j * p.ks_level + s;
         mask_words(aes, row * n, n, mask.data());
-        uint64_t acc = (uint64_t)e[l] + (glwe_key[j] << (64 - p.ks_base_log * (l + 1)));
+        uint64_t acc = (uint64_t)e[s] + (glwe_key[j] << (64 - p.ks_base_log * (p.ks_level - s)));
         for (uint32_t t = 0; t < n; t++) acc += mask[t] * lwe_key[t];
         ksk_bodies[row] = acc;
       }
@@ -265,9 +269,9 @@ void decompress_ksk(const tfhe_params& p, const uint64_t seed[2], const uint64_t
   key_bytes(seed, key);
   const Aes128 aes(key);
   parallel_for((int64_t)p.k * p.N, [&](int64_t j) {
-    for (uint32_t l = 0; l < p.ks_level; l++) {
-      const size_t row = (size_t)j * p.ks_level + l;
-      uint64_t* out = ksk + row * (n + 1);
+    for (uint32_t s = 0; s < p.ks_level; s++) {  // storage row s (least significant first) -> engine row
+      const size_t row = (size_t)j * p.ks_level + s;
+      uint64_t* out = ksk + ((size_t)j * p.ks_level + (p.ks_level - 1 - s)) * (n + 1);
       mask_words(aes, row * n, n, out);
       out[n] = bodies[row];
     }
