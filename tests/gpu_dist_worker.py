@@ -110,6 +110,35 @@ def main(preset_name: str, out_path: str, G: int = 1024) -> int:
             res["c5_s"] = time.time() - t0
             res["c5_ok"] = int(mx.decrypt(ck)[0]) == 2**32 - 3 and int(idx.decrypt(ck)[0]) == 77
             res["c5_pbs_this_rank"] = c.pbs_count
+            # the device-resident tree (round 5): every level sliced, launched and gathered as device tensors
+            import hashlib
+
+            def digest(*arrs):
+                h = hashlib.sha256()
+                for a in arrs:
+                    h.update(np.ascontiguousarray(a.cpu().numpy() if isinstance(a, torch.Tensor) else a).view(np.uint8))
+                return h.hexdigest()
+
+            cd = I.Circuit(eng, device="cuda:0")
+            bd = I.FheUint.encrypt(cd, ck, v, 32, seed=0xB1D, stream0=0)
+            torch.cuda.synchronize()
+            t0 = time.time()
+            mxd, idxd = max_tree(cd, bd, group=dist.group.WORLD)
+            torch.cuda.synchronize()
+            res["c5_dev_s"] = time.time() - t0
+            res["c5_dev_tensor"] = isinstance(mxd.bits, torch.Tensor) and mxd.bits.is_cuda
+            res["c5_dev_ok"] = int(mxd.decrypt(ck)[0]) == 2**32 - 3 and int(idxd.decrypt(ck)[0]) == 77
+            res["c5_dev_pbs_this_rank"] = cd.pbs_count
+            res["c5_dev_digest"] = digest(mxd.bits, idxd.bits)
+            res["c5_host_digest"] = digest(mx.bits.view(np.int64), idx.bits.view(np.int64))
+            if rank == 0:
+                # single rank, same circuit shape: a shard of P/world pairs costs what P pairs cost at world x the
+                # launch-round size (Circuit.carry_block's model is linear in the batch), so the block sizes agree
+                c1 = I.Circuit(eng, device="cuda:0", round_size=world * eng.round_size)
+                b1 = I.FheUint.encrypt(c1, ck, v, 32, seed=0xB1D, stream0=0)
+                mx1, idx1 = max_tree(c1, b1)
+                res["c5_single_digest"] = digest(mx1.bits, idx1.bits)
+                res["c5_single_pbs"] = c1.pbs_count
         eng.close()
     finally:
         with open(out_path, "w") as f:

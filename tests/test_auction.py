@@ -11,7 +11,7 @@ import torch.multiprocessing as mp
 
 from tfhe_amd import integer as I
 from tfhe_amd.auction import max_tree
-from test_integer import ClearKey, CleartextEngine
+from test_integer import ClearKey, CleartextEngine, CleartextTorchEngine
 
 
 def _bids(B, seed=5):
@@ -69,11 +69,14 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         v = _bids(64, seed=11)
-        eng = CleartextEngine()
-        c = I.Circuit(eng)
-        mx, idx = max_tree(c, I.FheUint.trivial(c, v, 32), group=dist.group.WORLD)
         ck = ClearKey()
-        q.put((rank, int(mx.decrypt(ck)[0]), int(idx.decrypt(ck)[0]), c.pbs_count))
+        out = [rank]
+        # host arrays, then the device-resident circuit (torch tensors: sliced and gathered as tensors)
+        for dev in (None, "cpu"):
+            c = I.Circuit(CleartextTorchEngine(), device=dev)
+            mx, idx = max_tree(c, I.FheUint.trivial(c, v, 32), group=dist.group.WORLD)
+            out += [int(mx.decrypt(ck)[0]), int(idx.decrypt(ck)[0]), c.pbs_count, type(mx.bits).__name__]
+        q.put(tuple(out))
     finally:
         dist.destroy_process_group()
 
@@ -90,12 +93,14 @@ def test_max_tree_gloo_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     want = _expected(_bids(64, seed=11))
-    for rank, mx, idx, pbs in res:
-        assert (mx, idx) == want, rank
-    # the comparisons were split: each rank bootstrapped only part of the tree
     c = I.Circuit(CleartextEngine())
     max_tree(c, I.FheUint.trivial(c, _bids(64, seed=11), 32))
-    assert max(r[3] for r in res) < c.pbs_count
+    for rank, mx, idx, pbs, kind, mx_d, idx_d, pbs_d, kind_d in res:
+        assert (mx, idx) == want and (mx_d, idx_d) == want, rank
+        assert kind == "ndarray" and kind_d == "Tensor"
+        # the comparisons were split: each rank bootstrapped only part of the tree, in both circuit forms
+        assert pbs == pbs_d and pbs < c.pbs_count
+    assert sum(r[3] for r in res) == c.pbs_count
 
 
 def test_max_tree_launch_shape():

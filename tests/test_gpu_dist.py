@@ -3,7 +3,9 @@ with its own tfhe_amd.Engine, in one torch.distributed group (gloo: both ranks s
 one-GPU box, which RCCL does not allow).  Rank 0 generates and broadcasts the keys once; a global
 batch is bootstrapped as per-rank contiguous shards and all_gathered; the result must equal a
 single-rank run bit for bit and the CPU oracle on a sample that straddles the shard boundary; the C5
-auction tree runs with every level sharded (tests/gpu_dist_worker.py does the work).
+auction tree runs with every level sharded, as host arrays and device-resident (the level's tensors sliced,
+launched and all_gathered on the device), bit-equal across ranks, forms and a single-rank run of the same
+circuit shape (tests/gpu_dist_worker.py does the work).
 
 The ranks are started as child processes (fork + exec of a fresh interpreter) of this pytest process.
 """
@@ -61,8 +63,13 @@ def test_world2_engines_shard_gather_bitexact(preset, tmp_path):
     if preset != "fhevm_fft":
         for r in res:
             assert r["c5_ok"], r
-        # the tree's comparisons really were split: each rank ran a share of the PBS
-        assert all(r["c5_pbs_this_rank"] > 0 for r in res)
+            assert r["c5_dev_ok"] and r["c5_dev_tensor"], r
+        # the tree's comparisons really were split: each rank ran a share of the PBS, on both circuit forms
+        assert all(r["c5_pbs_this_rank"] > 0 and r["c5_dev_pbs_this_rank"] > 0 for r in res)
+        assert sum(r["c5_dev_pbs_this_rank"] for r in res) == r0["c5_single_pbs"]
+        # the device-resident sharded tree: the same bits on every rank, as the host-array sharded tree and as a
+        # single-rank run of the same circuit shape
+        assert len({r["c5_dev_digest"] for r in res} | {r0["c5_host_digest"], r0["c5_single_digest"]}) == 1, res
     print({r["rank"]: {k: r[k] for k in r if k.endswith("_s") or k.endswith("_ms")} for r in res})
 
 

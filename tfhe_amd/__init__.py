@@ -411,7 +411,18 @@ class Engine:
         self.devices = devs
         self.device = devs[0]
 
-    CUS_PER_DEVICE = 256  # MI355X
+    CUS_PER_DEVICE = 256  # MI355X; the fallback when the device cannot be queried
+
+    @property
+    def cus_per_device(self) -> int:
+        """Compute units of the engine's first device (hipDeviceProp_t::multiProcessorCount, 256 on MI355X)."""
+        if getattr(self, "_cus", None) is None:
+            try:
+                import torch
+                self._cus = int(torch.cuda.get_device_properties(self.device).multi_processor_count)
+            except Exception:  # noqa: BLE001 - no torch device view: the MI355X figure
+                self._cus = self.CUS_PER_DEVICE
+        return self._cus
 
     @property
     def round_size(self) -> int:
@@ -420,7 +431,7 @@ class Engine:
         the N = 2048 NTT kernel, 8 on the N = 1024 NTT kernel.  The carry-out circuit's launch-round cost model
         (integer.Circuit) reads it."""
         per_wg = 8 if (self.params.transform == 0 and self.params.N == 1024) else 4
-        return per_wg * self.CUS_PER_DEVICE * len(self.devices)
+        return per_wg * self.cus_per_device * len(self.devices)
 
     @property
     def key_bcast_mode(self) -> str:

@@ -6,8 +6,10 @@ Each comparison keeps the larger bid and the bidder index that holds it (ties ke
 as a first-price auction that accepts the earliest highest bid): one `ge` carry chain, then one
 select over the concatenated (bid | index) bits with the shared condition.  All comparisons of a
 level run in lockstep on the circuit (one PBS launch per circuit level); with a process group the
-level's pairs are sharded over the ranks (one GPU each) and the winners all_gathered
-(tfhe_amd.dist.sharded_map) — the only collective, once per tree level.
+level's pairs are sharded over the ranks (one GPU each, a contiguous slice per rank) and the winners
+all_gathered (tfhe_amd.dist.sharded_map) — the only collective, once per tree level.  A device-resident
+circuit (Circuit(device=...)) keeps the level on the GPU: slice, launch and gather are device tensors (RCCL
+all_gather over xGMI under "nccl"; staged through host memory under gloo).
 
 The bidder positions are public, so an index bit stays a clear value while both sides of every pair agree
 on it and needs no bootstrap when they differ: ge ? 1 : 0 is the condition itself, ge ? 0 : 1 its negation
@@ -74,8 +76,11 @@ def max_tree(c: Circuit, bids: FheUint, group=None):
         enc = [v for kind, v in cols if kind == "enc"]
         full = _cat([cur] + [v[:, None] for v in enc], axis=1) if enc else cur   # (m, w + k, dim)
         pairs = full[: 2 * P].reshape(P, 2, full.shape[1], dim)
-        if group is None or _is_t(pairs):
+        if group is None:
             res = _run_level(c, pairs, w)
+        elif _is_t(pairs):   # device-resident circuit: the level's tensors are sliced and gathered on the device
+            from .dist import sharded_map
+            res = sharded_map(pairs, lambda s: _run_level(c, s, w), group=group)
         else:
             import torch
 
@@ -83,7 +88,7 @@ def max_tree(c: Circuit, bids: FheUint, group=None):
             t = torch.from_numpy(pairs.view(np.int64).copy())
             res_t = sharded_map(t, lambda s: torch.from_numpy(
                 _run_level(c, s.numpy().view(np.uint64), w).view(np.int64).copy()), group=group)
-            res = res_t.numpy().view(np.uint64).reshape(P, full.shape[1] + 1, dim)
+            res = res_t.cpu().numpy().view(np.uint64).reshape(P, full.shape[1] + 1, dim)
         win, ge = res[:, :-1], res[:, -1]
         cols = _index_level(c, cols, win[:, w:], ge, P)
         cur = _cat([win[:, :w], cur[2 * P:]], axis=0)                          # odd leftover advances

@@ -28,6 +28,8 @@ constexpr int MS_CT = MS_CT_N;  // ciphertexts per workgroup
 constexpr int MS_ZT = MS_ZT_N;  // zeros per scan step
 constexpr int MS_IC = 128;   // elements per LDS chunk
 constexpr int MS_THREADS = MS_CT * MS_ZT;
+// the per-ciphertext loop steps by MS_THREADS / 64 waves: a workgroup below one wave would never advance
+static_assert(MS_THREADS % 64 == 0 && MS_THREADS >= 64, "MS_CT_N * MS_ZT_N must be a positive multiple of 64");
 
 typedef long long i64;
 typedef unsigned __int128 u128;

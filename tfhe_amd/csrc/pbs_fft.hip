@@ -357,12 +357,21 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
   for (int e = 1; e < 8; e++) wb[e] = twB[64 * e + lane];
   wb[0] = make_double2(1.0, 0.0);
 #endif
+  // the wave's base priority (FFT_PRIO), also what FFT_MACPRIO drops back to after each MAC phase
 #if FFT_PRIO == 1
-  if (wave_s >= 4) __builtin_amdgcn_s_setprio(1);
+  const bool prio_hi = NW > 4 && wave_s >= 4;  // the 4-wave CTS = 2 workgroup has no second wave per SIMD
 #elif FFT_PRIO == 3
-  // A/B: with two workgroups per CU, one of them (by dispatch round) at the higher priority
-  if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_setprio(1);
+  // A/B: with two workgroups per CU, one of them (by dispatch round) at the higher priority.  Bit 8 of the
+  // workgroup index is the second dispatch half on a 256-CU part (MI355X only; other CU counts just alternate)
+  const bool prio_hi = (blockIdx.x >> 8) & 1;
+#else
+  constexpr bool prio_hi = false;
 #endif
+  auto base_prio = [&]() {
+    if (prio_hi) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  };
+  if (prio_hi) __builtin_amdgcn_s_setprio(1);
   for (int i = 0; i < n; i++) {
     // (X^a acc_c - acc_c), decomposed: the rotation image in this wave's own transpose area (its previous
     // user, the last inverse, is this wave: DS operations of a wave run in order)
@@ -375,7 +384,7 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
       constexpr int q = decltype(qc)::value;
       const int g = 3 * i + q;
 #if FFT_MACPRIO
-      if (q > 0) __builtin_amdgcn_s_setprio(0);
+      if (q > 0) base_prio();
 #endif
       if constexpr (LDS_TW) {
         glds_barrier();  // step g's chunk is in K[g & 1]; every wave is done with K[(g + 1) & 1]
@@ -426,7 +435,7 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
     level(std::integral_constant<int, 1>{});
     level(std::integral_constant<int, 2>{});
 #if FFT_MACPRIO
-    __builtin_amdgcn_s_setprio(0);
+    base_prio();
 #endif
     // exchange the partial sums: publish O_(1-c)^c, take O_c^(1-c) (c wave-uniform: a scalar branch, no selects)
     double xr[8], xi[8];

@@ -137,6 +137,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
 #if F1_PRIO == 1
   if (wave_s >= 4) __builtin_amdgcn_s_setprio(1);
 #elif F1_PRIO == 3
+  // bit 8 of the workgroup index = the second dispatch half on a 256-CU part (MI355X only; on other CU counts
+  // the two workgroups of a CU just get an arbitrary split)
   if constexpr (NW == 2 * CTS)
     if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_setprio(1);
 #endif

@@ -42,12 +42,25 @@ def broadcast_keys(bsk, ksk, src: int = 0, group=None) -> float:
     return (time.perf_counter() - t0) * 1e3
 
 
+def _gather_device(local, group):
+    """Where the all_gather buffers must live for the group's backend: device memory for "nccl" (RCCL over xGMI:
+    a host tensor would be refused), host memory for gloo (its all_gather takes CPU tensors only)."""
+    import torch
+    import torch.distributed as dist
+
+    if dist.get_backend(group) == "nccl":
+        return local.device if local.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 def sharded_map(global_in, fn: Callable, group=None):
-    """Apply `fn` (a batched per-rank kernel: (B_r, d) -> (B_r, d')) to this rank's contiguous shard
+    """Apply `fn` (a batched per-rank kernel: (B_r, ...) -> (B_r, ...)) to this rank's contiguous shard
     of `global_in` (same tensor on every rank) and all_gather the shards back in order.
 
-    Used for chained circuits (one tree level per call); for the throughput bench every rank owns
-    its batch and no gather is needed."""
+    `global_in` may be a host tensor or a device tensor (a device-resident circuit level); the result is on the
+    device of fn's output.  Under "nccl" the gather runs on device buffers (RCCL), under gloo through host
+    buffers.  Used for chained circuits (one tree level per call); for the throughput bench every rank owns its
+    batch and no gather is needed."""
     import torch
     import torch.distributed as dist
 
@@ -59,11 +72,12 @@ def sharded_map(global_in, fn: Callable, group=None):
     sizes = [shard_range(total, world, r) for r in range(world)]
     width = local.shape[1:]
     maxrows = max(b - a for a, b in sizes)
-    padded = torch.zeros((maxrows,) + tuple(width), dtype=local.dtype, device=local.device)
-    padded[: local.shape[0]] = local
+    gdev = _gather_device(local, group)
+    padded = torch.zeros((maxrows,) + tuple(width), dtype=local.dtype, device=gdev)
+    padded[: local.shape[0]] = local.to(gdev)
     bufs: List = [torch.empty_like(padded) for _ in range(world)]
     dist.all_gather(bufs, padded, group=group)
-    return torch.cat([bufs[r][: b - a] for r, (a, b) in enumerate(sizes)], dim=0)
+    return torch.cat([bufs[r][: b - a] for r, (a, b) in enumerate(sizes)], dim=0).to(local.device)
 
 
 def rank_batch_seed(base_seed: int, rank: int) -> int:
