@@ -1,9 +1,9 @@
 #!/bin/bash
-# Profile one bench preset on the GPU box: the bench line (with the CPU baseline), a rocprofv3
-# kernel-trace summary of the same command, one SQ counter pass, the FETCH/WRITE passes for the
-# HBM-traffic field and (last, optional) an SQ instruction-mix pass; then tools/roofline_summary.py
-# folds them into gpurun_out/<TAG>_roofline.json tagged with the tree's source_id (bench.py reads
-# the copy under profiles/ only while its own source_id matches).  Each GPU step has its own time
+# Profile one bench preset on the GPU box: a rocprofv3 kernel-trace summary of the bench command, one SQ
+# counter pass, the FETCH/WRITE passes for the HBM-traffic field and an SQ instruction-mix pass; then
+# tools/roofline_summary.py folds them into gpurun_out/<TAG>_roofline.json tagged with the tree's source_id,
+# and finally the bench line itself (with the CPU baseline) reads that summary (bench.py uses a profile under
+# profiles/ only while its source_id matches its own).  Each GPU step has its own time
 # limit; the script stops at the first failure.
 #   TAG=r02_fft1 PRESET=gate_fft tools/profile_round.sh
 set -u
@@ -14,10 +14,6 @@ TAG=${TAG:-r02}
 PRESET=${PRESET:-gate_fft}
 B="--preset $PRESET"
 BENCH=${BENCH:-1}
-if [ "$BENCH" = "1" ]; then
-  timeout -k 10 300 python bench.py $B > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { echo "bench failed"; tail -30 gpurun_out/bench_${TAG}.err; exit 1; }
-  cat gpurun_out/bench_${TAG}.json
-fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python3 bench.py $B --no-cpu > gpurun_out/prof_${TAG}.log 2>&1 || { echo "rocprof stats failed"; tail -30 gpurun_out/prof_${TAG}.log; exit 1; }
 find gpurun_out/prof_${TAG} -name '*kernel_stats.csv' -exec cp {} gpurun_out/${TAG}_kernel_stats.csv \;
 head -6 gpurun_out/${TAG}_kernel_stats.csv | cut -c1-200
@@ -37,4 +33,11 @@ if [ "${MIX:-1}" = "1" ]; then
   fi
 fi
 python tools/roofline_summary.py $TAG gpurun_out/${TAG}_kernel_stats.csv gpurun_out/${TAG}_pmc_sq.csv gpurun_out/${TAG}_pmc_fetch.csv gpurun_out/${TAG}_pmc_write.csv $MIXCSV gpurun_out/${TAG}_roofline.json || { echo "summary failed"; exit 1; }
+# the bench line LAST, with the summary placed under profiles/ of this box's copy, so bench.py picks up the counters
+# of this very build (same source_id) -- round 4's P-FHEVM line ran before its profile existed and carried nulls
+if [ "$BENCH" = "1" ]; then
+  cp gpurun_out/${TAG}_roofline.json profiles/${TAG}_roofline.json
+  timeout -k 10 300 python bench.py $B > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { echo "bench failed"; tail -30 gpurun_out/bench_${TAG}.err; exit 1; }
+  cat gpurun_out/bench_${TAG}.json
+fi
 echo ALL_OK
