@@ -232,7 +232,10 @@ def main() -> int:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if world > 1:
+    # a process group whenever a launcher set one up: N > 1, or torch.distributed.run with one rank (the 1-GPU
+    # rehearsal of the RCCL path: key broadcast, barriers and the max-over-ranks all_reduce on a world-1 communicator)
+    dist_on = world > 1 or ("RANK" in os.environ and "MASTER_ADDR" in os.environ)
+    if dist_on:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -265,7 +268,7 @@ def main() -> int:
         d_bsk = torch.empty(bsk_len, dtype=torch.int64, device=dev)
         d_ksk = torch.empty(ksk_len, dtype=torch.int64, device=dev)
     bcast_ms = 0.0
-    if world > 1:
+    if dist_on:
         dist.barrier()
         bcast_ms = broadcast_keys(d_bsk, d_ksk, src=0)
     eng = tfhe_amd.Engine(params, local)
@@ -301,14 +304,14 @@ def main() -> int:
 
     eng.timing(True)
     eng.timing_reset()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         eng.pbs_async(d_in, d_lut, d_out, stream=stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     eng.timing(False)
@@ -317,7 +320,7 @@ def main() -> int:
     msr_ms, msr_n = eng.timing_stats(2)
 
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     elapsed_max = float(t_max.item())
 
@@ -327,7 +330,7 @@ def main() -> int:
     else:
         correct = bool(np.array_equal(ck.decrypt_bool(out), bits))
     ok = torch.tensor([1 if correct else 0], dtype=torch.int32, device=dev)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
 
     ms_per_step = elapsed_max * 1e3 / args.steps
@@ -404,7 +407,7 @@ def main() -> int:
             result["sample_bitexact"] = exact
             result["bitexact_check"] = digest
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
     eng.close()

@@ -17,7 +17,8 @@
  *   cmul(z, w)       re = fma(z.re, w.re, -(z.im * w.im)),  im = fma(z.re, w.im, z.im * w.re)
  *                    (inverse transforms use w = (w.re, -w.im))
  *   dft8             radix-2 decimation in frequency, 3 stages, natural order in and out; the
- *                    internal rotations by e^{+-i pi/4 j} are the explicit forms in w8() below
+ *                    internal rotations by e^{+-i pi/4 j} are the explicit forms in w8() below, the
+ *                    sqrt(1/2) of the odd half folded into the last stage's fmas (round 5, see dft8)
  *   3 passes         M = 512 = 8 x 8 x 8 over a 64 x 8 grid (the device's lane x register grid),
  *                    w = e^{2 pi i / M}, n = n0 + 8 n1 + 64 n2, k = k0 + 8 k1 + 64 k2:
  *                    A: lane L = n0 + 8 n1 transforms n2, then x[k0] *= w^{L k0} (k0 > 0; with the twist
@@ -152,7 +153,48 @@ static inline or_c64 w8(or_c64 t, int j, int inv) {
   return r;
 }
 
+/* dft8 (round 5, = fft512.h FFT_DFT8_FMA): the even half as below; the odd half keeps the w8 forms unscaled
+ * (u5 = w8^1 t1 / s, u7 = w8^3 t3 / s, s = sqrt(1/2)) and folds s into the last stage:
+ *   z5' = u5 + u7, z7' = u5 - u7, z4 = t0 + r t2, z6 = t0 - r t2   (r = +i forward, -i inverse)
+ *   X1 = fma(s, z5', z4), X5 = fma(-s, z5', z4), X3 = z6 + r (s z7'), X7 = z6 - r (s z7') as fmas */
 static void dft8(or_c64 x[8], int inv) {
+  or_c64 y[4], t[4];
+  for (int j = 0; j < 4; j++) {
+    y[j] = cadd(x[j], x[j + 4]);
+    t[j] = csub(x[j], x[j + 4]);
+  }
+  double ar, ai, cr, ci, z4r, z4i, z6r, z6i;
+  if (!inv) {
+    ar = t[1].re - t[1].im; ai = t[1].re + t[1].im;
+    cr = -(t[3].re + t[3].im); ci = t[3].re - t[3].im;
+    z4r = t[0].re - t[2].im; z4i = t[0].im + t[2].re;
+    z6r = t[0].re + t[2].im; z6i = t[0].im - t[2].re;
+  } else {
+    ar = t[1].re + t[1].im; ai = t[1].im - t[1].re;
+    cr = t[3].im - t[3].re; ci = -(t[3].re + t[3].im);
+    z4r = t[0].re + t[2].im; z4i = t[0].im - t[2].re;
+    z6r = t[0].re - t[2].im; z6i = t[0].im + t[2].re;
+  }
+  const double z5r = ar + cr, z5i = ai + ci, z7r = ar - cr, z7i = ai - ci;
+  const or_c64 e0 = cadd(y[0], y[2]), e2 = csub(y[0], y[2]), e1 = cadd(y[1], y[3]);
+  const or_c64 e3 = w8(csub(y[1], y[3]), 2, inv);
+  x[0] = cadd(e0, e1);
+  x[4] = csub(e0, e1);
+  x[2] = cadd(e2, e3);
+  x[6] = csub(e2, e3);
+  x[1].re = fma(SQRT1_2, z5r, z4r); x[1].im = fma(SQRT1_2, z5i, z4i);
+  x[5].re = fma(-SQRT1_2, z5r, z4r); x[5].im = fma(-SQRT1_2, z5i, z4i);
+  if (!inv) {
+    x[3].re = fma(-SQRT1_2, z7i, z6r); x[3].im = fma(SQRT1_2, z7r, z6i);
+    x[7].re = fma(SQRT1_2, z7i, z6r); x[7].im = fma(-SQRT1_2, z7r, z6i);
+  } else {
+    x[3].re = fma(SQRT1_2, z7i, z6r); x[3].im = fma(-SQRT1_2, z7r, z6i);
+    x[7].re = fma(-SQRT1_2, z7i, z6r); x[7].im = fma(SQRT1_2, z7r, z6i);
+  }
+}
+
+/* the round-1..4 dft8 (56 f64 operations), kept for reference; unused */
+__attribute__((unused)) static void dft8_r4(or_c64 x[8], int inv) {
   or_c64 y[8], z[8], u[8];
   for (int j = 0; j < 4; j++) {
     y[j] = cadd(x[j], x[j + 4]);
@@ -298,7 +340,71 @@ static inline or_c64 w16(or_c64 t, int k, int inv) {
   }
 }
 
+/* w8^j (j = 1, 3) without its sqrt(1/2) (fft1k.h w8u) */
+static inline or_c64 w8u(or_c64 t, int j, int inv) {
+  const double p = t.re, q = t.im;
+  or_c64 r;
+  if (j == 1) {
+    if (!inv) { r.re = p - q; r.im = p + q; } else { r.re = p + q; r.im = q - p; }
+  } else {
+    if (!inv) { r.re = -(p + q); r.im = p - q; } else { r.re = q - p; r.im = -(p + q); }
+  }
+  return r;
+}
+/* radix4 over (a, b, c, d) with c = s cu (cs = 1) or b = s bu, d = s du (cs = 0), s folded into fmas (fft1k.h r4_cs /
+ * r4_bds) */
+static void radix4_s(or_c64* x, int i0, int cs, int inv) {
+  const or_c64 a = x[i0], b = x[i0 + 1], c = x[i0 + 2], d = x[i0 + 3];
+  or_c64 t0, t1, A, C, p, q;
+  if (cs) {
+    t0.re = fma(SQRT1_2, c.re, a.re); t0.im = fma(SQRT1_2, c.im, a.im);
+    t1.re = fma(-SQRT1_2, c.re, a.re); t1.im = fma(-SQRT1_2, c.im, a.im);
+    const or_c64 t2 = cadd(b, d), t3 = csub(b, d);
+    A = cadd(t0, t2);
+    C = csub(t0, t2);
+    p = (or_c64){t1.re - t3.im, t1.im + t3.re};
+    q = (or_c64){t1.re + t3.im, t1.im - t3.re};
+  } else {
+    t0 = cadd(a, c);
+    t1 = csub(a, c);
+    const or_c64 t2 = cadd(b, d), t3 = csub(b, d); /* / s */
+    A.re = fma(SQRT1_2, t2.re, t0.re); A.im = fma(SQRT1_2, t2.im, t0.im);
+    C.re = fma(-SQRT1_2, t2.re, t0.re); C.im = fma(-SQRT1_2, t2.im, t0.im);
+    p.re = fma(-SQRT1_2, t3.im, t1.re); p.im = fma(SQRT1_2, t3.re, t1.im);
+    q.re = fma(SQRT1_2, t3.im, t1.re); q.im = fma(-SQRT1_2, t3.re, t1.im);
+  }
+  x[i0] = A;
+  x[i0 + 2] = C;
+  x[i0 + 1] = inv ? q : p;
+  x[i0 + 3] = inv ? p : q;
+}
+
+/* dft16 (round 5, = fft1k.h F1_DFT16_FMA): the first radix-4 pass, then group k0 = 0 plain, groups 1 and 3 with
+ * W^1 / W^3 / W^9 as cmul and the W^2 / W^6 element unscaled (radix4_s cs = 1), group 2 with W^4 = i and the W^2 / W^6
+ * elements unscaled (radix4_s cs = 0) */
 static void dft16(or_c64 x[16], int inv) {
+  for (int n0 = 0; n0 < 4; n0++) radix4(x, n0, 4, inv);
+  radix4(x, 0, 1, inv);
+  x[5] = w16(x[5], 1, inv);
+  x[6] = w8u(x[6], 1, inv);
+  x[7] = w16(x[7], 3, inv);
+  radix4_s(x, 4, 1, inv);
+  x[9] = w8u(x[9], 1, inv);
+  x[10] = w16(x[10], 4, inv);
+  x[11] = w8u(x[11], 3, inv);
+  radix4_s(x, 8, 0, inv);
+  x[13] = w16(x[13], 3, inv);
+  x[14] = w8u(x[14], 3, inv);
+  x[15] = w16(x[15], 9, inv);
+  radix4_s(x, 12, 1, inv);
+  or_c64 y[16];
+  for (int k0 = 0; k0 < 4; k0++)
+    for (int k1 = 0; k1 < 4; k1++) y[k0 + 4 * k1] = x[4 * k0 + k1];
+  memcpy(x, y, sizeof(y));
+}
+
+/* the round-4 dft16, kept for reference; unused */
+__attribute__((unused)) static void dft16_r4(or_c64 x[16], int inv) {
   static const int K[16] = {0, 0, 0, 0, 0, 1, 2, 3, 0, 2, 4, 6, 0, 3, 6, 9}; /* n0 k0 at position n0 + 4 k0 */
   for (int n0 = 0; n0 < 4; n0++) radix4(x, n0, 4, inv);
   for (int pos = 5; pos < 16; pos++)

@@ -10,7 +10,10 @@ node) in a torch.distributed group:
   3. (P-GATE) the C5 auction tree (256 FheUint32 bids, 8 levels) with every level sharded over the
      ranks and the winners all_gathered between levels.
 
-  RANK=r WORLD_SIZE=w MASTER_ADDR=127.0.0.1 MASTER_PORT=p python tests/gpu_dist_worker.py PRESET OUT_JSON [G]
+  RANK=r WORLD_SIZE=w MASTER_ADDR=127.0.0.1 MASTER_PORT=p [DIST_BACKEND=nccl] python tests/gpu_dist_worker.py PRESET OUT_JSON [G]
+
+DIST_BACKEND (default gloo: two ranks sharing device 0, which RCCL refuses) = nccl runs the same steps over RCCL: the
+key broadcast and every all_gather on device buffers (one rank per GPU; on a one-GPU box a world-1 communicator).
 
 G (default 1024, C2) sets the global batch of step 2; G = 65536 is C4's global batch (BASELINE.json configs[3]),
 checked at both sides of the rank boundary; step 3 (C5) runs only at the default G.
@@ -35,8 +38,14 @@ KEY_SEED = 0x7F4E0001
 
 def main(preset_name: str, out_path: str, G: int = 1024) -> int:
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    res = {"rank": rank, "world": world, "preset": preset_name}
+    backend = os.environ.get("DIST_BACKEND", "gloo")
+    dev = torch.device("cuda", 0 if backend == "gloo" else int(os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
+    res = {"rank": rank, "world": world, "preset": preset_name, "backend": dist.get_backend()}
     try:
         preset = {"gate_fft": tfhe_amd.PRESET_GATE_FFT, "gate": tfhe_amd.PRESET_GATE,
                   "fhevm_fft": tfhe_amd.PRESET_FHEVM_FFT}[preset_name]
@@ -57,14 +66,16 @@ def main(preset_name: str, out_path: str, G: int = 1024) -> int:
             bsk = torch.empty(bsk_len, dtype=torch.int64)
             ksk = torch.empty(ksk_len, dtype=torch.int64)
             zeros = torch.empty((tfhe_amd.MS_FHEVM["count"], params.n + 1), dtype=torch.int64) if fhevm else None
+        if backend == "nccl":   # RCCL broadcasts device buffers
+            bsk, ksk = bsk.to(dev), ksk.to(dev)
+            zeros = zeros.to(dev) if fhevm else None
         res["bcast_ms"] = broadcast_keys(bsk, ksk, src=0)
         if fhevm:
             dist.broadcast(zeros, src=0)
-        dev = torch.device("cuda", 0)
-        eng = tfhe_amd.Engine(params, 0)
+        eng = tfhe_amd.Engine(params, dev.index)
         eng.load_keys_device(bsk.to(dev), ksk.to(dev))
         if fhevm:
-            eng.load_ms_key(zeros.numpy().view(np.uint64))
+            eng.load_ms_key(zeros.cpu().numpy().view(np.uint64))
 
         # 2. one global batch (C2 by default, C4 at G = 65536), sharded over the ranks and gathered
         rng = np.random.default_rng(0xC0FFEE02)
@@ -119,7 +130,7 @@ def main(preset_name: str, out_path: str, G: int = 1024) -> int:
                     h.update(np.ascontiguousarray(a.cpu().numpy() if isinstance(a, torch.Tensor) else a).view(np.uint8))
                 return h.hexdigest()
 
-            cd = I.Circuit(eng, device="cuda:0")
+            cd = I.Circuit(eng, device=str(dev))
             bd = I.FheUint.encrypt(cd, ck, v, 32, seed=0xB1D, stream0=0)
             torch.cuda.synchronize()
             t0 = time.time()
@@ -134,7 +145,7 @@ def main(preset_name: str, out_path: str, G: int = 1024) -> int:
             if rank == 0:
                 # single rank, same circuit shape: a shard of P/world pairs costs what P pairs cost at world x the
                 # launch-round size (Circuit.carry_block's model is linear in the batch), so the block sizes agree
-                c1 = I.Circuit(eng, device="cuda:0", round_size=world * eng.round_size)
+                c1 = I.Circuit(eng, device=str(dev), round_size=world * eng.round_size)
                 b1 = I.FheUint.encrypt(c1, ck, v, 32, seed=0xB1D, stream0=0)
                 mx1, idx1 = max_tree(c1, b1)
                 res["c5_single_digest"] = digest(mx1.bits, idx1.bits)

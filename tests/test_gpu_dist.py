@@ -29,13 +29,13 @@ def _free_port() -> int:
     return port
 
 
-def _run_world(preset: str, tmp_path, world: int = 2, G: int = 1024):
+def _run_world(preset: str, tmp_path, world: int = 2, G: int = 1024, backend: str = "gloo"):
     port = _free_port()
     procs, outs = [], []
     for r in range(world):
         out = str(tmp_path / f"rank{r}.json")
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port))
+                   MASTER_PORT=str(port), DIST_BACKEND=backend)
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "gpu_dist_worker.py"), preset, out,
                                        str(G)],
                                       cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
@@ -71,6 +71,34 @@ def test_world2_engines_shard_gather_bitexact(preset, tmp_path):
         # single-rank run of the same circuit shape
         assert len({r["c5_dev_digest"] for r in res} | {r0["c5_host_digest"], r0["c5_single_digest"]}) == 1, res
     print({r["rank"]: {k: r[k] for k in r if k.endswith("_s") or k.endswith("_ms")} for r in res})
+
+
+def test_world1_rccl_path(tmp_path):
+    """The RCCL ("nccl" backend) code path on a one-GPU box: a world-1 communicator runs the key broadcast, the C2
+    shard + all_gather and the C5 tree (host-array and device-resident forms, every level through sharded_map) on
+    DEVICE buffers -- what the 8-GPU node runs per rank, minus the peers (gloo cannot host device tensors, and RCCL
+    refuses two ranks on one device)."""
+    r0 = _run_world("gate_fft", tmp_path, world=1, backend="nccl")[0]
+    assert r0["backend"] == "nccl", r0
+    assert r0["equal_single_rank"] and r0["oracle_sample_ok"] and r0["decrypt_ok"], r0
+    assert r0["c5_ok"] and r0["c5_dev_ok"] and r0["c5_dev_tensor"], r0
+    assert len({r0["c5_dev_digest"], r0["c5_host_digest"], r0["c5_single_digest"]}) == 1, r0
+    print({k: r0[k] for k in r0 if k.endswith("_s") or k.endswith("_ms")})
+
+
+def test_bench_under_torchrun_one_rank(tmp_path):
+    """bench.py as the driver launches it for N > 1 (python -m torch.distributed.run ... bench.py --gpus N), with one
+    rank: the process group comes up on RCCL and the key broadcast, barriers and max-over-ranks all_reduce run."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "2",
+           "--warmup", "1", "--batch", "1024", "--no-cpu"]
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+    line = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["decrypt_ok"], line
+    assert "broadcast" in p.stderr or "bcast" in p.stderr or line.get("key_broadcast_ms") is not None, p.stderr[-2000:]
+    print({k: line[k] for k in ("value", "ms_per_step", "n_gpus")})
 
 
 def test_world2_c4_global_batch_65536(tmp_path):

@@ -118,6 +118,61 @@ __device__ __forceinline__ void w16(double& re, double& im) {
   else w8<INV, 2>(re, im);  // K == 4: i
 }
 
+// F1_DFT16_FMA 1 (default since round 5): the sqrt(1/2) of the W16^2 / W16^6 twiddles folded into the second radix-4
+// pass as fmas (as fft512.h's FFT_DFT8_FMA): group k0 = 2 takes b = s u9, d = s u11 (t2, t3 scaled by s: 4 fmas per
+// output pair), groups 1 and 3 take c = s u6 / s u14 (t0, t1 = a +- s u: 2 fmas each) -- 8 multiplies fewer per
+// DFT16, -32 f64 per wave and CMUX.  Restated in oracle/fft_oracle.c:dft16; 0 = the round-4 form.
+#ifndef F1_DFT16_FMA
+#define F1_DFT16_FMA 1
+#endif
+// w8^J (J = 1, 3) without its sqrt(1/2) factor: the oracle's w8u
+template <bool INV, int J>
+__device__ __forceinline__ void w8u(double& re, double& im) {
+  const double p = re, q = im;
+  if (J == 1) {
+    if (!INV) { re = p - q; im = p + q; }
+    else { re = p + q; im = q - p; }
+  } else {
+    if (!INV) { re = -(p + q); im = p - q; }
+    else { re = q - p; im = -(p + q); }
+  }
+}
+// r4 with c = s cu (cu given unscaled): t0 = a + s cu, t1 = a - s cu as fmas, the rest as r4
+template <bool INV>
+__device__ __forceinline__ void r4_cs(double& ar, double& ai, double& br, double& bi, double& cr, double& ci, double& dr,
+                                      double& di) {
+  const double t0r = __builtin_fma(SQRT1_2, cr, ar), t0i = __builtin_fma(SQRT1_2, ci, ai);
+  const double t1r = __builtin_fma(-SQRT1_2, cr, ar), t1i = __builtin_fma(-SQRT1_2, ci, ai);
+  const double t2r = br + dr, t2i = bi + di, t3r = br - dr, t3i = bi - di;
+  ar = t0r + t2r;
+  ai = t0i + t2i;
+  cr = t0r - t2r;
+  ci = t0i - t2i;
+  const double pr = t1r - t3i, pi = t1i + t3r, qr = t1r + t3i, qi = t1i - t3r;
+  br = INV ? qr : pr;
+  bi = INV ? qi : pi;
+  dr = INV ? pr : qr;
+  di = INV ? pi : qi;
+}
+// r4 with b = s bu, d = s du (unscaled): t2, t3 carry the factor s into the output fmas
+template <bool INV>
+__device__ __forceinline__ void r4_bds(double& ar, double& ai, double& br, double& bi, double& cr, double& ci, double& dr,
+                                       double& di) {
+  const double t0r = ar + cr, t0i = ai + ci, t1r = ar - cr, t1i = ai - ci;
+  const double t2r = br + dr, t2i = bi + di, t3r = br - dr, t3i = bi - di;  // / s
+  ar = __builtin_fma(SQRT1_2, t2r, t0r);
+  ai = __builtin_fma(SQRT1_2, t2i, t0i);
+  cr = __builtin_fma(-SQRT1_2, t2r, t0r);
+  ci = __builtin_fma(-SQRT1_2, t2i, t0i);
+  // p = t1 + i t3, q = t1 - i t3 with t3 = s t3'
+  const double pr = __builtin_fma(-SQRT1_2, t3i, t1r), pi = __builtin_fma(SQRT1_2, t3r, t1i);
+  const double qr = __builtin_fma(SQRT1_2, t3i, t1r), qi = __builtin_fma(-SQRT1_2, t3r, t1i);
+  br = INV ? qr : pr;
+  bi = INV ? qi : pi;
+  dr = INV ? pr : qr;
+  di = INV ? pi : qi;
+}
+
 // 16-point DFT in registers, natural order in and out: radix-4 over n1 (positions n0 + 4 k0), W16^{n0 k0}, radix-4
 // over n0 (positions 4 k0 + k1), X[k0 + 4 k1] = position 4 k0 + k1 (a renaming)
 template <bool INV>
@@ -125,6 +180,21 @@ __device__ __forceinline__ void dft16(double (&xr)[16], double (&xi)[16]) {
 #pragma unroll
   for (int n0 = 0; n0 < 4; n0++)
     r4<INV>(xr[n0], xi[n0], xr[n0 + 4], xi[n0 + 4], xr[n0 + 8], xi[n0 + 8], xr[n0 + 12], xi[n0 + 12]);
+#if F1_DFT16_FMA
+  r4<INV>(xr[0], xi[0], xr[1], xi[1], xr[2], xi[2], xr[3], xi[3]);
+  w16<INV, 1>(xr[5], xi[5]);  // group 1: W^0, W^1, s u(W^2), W^3
+  w8u<INV, 1>(xr[6], xi[6]);
+  w16<INV, 3>(xr[7], xi[7]);
+  r4_cs<INV>(xr[4], xi[4], xr[5], xi[5], xr[6], xi[6], xr[7], xi[7]);
+  w8u<INV, 1>(xr[9], xi[9]);  // group 2: W^0, s u(W^2), W^4 = i, s u(W^6)
+  w16<INV, 4>(xr[10], xi[10]);
+  w8u<INV, 3>(xr[11], xi[11]);
+  r4_bds<INV>(xr[8], xi[8], xr[9], xi[9], xr[10], xi[10], xr[11], xi[11]);
+  w16<INV, 3>(xr[13], xi[13]);  // group 3: W^0, W^3, s u(W^6), W^9
+  w8u<INV, 3>(xr[14], xi[14]);
+  w16<INV, 9>(xr[15], xi[15]);
+  r4_cs<INV>(xr[12], xi[12], xr[13], xi[13], xr[14], xi[14], xr[15], xi[15]);
+#else
   w16<INV, 1>(xr[5], xi[5]);
   w16<INV, 2>(xr[6], xi[6]);
   w16<INV, 3>(xr[7], xi[7]);
@@ -138,6 +208,7 @@ __device__ __forceinline__ void dft16(double (&xr)[16], double (&xi)[16]) {
   for (int k0 = 0; k0 < 4; k0++)
     r4<INV>(xr[4 * k0], xi[4 * k0], xr[4 * k0 + 1], xi[4 * k0 + 1], xr[4 * k0 + 2], xi[4 * k0 + 2], xr[4 * k0 + 3],
             xi[4 * k0 + 3]);
+#endif
   double yr[16], yi[16];
 #pragma unroll
   for (int k0 = 0; k0 < 4; k0++)

@@ -211,6 +211,15 @@ struct FpShared<2> {
 #endif
 typedef __attribute__((address_space(3))) u64 lds_u64;
 
+// FFT_ROT_UNIFORM 1 (default since round 5): the rotation split so that every per-slot decision is wave-uniform.
+// a (uniform) = 1024 s + 64 A + r.  The image written is W = X^r v (lane part: each lane writes at +r, only slot 15
+// of the lanes L + r >= 64 wraps, negated, to the image start); the reads take (X^(64 A) W)[L + 64 e] = W[L + 64 (e -
+// A)] for e >= A and -W[L + 64 (e - A + 16)] for e < A, so slot e's base (two per-lane bases 8 KB apart) and sign
+// (xor s) depend only on the SGPR comparison e < A.  Per slot 8 VALU instead of 10 (no compare, no negate-and-select:
+// y = (x ^ M) - (v + M), M = 0 or all ones); the values are the same, so no operation order changes.
+#ifndef FFT_ROT_UNIFORM
+#define FFT_ROT_UNIFORM 1
+#endif
 // (X^a v - v), v = this wave's polynomial (slot e <-> coefficient 64 e + L), to decomposition states.  The
 // rotation image is the wave's transpose area.  Coefficient 64 e + L reads image entry (u + 64 e) mod 1024 with
 // u = (L - a) mod 1024, negated iff the negacyclic source index (L - a + 64 e) mod 2048 lies in [1024, 2048):
@@ -218,6 +227,36 @@ typedef __attribute__((address_space(3))) u64 lds_u64;
 // and one select per slot instead of the index arithmetic; the sign mask is an SGPR xor).
 __device__ __forceinline__ void rotate_states(const u64 (&v)[16], int a, int lane, double2* T, u32 (&st)[16]) {
   u64* Tu = (u64*)T;
+#if FFT_ROT_UNIFORM
+  a = __builtin_amdgcn_readfirstlane(a);  // ms2048(ct[i]): the same for every lane
+  const int A = (a >> 6) & 15, r = a & 63;
+  const bool sgn = a >= 1024;
+  {
+    const u32 wb = (u32)(uintptr_t)(lds_u64*)&Tu[lane + r];
+#pragma unroll
+    for (int e = 0; e < 15; e++) ((lds_u64*)(uintptr_t)wb)[64 * e] = v[e];
+    const bool w15 = lane + r >= 64;  // coefficient 960 + L + r >= 1024: to L + r - 64, negated
+    const u32 a15 = w15 ? wb + 960u * 8u - 8192u : wb + 960u * 8u;
+    *(lds_u64*)(uintptr_t)a15 = w15 ? 0 - v[15] : v[15];
+  }
+  lds_order();
+  const u32 rb = (u32)(uintptr_t)(lds_u64*)&Tu[lane] - 512u * (u32)A;  // >= T - 7.5 KB: inside the block
+  // bit e of wmask: slot e reads the wrapped part (e < A); bit e of mbits: slot e negated.  Bit-field extracts of
+  // these SGPR words keep every per-slot decision scalar (a compare would be rebuilt as a per-lane select)
+  const u32 wmask = (1u << A) - 1u;
+  const u32 mbits = __builtin_amdgcn_readfirstlane(wmask ^ (sgn ? ~0u : 0u));
+#pragma unroll
+  for (int e = 0; e < 16; e++) {
+    // s_bfe_i32 (0 or -1) in inline asm: hipcc's known-bits treat the width-1 sbfe builtin as non-negative and drop
+    // the sign extension (a probe kernel stores hi = 0 for it)
+    int m32;
+    asm("s_bfe_i32 %0, %1, %2" : "=s"(m32) : "s"(mbits), "i"(e | (1 << 16)));
+    const u64 M = (u64)(long long)m32;
+    const u64 x = ((const lds_u64*)(uintptr_t)(rb + (__builtin_amdgcn_ubfe(wmask, e, 1) << 13)))[64 * e];
+    st[e] = decomp_state((x ^ M) - (v[e] + M));
+  }
+  lds_order();
+#else
 #pragma unroll
   for (int e = 0; e < 16; e++) Tu[64 * e + lane] = v[e];
   lds_order();
@@ -252,6 +291,7 @@ __device__ __forceinline__ void rotate_states(const u64 (&v)[16], int a, int lan
   }
 #endif
   lds_order();
+#endif
 }
 
 // the partial-sum exchange of wave c (compile-time): publish O_(1-c)^c in this wave's area, add O_c^(1-c) from

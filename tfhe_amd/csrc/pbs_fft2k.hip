@@ -34,8 +34,9 @@ constexpr int N2 = 2048;
 __device__ __forceinline__ int ms4096(u64 x) { return (int)((((x >> 51) + 1) >> 1) & 4095u); }
 // tfhe-rs SignedDecomposer 2^23 x 1 on the high word (pbs_fft2k.hip: decomp_23x1_hi; tests/test_fft.py)
 __device__ __forceinline__ int dig23(u32 hi) {
-  const u32 st = (hi + 256u) >> 9;
-  return (int)((st + 0x3FFFFFu) & 0x7FFFFFu) - 0x3FFFFF;
+  // ((((hi + 2^8) >> 9) + 2^22 - 1) mod 2^23) - (2^22 - 1): the offset folded in before the shift (a multiple of 2^9
+  // there), the mod 2^23 is the u32 wrap after >> 9 -- 3 VALU instead of 5, the same value
+  return (int)((hi + (256u + (0x3FFFFFu << 9))) >> 9) - 0x3FFFFF;
 }
 typedef __attribute__((address_space(3))) u64 lds_u64;
 #ifndef F1_KPF
@@ -67,9 +68,49 @@ __device__ __forceinline__ void load_ta(double2* ta, const double2* __restrict__
 }
 
 // (X^a v - v) through the area, then 23-bit digits as doubles: xr[e] <- coefficient L + 64 e, xi[e] <- + 1024
+// F1_ROT_UNIFORM 1 (default since round 5): every per-slot decision wave-uniform, as pbs_fft.hip's FFT_ROT_UNIFORM
+// (a = 2048 s + 64 A + r; the image is W = X^r v, only slot 31 of the lanes L + r >= 64 wraps on the write; slot e
+// reads W[L + 64 (e - A)] for e >= A, -W[L + 64 (e - A + 32)] for e < A, sign xor s): 10 VALU per coefficient with
+// dig23 instead of 14, the same values
+#ifndef F1_ROT_UNIFORM
+#define F1_ROT_UNIFORM 1
+#endif
 __device__ __forceinline__ void rotate_digits(const u64 (&v)[32], int a, int lane, double2* area, double (&xr)[16],
                                               double (&xi)[16]) {
   u64* Tu = (u64*)area;
+#if F1_ROT_UNIFORM
+  a = __builtin_amdgcn_readfirstlane(a);  // ms4096(ct[i]): the same for every lane
+  const int A = (a >> 6) & 31, r = a & 63;
+  const bool sgn = a >= 2048;
+  {
+    const u32 wb = (u32)(uintptr_t)(lds_u64*)&Tu[lane + r];
+#pragma unroll
+    for (int e = 0; e < 31; e++) ((lds_u64*)(uintptr_t)wb)[64 * e] = v[e];
+    const bool w31 = lane + r >= 64;  // coefficient 1984 + L + r >= 2048: to L + r - 64, negated
+    const u32 a31 = w31 ? wb + 1984u * 8u - 16384u : wb + 1984u * 8u;
+    *(lds_u64*)(uintptr_t)a31 = w31 ? 0 - v[31] : v[31];
+  }
+  lds_order();
+  const u32 rb = (u32)(uintptr_t)(lds_u64*)&Tu[lane] - 512u * (u32)A;  // >= area - 15.5 KB: the table lies below
+  // bit e of wmask: slot e reads the wrapped part (e < A); bit e of mbits: slot e negated.  Bit-field extracts of
+  // these SGPR words keep every per-slot decision scalar (a compare would be rebuilt as a per-lane select)
+  const u32 wmask = (1u << A) - 1u;
+  const u32 mbits = __builtin_amdgcn_readfirstlane(wmask ^ (sgn ? ~0u : 0u));
+#pragma unroll
+  for (int e = 0; e < 32; e++) {
+    // s_bfe_i32 (0 or -1) in inline asm: hipcc's known-bits treat the width-1 sbfe builtin as non-negative and drop
+    // the sign extension (a probe kernel stores hi = 0 for it)
+    int m32;
+    asm("s_bfe_i32 %0, %1, %2" : "=s"(m32) : "s"(mbits), "i"(e | (1 << 16)));
+    const u64 M = (u64)(long long)m32;
+    const u64 x = ((const lds_u64*)(uintptr_t)(rb + (__builtin_amdgcn_ubfe(wmask, e, 1) << 14)))[64 * e];
+    const u64 y = (x ^ M) - (v[e] + M);
+    const double d = (double)dig23((u32)(y >> 32));
+    if (e < 16) xr[e] = d;
+    else xi[e - 16] = d;
+  }
+  lds_order();
+#else
 #pragma unroll
   for (int e = 0; e < 32; e++) Tu[64 * e + lane] = v[e];
   lds_order();
@@ -89,6 +130,7 @@ __device__ __forceinline__ void rotate_digits(const u64 (&v)[32], int a, int lan
     else xi[e - 16] = d;
   }
   lds_order();
+#endif
 }
 
 // NW waves per workgroup: 8 (the MAC spread over 8 waves, 2 slots each) or 2 CTS (every wave a transform wave,
