@@ -215,14 +215,51 @@ __attribute__((unused)) static void dft8_r4(or_c64 x[8], int inv) {
   for (int k = 0; k < 8; k++) x[k] = u[brv3[k]];
 }
 
+/* the N = 1024 forward's slot twist + pass A's DFT8 as one twisted DFT8 (round 5, = fft512.h twist_dft8_fwd): x(X) =
+ * sum_e x_e X^e at the roots X_k = e^{i pi (1 + 4k)/16} of X^8 = i by a radix-2 split (X^8 - i = (X^4 - w)(X^4 + w), ...),
+ * 12 butterflies a +- e^{i th} b each with b through the tangent / cotangent form and cos / sin th in the output fmas */
+#define TD_T8 0.41421356237309504880   /* tan(pi/8) */
+#define TD_C8 0.92387953251128675613   /* cos(pi/8) */
+#define TD_T16 0.19891236737965800691  /* tan(pi/16) */
+#define TD_C16 0.98078528040323044913  /* cos(pi/16) */
+#define TD_T316 0.66817863791929891999 /* tan(3pi/16) */
+#define TD_C316 0.83146961230254523708 /* cos(3pi/16) */
+static void tbfly(or_c64* a, or_c64* b, double t, double sc, int cot) {
+  double ur, ui;
+  if (!cot) { ur = fma(-t, b->im, b->re); ui = fma(t, b->re, b->im); }
+  else { ur = fma(t, b->re, -b->im); ui = fma(t, b->im, b->re); }
+  const or_c64 p = *a;
+  a->re = fma(sc, ur, p.re); a->im = fma(sc, ui, p.im);
+  b->re = fma(-sc, ur, p.re); b->im = fma(-sc, ui, p.im);
+}
+static void tdft8_fwd(or_c64 x[8]) {
+  for (int e = 0; e < 4; e++) {
+    const double ur = x[e + 4].re - x[e + 4].im, ui = x[e + 4].im + x[e + 4].re;
+    const or_c64 p = x[e];
+    x[e].re = fma(SQRT1_2, ur, p.re); x[e].im = fma(SQRT1_2, ui, p.im);
+    x[e + 4].re = fma(-SQRT1_2, ur, p.re); x[e + 4].im = fma(-SQRT1_2, ui, p.im);
+  }
+  tbfly(&x[0], &x[2], TD_T8, TD_C8, 0);
+  tbfly(&x[1], &x[3], TD_T8, TD_C8, 0);
+  tbfly(&x[4], &x[6], -TD_T8, TD_C8, 1);
+  tbfly(&x[5], &x[7], -TD_T8, TD_C8, 1);
+  tbfly(&x[0], &x[1], TD_T16, TD_C16, 0);
+  tbfly(&x[2], &x[3], -TD_T16, TD_C16, 1);
+  tbfly(&x[4], &x[5], TD_T316, TD_C316, 1);
+  tbfly(&x[6], &x[7], -TD_T316, -TD_C316, 0);
+  const or_c64 y[8] = {x[0], x[4], x[2], x[6], x[1], x[5], x[3], x[7]}; /* positions -> X_k */
+  memcpy(x, y, sizeof(y));
+}
+
 /* forward 3-pass DFT: natural order in, device order out; pass A multiplies slots merged ? 0..7 : 1..7 by twa
- * (the twist-merged tables multiply every slot) */
-static void dft512_fwd_tab(const or_c64* in, or_c64* out, const or_c64 (*twa)[64], int merged) {
+ * (the twist-merged tables multiply every slot); twin: the input is not yet twisted, pass A's DFT8 is tdft8_fwd */
+static void dft512_fwd_tab(const or_c64* in, or_c64* out, const or_c64 (*twa)[64], int merged, int twin) {
   const fft_tab* T = tab();
   or_c64 A[64][8], Bv[64][8], x[8];
   for (int L = 0; L < 64; L++) {
     for (int e = 0; e < 8; e++) x[e] = in[L + 64 * e];
-    dft8(x, 0);
+    if (twin) tdft8_fwd(x);
+    else dft8(x, 0);
     for (int e = merged ? 0 : 1; e < 8; e++) x[e] = cmul(x[e], twa[e][L].re, twa[e][L].im);
     memcpy(A[L], x, sizeof(x));
   }
@@ -477,12 +514,9 @@ void or_fft_fwd(const double* a, uint32_t N, or_c64* out) {
   if (N != 2 * FFT_M) abort();
   const fft_tab* T = tab();
   or_c64 z[FFT_M];
-  for (int j = 0; j < FFT_M; j++) { /* j = L + 64 e: slot constant zeta^{64 e} (e > 0), zeta^L in pass A */
-    const or_c64 v = {a[j], a[j + FFT_M]};
-    const int e = j >> 6;
-    z[j] = e ? cmul(v, T->twist[64 * e].re, T->twist[64 * e].im) : v;
-  }
-  dft512_fwd_tab(z, out, T->twAm, 1);
+  for (int j = 0; j < FFT_M; j++) z[j] = (or_c64){a[j], a[j + FFT_M]};
+  /* j = L + 64 e: the slot part zeta^{64 e} of the twist inside pass A's twisted DFT8, zeta^L in pass A's table */
+  dft512_fwd_tab(z, out, T->twAm, 1, 1);
 }
 
 void or_fft_inv(const or_c64* in, uint32_t N, double* out) {

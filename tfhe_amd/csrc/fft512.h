@@ -217,6 +217,84 @@ __device__ __forceinline__ void t1_regs(double (&xr)[8], double (&xi)[8], int la
   }
 }
 
+template <bool INV>
+__device__ __forceinline__ void twist_slots(double (&xr)[8], double (&xi)[8]);
+
+// FFT_TDFT8 1 (default since round 5): the N = 1024 forward's slot twist and pass A's DFT8 as ONE twisted DFT8.
+// Slot e carries zeta^(64 e) = e^(i pi e / 16) before the DFT8 over e, so pass A evaluates x(X) = sum_e x_e X^e at the
+// 8 roots of X^8 = i, X_k = e^(i pi (1 + 4 k) / 16) -- a negacyclic-style split:
+//   stage 1  X^8 - i = (X^4 - w)(X^4 + w), w = e^(i pi/4):       u_e = x_e + w x_(e+4),  v_e = x_e - w x_(e+4)
+//   stage 2  u: (X^2 -+ e^(i pi/8)),  v: (X^2 -+ e^(i 5pi/8))    pairs (e, e + 2)
+//   stage 3  roots +-e^(i pi/16), +-e^(i 9pi/16), +-e^(i 5pi/16), +-e^(i 13pi/16) -> X_0 X_4, X_2 X_6, X_1 X_5, X_3 X_7
+// Each of the 12 butterflies a +- e^(i th) b takes b through a tangent (or cotangent) form, u = (b.re - t b.im,
+// b.im + t b.re), and folds cos th (or sin th) into the two output fmas: 6 f64 instructions, 72 for the whole step
+// against 28 (7 slot cmuls) + 52 (DFT8) = 80.  Restated in oracle/fft_oracle.c:tdft8_fwd; 0 = twist, then DFT8.
+#ifndef FFT_TDFT8
+#define FFT_TDFT8 1
+#endif
+namespace tdft {
+constexpr double T8 = 0.41421356237309504880, C8 = 0.92387953251128675613;     // tan, cos (pi / 8)
+constexpr double T16 = 0.19891236737965800691, C16 = 0.98078528040323044913;   // tan, cos (pi / 16)
+constexpr double T316 = 0.66817863791929891999, C316 = 0.83146961230254523708; // tan, cos (3 pi / 16)
+}  // namespace tdft
+// a + e^(i th) b -> a, a - e^(i th) b -> b, with e^(i th) b = sc (u), u = (b.re - t b.im, b.im + t b.re) (COT = false:
+// t = tan th, sc = cos th) or u = (t b.re - b.im, b.re + t b.im) (COT: t = cot th, sc = sin th)
+template <bool COT>
+__device__ __forceinline__ void tbfly(double& ar, double& ai, double& br, double& bi, double t, double sc) {
+  double ur, ui;
+  if (!COT) {
+    ur = __builtin_fma(-t, bi, br);
+    ui = __builtin_fma(t, br, bi);
+  } else {
+    ur = __builtin_fma(t, br, -bi);
+    ui = __builtin_fma(t, bi, br);
+  }
+  const double pr = ar, pi = ai;
+  ar = __builtin_fma(sc, ur, pr);
+  ai = __builtin_fma(sc, ui, pi);
+  br = __builtin_fma(-sc, ur, pr);
+  bi = __builtin_fma(-sc, ui, pi);
+}
+// the slot twist + pass A's DFT8 of the N = 1024 forward transform (natural order in and out)
+__device__ __forceinline__ void twist_dft8_fwd(double (&xr)[8], double (&xi)[8]) {
+#if FFT_TDFT8
+  using namespace tdft;
+#pragma unroll
+  for (int e = 0; e < 4; e++) {  // stage 1, w = e^(i pi/4): u = (b.re - b.im, b.im + b.re), sc = sqrt(1/2)
+    const double ur = xr[e + 4] - xi[e + 4], ui = xi[e + 4] + xr[e + 4];
+    const double pr = xr[e], pi = xi[e];
+    xr[e] = __builtin_fma(SQRT1_2, ur, pr);
+    xi[e] = __builtin_fma(SQRT1_2, ui, pi);
+    xr[e + 4] = __builtin_fma(-SQRT1_2, ur, pr);
+    xi[e + 4] = __builtin_fma(-SQRT1_2, ui, pi);
+  }
+  // stage 2: u pairs at th = pi/8 (tan), v pairs at th = 5 pi/8 (cot = -tan(pi/8), sin = cos(pi/8))
+  tbfly<false>(xr[0], xi[0], xr[2], xi[2], T8, C8);
+  tbfly<false>(xr[1], xi[1], xr[3], xi[3], T8, C8);
+  tbfly<true>(xr[4], xi[4], xr[6], xi[6], -T8, C8);
+  tbfly<true>(xr[5], xi[5], xr[7], xi[7], -T8, C8);
+  // stage 3: (0, 1) pi/16 -> X0, X4; (2, 3) 9 pi/16 (cot = -tan(pi/16), sin = cos(pi/16)) -> X2, X6;
+  //          (4, 5) 5 pi/16 (cot = tan(3 pi/16), sin = cos(3 pi/16)) -> X1, X5; (6, 7) 13 pi/16 (tan = -tan(3 pi/16),
+  //          cos = -cos(3 pi/16)) -> X3, X7
+  tbfly<false>(xr[0], xi[0], xr[1], xi[1], T16, C16);
+  tbfly<true>(xr[2], xi[2], xr[3], xi[3], -T16, C16);
+  tbfly<true>(xr[4], xi[4], xr[5], xi[5], T316, C316);
+  tbfly<false>(xr[6], xi[6], xr[7], xi[7], -T316, -C316);
+  // positions 0..7 now hold X0 X4 X2 X6 X1 X5 X3 X7: rename to natural order
+  const double r1 = xr[4], i1 = xi[4], r2 = xr[2], i2 = xi[2], r3 = xr[6], i3 = xi[6], r4 = xr[1], i4 = xi[1];
+  const double r6 = xr[3], i6 = xi[3];
+  xr[1] = r1; xi[1] = i1;
+  xr[2] = r2; xi[2] = i2;
+  xr[3] = r3; xi[3] = i3;
+  xr[4] = r4; xi[4] = i4;
+  xr[6] = r6; xi[6] = i6;
+  // 5 (X5) and 7 (X7) are in place, 0 (X0) too
+#else
+  twist_slots<false>(xr, xi);
+  dft8<false>(xr, xi);
+#endif
+}
+
 // per-lane transpose bases: b1 = T1 read / inverse write, b2 = T2 read / inverse write
 struct TBase {
   int b1, b2;
@@ -227,10 +305,12 @@ struct TBase {
 // forward 512-point DFT: natural order in (lane L, slot e <-> L + 64 e), device order out.
 // TW0: pass A multiplies slot 0 too (the N = 1024 tables fold the lane part of the twist into pass A)
 // (twA / twB: the pass A / pass B tables, 512 complex each, [64 e + L])
-template <bool TW0 = false>
+// TWIN: the input is not yet twisted and pass A's DFT8 is the twisted one (twist_dft8_fwd; N = 1024 only)
+template <bool TW0 = false, bool TWIN = false>
 __device__ __forceinline__ void dft512_fwd_t(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
                                              const double2* twA, const double2* twB) {
-  dft8<false>(xr, xi);
+  if constexpr (TWIN) twist_dft8_fwd(xr, xi);
+  else dft8<false>(xr, xi);
 #pragma unroll
   for (int e = TW0 ? 0 : 1; e < 8; e++) cmul<false>(xr[e], xi[e], twA[64 * e + lane]);
 #if FFT_T1_PERM
@@ -264,9 +344,11 @@ __device__ __forceinline__ void dft512_fwd_t(double (&xr)[8], double (&xi)[8], d
 }
 
 // the same with pass A's twiddles (this lane's 8, slot 0 included: the merged twist) held in registers
+template <bool TWIN = false>
 __device__ __forceinline__ void dft512_fwd_ra(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
                                               const double2 (&wa)[8], const double2* twB) {
-  dft8<false>(xr, xi);
+  if constexpr (TWIN) twist_dft8_fwd(xr, xi);
+  else dft8<false>(xr, xi);
 #pragma unroll
   for (int e = 0; e < 8; e++) cmul<false>(xr[e], xi[e], wa[e]);
 #pragma unroll
@@ -296,9 +378,11 @@ __device__ __forceinline__ void dft512_fwd_ra(double (&xr)[8], double (&xi)[8], 
 }
 
 // pass A and pass B twiddles both in registers (wb[0] unused)
+template <bool TWIN = false>
 __device__ __forceinline__ void dft512_fwd_rab(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
                                                const double2 (&wa)[8], const double2 (&wb)[8]) {
-  dft8<false>(xr, xi);
+  if constexpr (TWIN) twist_dft8_fwd(xr, xi);
+  else dft8<false>(xr, xi);
 #pragma unroll
   for (int e = 0; e < 8; e++) cmul<false>(xr[e], xi[e], wa[e]);
 #pragma unroll
@@ -359,10 +443,10 @@ __device__ __forceinline__ void dft512_inv_rb(double (&xr)[8], double (&xi)[8], 
   dft8<true>(xr, xi);
 }
 
-template <bool TW0 = false>
+template <bool TW0 = false, bool TWIN = false>
 __device__ __forceinline__ void dft512_fwd(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
                                            const double2* tw) {
-  dft512_fwd_t<TW0>(xr, xi, T, lane, tb, tw + TW_A, tw + TW_B);
+  dft512_fwd_t<TW0, TWIN>(xr, xi, T, lane, tb, tw + TW_A, tw + TW_B);
 }
 
 // inverse (no 1/M): device order in, natural order out — the forward's passes reversed

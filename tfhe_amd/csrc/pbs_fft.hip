@@ -47,8 +47,7 @@ __device__ __forceinline__ void fft_fwd_real(const double (&a)[16], double (&xr)
     xr[e] = a[e];
     xi[e] = a[e + 8];
   }
-  twist_slots<false>(xr, xi);
-  dft512_fwd<true>(xr, xi, T, lane, TBase(lane), tw);
+  dft512_fwd<true, true>(xr, xi, T, lane, TBase(lane), tw);  // the slot twist inside pass A (twist_dft8_fwd)
 }
 
 // inverse transform (no 1/M) + untwist: slot e -> coefficient 64 e + L (re), 64 (e + 8) + L (im)
@@ -445,13 +444,13 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
           xi[e] = (double)decomp_step(st[e + 8], 1u);
         }
       }
-      twist_slots<false>(xr, xi);
+      // the slot twist rides in pass A's twisted DFT8 (twist_dft8_fwd)
 #if FFT_PAIR_TWREG >= 2
-      dft512_fwd_rab(xr, xi, T, lane, tb, wa, wb);
+      dft512_fwd_rab<true>(xr, xi, T, lane, tb, wa, wb);
 #elif FFT_PAIR_TWREG
-      dft512_fwd_ra(xr, xi, T, lane, tb, wa, twB);
+      dft512_fwd_ra<true>(xr, xi, T, lane, tb, wa, twB);
 #else
-      dft512_fwd_t<true>(xr, xi, T, lane, tb, twA, twB);
+      dft512_fwd_t<true, true>(xr, xi, T, lane, tb, twA, twB);
 #endif
       if constexpr (!LDS_TW) glds_barrier();  // step g's chunk has landed
 #if FFT_MACPRIO
@@ -576,8 +575,7 @@ __device__ __forceinline__ void lat_cmux(FftLatShared& sh, const u64* __restrict
       xr[e] = (double)dg[e];
       xi[e] = (double)dg[e + 8];
     }
-    twist_slots<false>(xr, xi);
-    dft512_fwd<true>(xr, xi, sh.T[wave], lane, tb, sh.tw);
+    dft512_fwd<true, true>(xr, xi, sh.T[wave], lane, tb, sh.tw);
 #pragma unroll
     for (int e = 0; e < 8; e++) sh.F[wave][64 * e + lane] = make_double2(xr[e], xi[e]);
   }
