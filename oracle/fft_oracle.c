@@ -215,6 +215,10 @@ __attribute__((unused)) static void dft8_r4(or_c64 x[8], int inv) {
   for (int k = 0; k < 8; k++) x[k] = u[brv3[k]];
 }
 
+/* FFT_TDFT8 (default 0, = fft512.h): measured slower on the device, kept for its A/B build (make FFT_TDFT8=1 ...) */
+#ifndef FFT_TDFT8
+#define FFT_TDFT8 0
+#endif
 /* the N = 1024 forward's slot twist + pass A's DFT8 as one twisted DFT8 (round 5, = fft512.h twist_dft8_fwd): x(X) =
  * sum_e x_e X^e at the roots X_k = e^{i pi (1 + 4k)/16} of X^8 = i by a radix-2 split (X^8 - i = (X^4 - w)(X^4 + w), ...),
  * 12 butterflies a +- e^{i th} b each with b through the tangent / cotangent form and cos / sin th in the output fmas */
@@ -232,7 +236,7 @@ static void tbfly(or_c64* a, or_c64* b, double t, double sc, int cot) {
   a->re = fma(sc, ur, p.re); a->im = fma(sc, ui, p.im);
   b->re = fma(-sc, ur, p.re); b->im = fma(-sc, ui, p.im);
 }
-static void tdft8_fwd(or_c64 x[8]) {
+__attribute__((unused)) static void tdft8_fwd(or_c64 x[8]) {
   for (int e = 0; e < 4; e++) {
     const double ur = x[e + 4].re - x[e + 4].im, ui = x[e + 4].im + x[e + 4].re;
     const or_c64 p = x[e];
@@ -514,9 +518,18 @@ void or_fft_fwd(const double* a, uint32_t N, or_c64* out) {
   if (N != 2 * FFT_M) abort();
   const fft_tab* T = tab();
   or_c64 z[FFT_M];
+#if FFT_TDFT8
   for (int j = 0; j < FFT_M; j++) z[j] = (or_c64){a[j], a[j + FFT_M]};
   /* j = L + 64 e: the slot part zeta^{64 e} of the twist inside pass A's twisted DFT8, zeta^L in pass A's table */
   dft512_fwd_tab(z, out, T->twAm, 1, 1);
+#else
+  for (int j = 0; j < FFT_M; j++) { /* j = L + 64 e: slot constant zeta^{64 e} (e > 0), zeta^L in pass A */
+    const or_c64 v = {a[j], a[j + FFT_M]};
+    const int e = j >> 6;
+    z[j] = e ? cmul(v, T->twist[64 * e].re, T->twist[64 * e].im) : v;
+  }
+  dft512_fwd_tab(z, out, T->twAm, 1, 0);
+#endif
 }
 
 void or_fft_inv(const or_c64* in, uint32_t N, double* out) {

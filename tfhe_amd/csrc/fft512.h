@@ -228,9 +228,12 @@ __device__ __forceinline__ void twist_slots(double (&xr)[8], double (&xi)[8]);
 //   stage 3  roots +-e^(i pi/16), +-e^(i 9pi/16), +-e^(i 5pi/16), +-e^(i 13pi/16) -> X_0 X_4, X_2 X_6, X_1 X_5, X_3 X_7
 // Each of the 12 butterflies a +- e^(i th) b takes b through a tangent (or cotangent) form, u = (b.re - t b.im,
 // b.im + t b.re), and folds cos th (or sin th) into the two output fmas: 6 f64 instructions, 72 for the whole step
-// against 28 (7 slot cmuls) + 52 (DFT8) = 80.  Restated in oracle/fft_oracle.c:tdft8_fwd; 0 = twist, then DFT8.
+// against 28 (7 slot cmuls) + 52 (DFT8) = 80.  Measured SLOWER on MI355X (round 5, same box, three rounds: 24.76 vs 24.62
+// ms per 4096, profiles/r05c_ab_tdft8.txt: the three dependent fma stages and 3 spilled VGPRs cost more than the 24 f64
+// instructions saved), so 0 -- twist, then DFT8 -- is the default and the one oracle/fft_oracle.c restates (its tdft8_fwd
+// is kept for the A/B build only).
 #ifndef FFT_TDFT8
-#define FFT_TDFT8 1
+#define FFT_TDFT8 0
 #endif
 namespace tdft {
 constexpr double T8 = 0.41421356237309504880, C8 = 0.92387953251128675613;     // tan, cos (pi / 8)

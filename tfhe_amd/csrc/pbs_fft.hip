@@ -67,11 +67,24 @@ __device__ __forceinline__ int ms2048(u64 x) { return (int)((((x >> 52) + 1) >> 
 __device__ __forceinline__ u32 decomp_state(u64 x) { return ((u32)(x >> 32) + 1024u) >> 11; }
 // bmask = 1 below the top level, 0 at the top level
 // (W & 127) - 63 - b = st - (W & ~127): the digit is the old state minus the new one shifted back
+// FFT_DIG_MAD 1 (default since round 5): the digit as st - 128 st' in one v_mad_i32_i24 (st < 2^22, st' < 2^15 fit the
+// 24-bit operands): 4 VALU per digit instead of 5 (hipcc turns the multiply into a shift + subtract, hence the asm;
+// -128 is not a VOP3 inline constant on gfx9, so it rides in an SGPR)
+#ifndef FFT_DIG_MAD
+#define FFT_DIG_MAD 1
+#endif
 __device__ __forceinline__ int decomp_step(u32& st, u32 bmask) {
   const u32 b = __builtin_amdgcn_ubfe(st, 13, bmask);
   const u32 W = st + 63u + b;
+#if FFT_DIG_MAD
+  const u32 stn = W >> 7;
+  int d;
+  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(stn), "s"(-128), "v"(st));
+  st = stn;
+#else
   const int d = (int)(st - (W & ~127u));  // 5 VALU per digit with the bfe, add3 and shift
   st = W >> 7;
+#endif
   return d;
 }
 // the top level (b = 0, no next state): 3 VALU per digit
