@@ -341,6 +341,24 @@ __device__ __forceinline__ void load_step(const double2* __restrict__ bsk, int g
                                      (__attribute__((address_space(3))) void*)((char*)dst + blk * 1024), 16, 0, 0);
   }
 }
+// FFT_BUF_LDS 1 (default since round 5): the same level-step chunk through buffer_load_dwordx4 ... lds with the BSK as a
+// buffer resource: the per-load byte offset is an SGPR (soffset) and the lane offset one loop-invariant VGPR, so the
+// 24 loads of a CMUX cost no VALU (the global_load_lds form needs a 64-bit VALU address add per load)
+#ifndef FFT_BUF_LDS
+#define FFT_BUF_LDS 1
+#endif
+template <int NW>
+__device__ __forceinline__ void load_step_buf(__amdgpu_buffer_rsrc_t bsr, int g, double2* dst, int wave_s, int voff) {
+  const int i = g / 3, q = g - 3 * (g / 3);
+#pragma unroll
+  for (int u = 0; u < 32 / NW; u++) {
+    const int blk = wave_s * (32 / NW) + u;
+    const int c = blk >> 4;
+    const int soff = ((i * 6 + c * 3 + q) * (2 * M)) * (int)sizeof(double2) + (blk & 15) * 1024;  // < 2^31: BSK < 2 GB
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(bsr, (__attribute__((address_space(3))) void*)((char*)dst + blk * 1024),
+                                             16, voff, soff, 0, 0);
+  }
+}
 
 template <int CTS, bool WRITE_ACC, bool WRITE_BIG>
 __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kernel(
@@ -362,6 +380,12 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
   const int c_s = wave_s & 1;
   const int n_steps = 3 * n;
 
+#if FFT_BUF_LDS
+  // the BSK as a raw buffer (num_records = its byte size; gfx9 dword 3 = 0x00020000, as composable_kernel uses on gfx9)
+  const __amdgpu_buffer_rsrc_t bsr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)bsk, (short)0, n * 6 * 2 * M * (int)sizeof(double2), 0x00020000);
+  const int voff = lane * 16;
+#endif
   if constexpr (LDS_TW) {
     for (int q = threadIdx.x; q < 3 * M; q += 64 * NW) sh.tw[q] = tw_g[TW_A + q];
     load_step<NW>(bsk, 0, sh.K[0], wave_s, lane);
@@ -444,7 +468,11 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
       } else {
         // one buffer: every wave is done with step g - 1's chunk (the exchange's barriers order q = 0)
         if (q > 0) __syncthreads();
+#if FFT_BUF_LDS
+        load_step_buf<NW>(bsr, g, sh.K[0], wave_s, voff);
+#else
         load_step<NW>(bsk, g, sh.K[0], wave_s, lane);
+#endif
       }
       double xr[8], xi[8];
 #pragma unroll
