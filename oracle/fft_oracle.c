@@ -546,6 +546,19 @@ void or_fft_inv(const or_c64* in, uint32_t N, double* out) {
   }
 }
 
+/* The device's accumulator update (fft512.h torus_acc_add / torus_acc_add_wide, FFT_TORUS_NORINT, round 5): h =
+ * floor(x 2^-32), l = fma(-h, 2^32, x) (exact unless -2^32 < x < 0, where x + 2^32 rounds once), and the increment
+ * h 2^32 + rint(l) mod 2^64 -- rint(x) mod 2^64 except for that double rounding of tiny negative x.  The device takes
+ * rint(l) from the bits of l + 2^52 and h mod 2^32 from those of h + 1.5 2^52 (N = 1024) or of the exact split
+ * h - 2^32 floor(h 2^-32) + 1.5 2^52 (N = 2048); both are h mod 2^32 exactly, as computed here. */
+uint64_t or_f64_to_torus_dev(double x) {
+  const double h = floor(x * 0x1p-32);
+  const double l = fma(-h, 0x1p32, x);
+  const double hh = floor(h * 0x1p-32);
+  const double hm = fma(-hh, 0x1p32, h); /* exact, in [0, 2^32) */
+  return ((uint64_t)hm << 32) + (uint64_t)rint(l); /* rint(l) in [0, 2^32], the same as the bits of l + 2^52 */
+}
+
 /* round(x) (ties to even) mod 2^64; every step after rint is exact */
 uint64_t or_f64_to_torus(double x) {
   const double t = rint(x);
@@ -657,7 +670,9 @@ static void blind_rotate_fft_impl(const or_params* p, const or_c64* bsk_f, const
     }
     for (uint32_t j = 0; j <= k; j++) {
       or_fft_inv(O[j], N, res);
-      for (uint32_t f = 0; f < N; f++) acc[(size_t)j * N + f] += or_f64_to_torus(res[f]);
+      /* N = 2048: the device's rint-free update (FFT_TORUS_NORINT); N = 1024 keeps rint (FFT_TORUS_NORINT_1K 0) */
+      for (uint32_t f = 0; f < N; f++)
+        acc[(size_t)j * N + f] += N == 2048 ? or_f64_to_torus_dev(res[f]) : or_f64_to_torus(res[f]);
     }
     if (trace) memcpy(trace + (i + 1) * row, acc, row * 8);
   }

@@ -76,6 +76,8 @@ def lib():
         L.or_ksk_len.restype = ctypes.c_size_t
         L.or_f64_to_torus.restype = ctypes.c_uint64
         L.or_f64_to_torus.argtypes = [ctypes.c_double]
+        L.or_f64_to_torus_dev.restype = ctypes.c_uint64
+        L.or_f64_to_torus_dev.argtypes = [ctypes.c_double]
         _LIB = L
     return _LIB
 
@@ -307,6 +309,11 @@ def fft_inv(z) -> np.ndarray:
 
 def f64_to_torus(x: float) -> int:
     return int(lib().or_f64_to_torus(float(x)))
+
+
+def f64_to_torus_dev(x: float) -> int:
+    """the device's accumulator increment (fft512.h torus_acc_add): rint(x) mod 2^64 but for tiny negative x"""
+    return int(lib().or_f64_to_torus_dev(float(x)))
 
 
 def fft_twiddle(t: int, M: int) -> tuple:

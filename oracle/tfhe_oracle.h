@@ -246,6 +246,7 @@ void or_fft_fwd(const double* a, uint32_t N, or_c64* out);
 void or_fft_inv(const or_c64* in, uint32_t N, double* out);
 /* round(x) mod 2^64 (ties to even) */
 uint64_t or_f64_to_torus(double x);
+uint64_t or_f64_to_torus_dev(double x); /* the device's accumulator increment (round 5, see fft_oracle.c) */
 /* Fourier BSK: or_bsk_len/N polynomials x N/2 complex, scaled by 2^-log2(N/2) */
 void or_bsk_to_fourier(const or_params* p, const uint64_t* bsk, or_c64* bsk_f);
 /* acc_out: (k+1)*N native torus values.  lut: N values in the Z_p LUT encoding. */

@@ -83,6 +83,33 @@ def test_f64_to_torus_rounding(oracle_mod):
     assert f(2.0**63) == 2**63 and f(-(2.0**63)) == 2**63
 
 
+def test_device_accumulator_increment(oracle_mod):
+    """or_f64_to_torus_dev (the device's rint-free update, fft512.h torus_acc_add[_wide]): equal to rint(x) mod 2^64
+    for every |x| >= 2^32 and every x >= 0, and off by at most one for tiny negative x (x + 2^32 rounded once before
+    the integer rounding); the two bit-pattern words of the device form restated in Python agree with it."""
+    import struct
+    f, g = oracle_mod.f64_to_torus_dev, oracle_mod.f64_to_torus
+    rng = np.random.default_rng(0xACC)
+    xs = np.concatenate([rng.standard_normal(400) * 2.0 ** rng.integers(0, 106, 400),
+                         np.array([0.5, 1.5, 2.5, -0.5, -1.5, 2.0 ** 32 - 0.5, -(2.0 ** 32) + 0.5, 2.0 ** 63, -(2.0 ** 63),
+                                   2.0 ** 83 - 2.0 ** 31, -(2.0 ** 81.5), 2.0 ** 105, -(2.0 ** 105) + 2.0 ** 60])])
+    for x in xs.tolist():
+        if abs(x) >= 2.0 ** 32 or x >= 0:
+            assert f(x) == g(x), x
+        else:
+            assert (f(x) - g(x)) % 2 ** 64 in (0, 1, 2 ** 64 - 1), x
+
+        def bits(d):
+            return struct.unpack("<Q", struct.pack("<d", d))[0]
+        h = math.floor(x * 2.0 ** -32)
+        l = float(np.float64(x) - np.float64(h) * 2.0 ** 32)   # h 2^32 is exact: one rounding, as the fma
+        hh = math.floor(h * 2.0 ** -32)
+        hm = float(h - hh * 2 ** 32)
+        dev = ((bits(hm + (1.5 * 2.0 ** 52 - 1127219200.0)) << 32) + bits(l + 2.0 ** 52)) % 2 ** 64
+        assert dev == f(x), x
+    assert (f(-0.5 - 2.0 ** -30) - g(-0.5 - 2.0 ** -30)) % 2 ** 64 == 1   # the double-rounding case, restated
+
+
 def test_product_keygen_matches_oracle(oracle_mod):
     """tfhe_hip_keygen on the FFT64 preset: native-torus BSK bit-identical to or_keygen (host code)."""
     import tfhe_amd

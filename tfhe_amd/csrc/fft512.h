@@ -612,6 +612,42 @@ __device__ __forceinline__ u64 f64_to_torus(double x) {
   return ((u64)hm << 32) | (u64)(u32)l;
 }
 
+// FFT_TORUS_NORINT 1 (default since round 5): the accumulator update without the rint and without building the u64 from
+// two halves.  h = floor(x 2^-32), l = fma(-h, 2^32, x) (exact whenever |x| >= 2^32 or h = 0; for -2^32 < x < 0 it is
+// x + 2^32 rounded once), and the two words come straight out of doubles' bit patterns:
+//   l + 2^52                     bits = 0x43300000_00000000 + rint(l)        (rint(l) may be 2^32: the carry is kept)
+//   h + (1.5 2^52 - 0x43300000)  low word = (h - 0x43300000) mod 2^32       (|h| < 2^51 - 2^32)
+// acc += (hb << 32) + lb (two v_lshl_add_u64), the 0x43300000 offsets cancel mod 2^64.  The value is h 2^32 + rint(l):
+// rint(x) mod 2^64 exactly, except that a tiny negative x (|x| < 2^32) rounds twice (x + 2^32, then to an integer) --
+// oracle/fft_oracle.c:or_f64_to_torus_dev restates the same operations.  7 VALU per coefficient instead of 8 (P-GATE)
+// and 10 instead of 12 (P-FHEVM, below).
+#ifndef FFT_TORUS_NORINT
+#define FFT_TORUS_NORINT 1
+#endif
+// acc + (low word of d's bit pattern) << 32: a 32-bit add on acc's high word (no carry can come from below; hipcc
+// otherwise moves the word into the high half of a fresh pair for a 64-bit add -- v_lshl_add_u64 shifts by 0..4 only)
+__device__ __forceinline__ u64 add_hi_word(u64 acc, double d) {
+  const u32x2v a = __builtin_bit_cast(u32x2v, acc);
+  const u32x2v w = __builtin_bit_cast(u32x2v, d);
+  return __builtin_bit_cast(u64, (u32x2v){a.x, a.y + w.x});
+}
+// N = 1024 keeps the rint form (FFT_TORUS_NORINT_1K 0): the rint-free one measured 0.3 % slower on the P-GATE pair kernel
+// (24.19 vs 24.14 ms, profiles/r05f_ab_norint.txt) while it gains 0.3 % at N = 2048
+#ifndef FFT_TORUS_NORINT_1K
+#define FFT_TORUS_NORINT_1K 0
+#endif
+__device__ __forceinline__ u64 torus_acc_add(u64 acc, double x) {
+#if FFT_TORUS_NORINT && FFT_TORUS_NORINT_1K
+  const double h = __builtin_floor(x * 0x1p-32);
+  const double l = __builtin_fma(-h, 0x1p32, x);
+  const double lb = l + 0x1p52;
+  const double hb = h + (0x1.8p52 - 1127219200.0);  // 1.5 * 2^52 - 0x43300000, an exact double
+  return add_hi_word(acc, hb) + (u64)__double_as_longlong(lb);
+#else
+  return acc + f64_to_torus(x);
+#endif
+}
+
 // the same for any |x| < 2^115 (N = 2048 with 23-bit digits reaches |x| ~ 2^91, beyond the magic-number
 // step above): the high word comes off a second exact floor/fma split
 __device__ __forceinline__ u64 f64_to_torus_wide(double x) {
@@ -621,6 +657,21 @@ __device__ __forceinline__ u64 f64_to_torus_wide(double x) {
   const double hh = __builtin_floor(h * 0x1p-32);
   const double hm = __builtin_fma(-hh, 0x1p32, h);
   return ((u64)(u32)hm << 32) | (u64)(u32)l;
+}
+// torus_acc_add for |x| < 2^115 (FFT_TORUS_NORINT): h mod 2^32 off a second exact floor/fma split, then the same two
+// bit-pattern words
+__device__ __forceinline__ u64 torus_acc_add_wide(u64 acc, double x) {
+#if FFT_TORUS_NORINT
+  const double h = __builtin_floor(x * 0x1p-32);
+  const double l = __builtin_fma(-h, 0x1p32, x);
+  const double lb = l + 0x1p52;
+  const double hh = __builtin_floor(h * 0x1p-32);
+  const double hm = __builtin_fma(-hh, 0x1p32, h);    // h mod 2^32, exact, in [0, 2^32)
+  const double hb = hm + (0x1.8p52 - 1127219200.0);
+  return add_hi_word(acc, hb) + (u64)__double_as_longlong(lb);
+#else
+  return acc + f64_to_torus_wide(x);
+#endif
 }
 
 }  // namespace fftk

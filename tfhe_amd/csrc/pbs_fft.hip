@@ -529,8 +529,8 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
     twist_slots<true>(xr, xi);
 #pragma unroll
     for (int e = 0; e < 8; e++) {
-      acc[e] += f64_to_torus(xr[e]);
-      acc[e + 8] += f64_to_torus(xi[e]);
+      acc[e] = torus_acc_add(acc[e], xr[e]);
+      acc[e + 8] = torus_acc_add(acc[e + 8], xi[e]);
     }
   }
 
@@ -651,8 +651,8 @@ __device__ __forceinline__ void lat_cmux(FftLatShared& sh, const u64* __restrict
     u64* acc = sh.A[wave];
 #pragma unroll
     for (int e = 0; e < 8; e++) {
-      acc[64 * e + lane] += f64_to_torus(xr[e]);
-      acc[64 * (e + 8) + lane] += f64_to_torus(xi[e]);
+      acc[64 * e + lane] = torus_acc_add(acc[64 * e + lane], xr[e]);
+      acc[64 * (e + 8) + lane] = torus_acc_add(acc[64 * (e + 8) + lane], xi[e]);
     }
   }
   __syncthreads();

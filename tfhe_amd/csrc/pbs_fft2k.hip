@@ -255,8 +255,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
       fft1k_inv(xr, xi, area, lane, sh.ta, tb);
 #pragma unroll
       for (int e = 0; e < 16; e++) {
-        acc[e] += f64_to_torus_wide(xr[e]);
-        acc[e + 16] += f64_to_torus_wide(xi[e]);
+        acc[e] = torus_acc_add_wide(acc[e], xr[e]);
+        acc[e + 16] = torus_acc_add_wide(acc[e + 16], xi[e]);
       }
     }
   };
