@@ -36,4 +36,6 @@ find gpurun_out/prof_${T} -name "*kernel_stats.csv" -exec cp {} gpurun_out/${T}_
 pmc fetch FETCH_SIZE || exit 1
 pmc write WRITE_SIZE || exit 1
 BATCH=512 python tools/roofline_summary.py $T gpurun_out/${T}_kernel_stats.csv /dev/null gpurun_out/${T}_pmc_fetch.csv gpurun_out/${T}_pmc_write.csv gpurun_out/${T}_roofline.json || { echo "summary failed"; exit 1; }
+# the raw rocprofv3 directories (per-launch traces of 918 x 3 launches) stay on the box: gpurun copies back <= 64 MiB
+rm -rf gpurun_out/prof_${T0}* gpurun_out/pmc_*_${T0}*
 echo ALL_OK

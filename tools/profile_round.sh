@@ -40,4 +40,5 @@ if [ "$BENCH" = "1" ]; then
   timeout -k 10 300 python bench.py $B > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { echo "bench failed"; tail -30 gpurun_out/bench_${TAG}.err; exit 1; }
   cat gpurun_out/bench_${TAG}.json
 fi
+rm -rf gpurun_out/prof_${TAG} gpurun_out/pmc_*_${TAG}   # raw rocprofv3 directories: the summaries above are kept
 echo ALL_OK
