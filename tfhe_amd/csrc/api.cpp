@@ -893,7 +893,16 @@ int tfhe_hip_load_ms_key(tfhe_ctx* c, const uint64_t* zeros, uint32_t count, dou
     return fail(TFHE_HIP_EINVAL, "load_ms_key: count %u / bound / r_sigma / variance out of range", count);
   std::lock_guard<std::mutex> lk(c->mu);
   c->ms_count = 0;
-  const size_t bytes = (size_t)count * (c->p.n + 1) * 8;
+  // two layouts in one allocation: rows [count][n+1] (the add of the chosen zero) then the element-major
+  // transpose [n+1][zp] the scan reads 64 zeros per load from (pbs_kernels.h: ms_zeros_pitch)
+  const size_t dim = c->p.n + 1, zp = tfhe::ms_zeros_pitch(count);
+  const size_t bytes = (count * dim + dim * zp) * 8;
+  std::vector<uint64_t> tr;
+  if (count) {
+    tr.assign(dim * zp, 0);
+    for (size_t z = 0; z < count; z++)
+      for (size_t i = 0; i < dim; i++) tr[i * zp + z] = zeros[z * dim + i];
+  }
   for (auto& s : c->sh) {
     DeviceGuard g(s.device);
     HIP_TRY(hipStreamSynchronize(s.stream));
@@ -902,7 +911,8 @@ int tfhe_hip_load_ms_key(tfhe_ctx* c, const uint64_t* zeros, uint32_t count, dou
     s.d_ms_zeros = nullptr;
     if (!count) continue;
     HIP_TRY(hipMalloc(&s.d_ms_zeros, bytes));
-    HIP_TRY(hipMemcpy(s.d_ms_zeros, zeros, bytes, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s.d_ms_zeros, zeros, count * dim * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s.d_ms_zeros + count * dim, tr.data(), tr.size() * 8, hipMemcpyHostToDevice));
   }
   c->ms_count = count;
   c->ms_bound = bound;

@@ -87,7 +87,10 @@ hipError_t launch_pks_gemm_mfma(const u64* lwes, size_t count, int in_dim, int b
                                 const void* planes, void* A0, void* A1, u64* T, hipStream_t s);
 hipError_t launch_pks_pack_mfma(const u64* lwes, size_t count, int in_dim, int base_log, int L, int k, int N, int lpg,
                                 const void* planes, void* A0, void* A1, u64* T, u64* out, hipStream_t s);
-// modulus-switch noise reduction (ms_reduce.hip), in place on B x (n+1); picks (device, nullable)
+// modulus-switch noise reduction (ms_reduce.hip), in place on B x (n+1); picks (device, nullable).
+// `zeros` holds the rows [count][n+1] followed by their element-major transpose [n+1][ms_zeros_pitch(count)]
+// (padding columns zero).
+inline size_t ms_zeros_pitch(size_t count) { return (count + 63) / 64 * 64; }
 hipError_t launch_ms_reduce(u64* lwe, size_t B, int n, const u64* zeros, int count, int log2_2N, double bound,
                             double r_sigma, double var128, int* picks, hipStream_t s);
 hipError_t launch_ntt2048_inv(u64* polys, size_t count, const u64* tw, u64 ninv, hipStream_t s);
