@@ -674,6 +674,24 @@ __device__ __forceinline__ u64 torus_acc_add_wide(u64 acc, double x) {
 #endif
 }
 
+// torus_acc_add_wide of x = y * 2^32, given y: the N = 2048 keys' spectra carry the factor 2^-32 (launch_bsk_to_fourier2k
+// scales by 2^-42 instead of 2^-10) and every later step -- the MAC's fmas, the inverse transform's adds, multiplies and
+// fmas -- rounds a power-of-two multiple of its exact value, so y is x * 2^-32 bit for bit.  Then h = floor(y) directly,
+// and y - h = 2^-32 RN(x - 2^32 h) (the same scaling argument), so (y - h) + 2^20 = 2^-32 RN(l + 2^52): the same low
+// word as lb above (ulp 2^-32 at 2^20), the high word 0x41300000 instead of 0x43300000 (hb's constant compensates), one
+// f64 operation (the x * 2^-32) fewer per coefficient.  The oracle keeps the x form.
+// The high word: h is an integer, so fract(h 2^-32) = (h mod 2^32) 2^-32 exactly (granularity 2^-32, any sign), and
+// fract + 2^20 carries h mod 2^32 in its low word; the two 0x41300000 high words cost one v_add3_u32 operand.
+// Six f64 operations per coefficient against eight.
+__device__ __forceinline__ u64 torus_acc_add_wide_y(u64 acc, double y) {
+  const double h = __builtin_floor(y);
+  const double lb = (y - h) + 0x1p20;
+  const double hb = __builtin_amdgcn_fract(h * 0x1p-32) + 0x1p20;
+  const u32x2v a = __builtin_bit_cast(u32x2v, acc);
+  const u32x2v w = __builtin_bit_cast(u32x2v, hb);
+  return __builtin_bit_cast(u64, (u32x2v){a.x, a.y + w.x - 0x41300000u}) + (u64)__double_as_longlong(lb);
+}
+
 }  // namespace fftk
 
 // cos / sin (2 pi t / m): fixed series in plain double, octant-reduced (the oracle's or_fft_twiddle)

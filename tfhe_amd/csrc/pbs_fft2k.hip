@@ -75,6 +75,11 @@ __device__ __forceinline__ void load_ta(double2* ta, const double2* __restrict__
 #ifndef F1_ROT_UNIFORM
 #define F1_ROT_UNIFORM 1
 #endif
+// F1_Y32 1 (round 5): the keys' spectra carry 2^-32 (scale 2^-42 at conversion), so the inverse transform returns
+// y = x * 2^-32 bit for bit and the accumulator update starts at floor(y) (fft512.h: torus_acc_add_wide_y)
+#ifndef F1_Y32
+#define F1_Y32 1
+#endif
 __device__ __forceinline__ void rotate_digits(const u64 (&v)[32], int a, int lane, double2* area, double (&xr)[16],
                                               double (&xi)[16]) {
   u64* Tu = (u64*)area;
@@ -255,8 +260,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
       fft1k_inv(xr, xi, area, lane, sh.ta, tb);
 #pragma unroll
       for (int e = 0; e < 16; e++) {
+#if F1_Y32
+        acc[e] = torus_acc_add_wide_y(acc[e], xr[e]);
+        acc[e + 16] = torus_acc_add_wide_y(acc[e + 16], xi[e]);
+#else
         acc[e] = torus_acc_add_wide(acc[e], xr[e]);
         acc[e + 16] = torus_acc_add_wide(acc[e + 16], xi[e]);
+#endif
       }
     }
   };
@@ -398,7 +408,7 @@ bool fft2k_slot_constants_ok() {
 hipError_t launch_bsk_to_fourier2k(const u64* bsk_std, double* bsk_f, size_t polys, const double* tw, hipStream_t s) {
   if (polys == 0) return hipSuccess;
   hipLaunchKernelGGL(fft1k::fwd2k_kernel, dim3((unsigned)polys), dim3(64), 0, s, bsk_std, (double2*)bsk_f,
-                     (const double2*)tw, 0x1p-10);
+                     (const double2*)tw, F1_Y32 ? 0x1p-42 : 0x1p-10);
   return hipGetLastError();
 }
 
