@@ -670,9 +670,8 @@ static void blind_rotate_fft_impl(const or_params* p, const or_c64* bsk_f, const
     }
     for (uint32_t j = 0; j <= k; j++) {
       or_fft_inv(O[j], N, res);
-      /* N = 2048: the device's rint-free update (FFT_TORUS_NORINT); N = 1024 keeps rint (FFT_TORUS_NORINT_1K 0) */
-      for (uint32_t f = 0; f < N; f++)
-        acc[(size_t)j * N + f] += N == 2048 ? or_f64_to_torus_dev(res[f]) : or_f64_to_torus(res[f]);
+      /* the device's rint-free update at both N (fft512.h torus_acc_add_y / torus_acc_add_wide_y, round 5) */
+      for (uint32_t f = 0; f < N; f++) acc[(size_t)j * N + f] += or_f64_to_torus_dev(res[f]);
     }
     if (trace) memcpy(trace + (i + 1) * row, acc, row * 8);
   }

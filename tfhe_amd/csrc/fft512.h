@@ -658,6 +658,18 @@ __device__ __forceinline__ u64 f64_to_torus_wide(double x) {
   const double hm = __builtin_fma(-hh, 0x1p32, h);
   return ((u64)(u32)hm << 32) | (u64)(u32)l;
 }
+// torus_acc_add of x = y * 2^32 (|x| < 2^83), given y: the N = 1024 keys' spectra carry 2^-32 (bsk_to_fourier_kernel
+// scales by 2^-41, FFT_Y32) and, as for torus_acc_add_wide_y below, the MAC and the inverse transform then return
+// x * 2^-32 bit for bit.  h = floor(y), (y - h) + 2^20 = 2^-32 RN(l + 2^52) (low word rint(l), high word 0x41300000),
+// h + 1.5 2^52 - 0x41300000 (low word h - 0x41300000 mod 2^32): the rint-free update above, bit for bit, in four f64
+// operations instead of five (the oracle's or_f64_to_torus_dev)
+__device__ __forceinline__ u64 torus_acc_add_y(u64 acc, double y) {
+  const double h = __builtin_floor(y);
+  const double lb = (y - h) + 0x1p20;
+  const double hb = h + (0x1.8p52 - 1093664768.0);  // 1.5 * 2^52 - 0x41300000
+  return add_hi_word(acc, hb) + (u64)__double_as_longlong(lb);
+}
+
 // torus_acc_add for |x| < 2^115 (FFT_TORUS_NORINT): h mod 2^32 off a second exact floor/fma split, then the same two
 // bit-pattern words
 __device__ __forceinline__ u64 torus_acc_add_wide(u64 acc, double x) {

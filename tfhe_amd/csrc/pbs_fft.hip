@@ -106,7 +106,17 @@ __device__ __forceinline__ void mac_next(double& re, double& im, double dr, doub
 }
 
 // ---------------------------------------------------------------------------------------------
-// BSK conversion: one wavefront per polynomial; [i][r][j] order kept, 512 complex natural, x 2^-9
+// BSK conversion: one wavefront per polynomial; [i][r][j] order kept, 512 complex natural, x 2^-9 (x 2^-41 with
+// FFT_Y32: the blind rotations then update their accumulators from y = x 2^-32, fft512.h torus_acc_add_y)
+#ifndef FFT_Y32
+#define FFT_Y32 1
+#endif
+constexpr double BSK_SCALE = FFT_Y32 ? 0x1p-41 : 0x1p-9;
+#if FFT_Y32
+#define ACC_ADD torus_acc_add_y
+#else
+#define ACC_ADD torus_acc_add
+#endif
 __global__ __launch_bounds__(64) void bsk_to_fourier_kernel(const u64* __restrict__ bsk_std,
                                                             double2* __restrict__ bsk_f,
                                                             const double2* __restrict__ tw) {
@@ -121,7 +131,7 @@ __global__ __launch_bounds__(64) void bsk_to_fourier_kernel(const u64* __restric
   const size_t j = q % 2, r = (q / 2) % 6, i = q / 12;  // device layout [i][c*3 + (2 - l)][j]
   double2* dst = bsk_f + ((i * 6 + (r / 3) * 3 + (2 - r % 3)) * 2 + j) * M;
 #pragma unroll
-  for (int e = 0; e < 8; e++) dst[64 * e + lane] = make_double2(xr[e] * 0x1p-9, xi[e] * 0x1p-9);
+  for (int e = 0; e < 8; e++) dst[64 * e + lane] = make_double2(xr[e] * BSK_SCALE, xi[e] * BSK_SCALE);
 }
 
 // natural-order transforms for the parity tests (one wavefront per polynomial)
@@ -529,8 +539,8 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
     twist_slots<true>(xr, xi);
 #pragma unroll
     for (int e = 0; e < 8; e++) {
-      acc[e] = torus_acc_add(acc[e], xr[e]);
-      acc[e + 8] = torus_acc_add(acc[e + 8], xi[e]);
+      acc[e] = ACC_ADD(acc[e], xr[e]);
+      acc[e + 8] = ACC_ADD(acc[e + 8], xi[e]);
     }
   }
 
@@ -651,8 +661,8 @@ __device__ __forceinline__ void lat_cmux(FftLatShared& sh, const u64* __restrict
     u64* acc = sh.A[wave];
 #pragma unroll
     for (int e = 0; e < 8; e++) {
-      acc[64 * e + lane] = torus_acc_add(acc[64 * e + lane], xr[e]);
-      acc[64 * (e + 8) + lane] = torus_acc_add(acc[64 * (e + 8) + lane], xi[e]);
+      acc[64 * e + lane] = ACC_ADD(acc[64 * e + lane], xr[e]);
+      acc[64 * (e + 8) + lane] = ACC_ADD(acc[64 * (e + 8) + lane], xi[e]);
     }
   }
   __syncthreads();
