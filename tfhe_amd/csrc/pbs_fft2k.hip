@@ -38,6 +38,15 @@ __device__ __forceinline__ int dig23(u32 hi) {
   // there), the mod 2^23 is the u32 wrap after >> 9 -- 3 VALU instead of 5, the same value
   return (int)((hi + (256u + (0x3FFFFFu << 9))) >> 9) - 0x3FFFFF;
 }
+// -dig23(hi) in 2 VALU: dig23(h) = ceil((h - 255) / 512) in the signed reading of h with the digit range
+// (-2^22, 2^22], so -dig23(h) = floor((255 - h) / 512) = (int)(255 - h) >> 9 (the i32 wrap of 255 - h lands exactly
+// the tie h in [2^31 - 256, 2^31 + 256) on -2^22); checked for all 2^32 words.  With F1_NEGDIG the transforms run on
+// the negated digits against negated key spectra (launch_bsk_to_fourier2k), and every product of the MAC -- digit
+// term times key term -- is the same double, so the accumulators do not change by a bit.
+__device__ __forceinline__ int dig23_neg(u32 hi) { return (int)(255u - hi) >> 9; }
+#ifndef F1_NEGDIG
+#define F1_NEGDIG 1
+#endif
 typedef __attribute__((address_space(3))) u64 lds_u64;
 #ifndef F1_KPF
 #define F1_KPF 0
@@ -110,7 +119,11 @@ __device__ __forceinline__ void rotate_digits(const u64 (&v)[32], int a, int lan
     const u64 M = (u64)(long long)m32;
     const u64 x = ((const lds_u64*)(uintptr_t)(rb + (__builtin_amdgcn_ubfe(wmask, e, 1) << 14)))[64 * e];
     const u64 y = (x ^ M) - (v[e] + M);
+#if F1_NEGDIG
+    const double d = (double)dig23_neg((u32)(y >> 32));
+#else
     const double d = (double)dig23((u32)(y >> 32));
+#endif
     if (e < 16) xr[e] = d;
     else xi[e - 16] = d;
   }
@@ -130,7 +143,7 @@ __device__ __forceinline__ void rotate_digits(const u64 (&v)[32], int a, int lan
     const u64 x = ((const lds_u64*)(uintptr_t)(wrap ? a1 : a0))[64 * e];
     const u64 m = 0ull - (u64)(neg0 != wrap);  // all ones iff negated
     const u64 y = ((x ^ m) - m) - v[e];
-    const double d = (double)dig23((u32)(y >> 32));
+    const double d = (double)(F1_NEGDIG ? dig23_neg((u32)(y >> 32)) : dig23((u32)(y >> 32)));
     if (e < 16) xr[e] = d;
     else xi[e - 16] = d;
   }
@@ -408,7 +421,7 @@ bool fft2k_slot_constants_ok() {
 hipError_t launch_bsk_to_fourier2k(const u64* bsk_std, double* bsk_f, size_t polys, const double* tw, hipStream_t s) {
   if (polys == 0) return hipSuccess;
   hipLaunchKernelGGL(fft1k::fwd2k_kernel, dim3((unsigned)polys), dim3(64), 0, s, bsk_std, (double2*)bsk_f,
-                     (const double2*)tw, F1_Y32 ? 0x1p-42 : 0x1p-10);
+                     (const double2*)tw, (F1_NEGDIG ? -1.0 : 1.0) * (F1_Y32 ? 0x1p-42 : 0x1p-10));
   return hipGetLastError();
 }
 
