@@ -110,6 +110,50 @@ def test_device_accumulator_increment(oracle_mod):
     assert (f(-0.5 - 2.0 ** -30) - g(-0.5 - 2.0 ** -30)) % 2 ** 64 == 1   # the double-rounding case, restated
 
 
+def test_scaled_accumulator_update_forms(oracle_mod):
+    """Round 5 (FFT_Y32 / F1_Y32): the keys' spectra carry 2^-32, so the inverse returns y = x 2^-32 and the device
+    updates from y (fft512.h torus_acc_add_y at N = 1024, torus_acc_add_wide_y at N = 2048).  Restated here in IEEE
+    double steps (numpy float64, one rounding per operation): both forms give or_f64_to_torus_dev(x) bit for bit,
+    the wide one for every |x| < 2^96 (P-FHEVM reaches ~2^91), the N = 1024 one for |x| < 2^83 (P-GATE: 2^81.6)."""
+    import struct
+    f = oracle_mod.f64_to_torus_dev
+    f64 = np.float64
+
+    def bits(d):
+        return struct.unpack("<Q", struct.pack("<d", float(d)))[0]
+    rng = np.random.default_rng(0x5CA1ED)
+    xs = np.concatenate([rng.standard_normal(600) * 2.0 ** rng.integers(0, 96, 600),
+                         rng.integers(-2 ** 62, 2 ** 62, 100).astype(np.float64) + 0.5,
+                         np.array([0.0, -0.0, 0.5, -0.5, 1.5, -1.5, 2.0 ** 32 - 0.5, -(2.0 ** 32) + 0.5, 2.0 ** 52,
+                                   -(2.0 ** 52) - 1.0, 2.0 ** 63, -(2.0 ** 63), 2.0 ** 64 - 2.0 ** 11, 2.0 ** 80 + 2.0 ** 31,
+                                   -(2.0 ** 81.5), 2.0 ** 95, -(2.0 ** 95) + 2.0 ** 50, -0.5 - 2.0 ** -30])])
+    acc = 0x0123456789ABCDEF
+    for x in xs.tolist():
+        y = f64(x) * f64(2.0 ** -32)                       # exact: what the scaled pipeline returns
+        h = np.floor(y)
+        lb = (y - h) + f64(2.0 ** 20)
+        want = (acc + f(x)) % 2 ** 64
+        hb = (h * f64(2.0 ** -32) - np.floor(h * f64(2.0 ** -32))) + f64(2.0 ** 20)   # fract(h 2^-32) + 2^20
+        hi = ((bits(hb) & 0xFFFFFFFF) - 0x41300000) % 2 ** 32
+        assert (acc + (hi << 32) + bits(lb)) % 2 ** 64 == want, x
+        if abs(x) < 2.0 ** 83:
+            hb1 = h + f64(1.5 * 2.0 ** 52 - 1093664768.0)
+            assert (acc + ((bits(hb1) & 0xFFFFFFFF) << 32) + bits(lb)) % 2 ** 64 == want, x
+
+
+def test_negated_digit_form():
+    """F1_NEGDIG (pbs_fft2k.hip dig23_neg): (int)(255 - h) >> 9 == -dig23(h) for the high word h of the rotated
+    difference (checked on the device build for all 2^32 words; here on every 2^20-th word, the ties and the wrap)."""
+    h = np.concatenate([np.arange(0, 2 ** 32, 2 ** 12, dtype=np.uint64),
+                        np.arange(2 ** 31 - 1024, 2 ** 31 + 1024, dtype=np.uint64),
+                        np.arange(0, 1024, dtype=np.uint64), np.arange(2 ** 32 - 1024, 2 ** 32, dtype=np.uint64),
+                        (np.arange(0, 2 ** 23, dtype=np.uint64) << np.uint64(9)) + np.uint64(256)]) % 2 ** 32
+    h = h.astype(np.uint32)
+    dig = ((h + np.uint32(256 + (0x3FFFFF << 9))) >> np.uint32(9)).astype(np.int64) - 0x3FFFFF
+    neg = (np.uint32(255) - h).view(np.int32) >> 9
+    assert np.array_equal(neg.astype(np.int64), -dig)
+
+
 def test_product_keygen_matches_oracle(oracle_mod):
     """tfhe_hip_keygen on the FFT64 preset: native-torus BSK bit-identical to or_keygen (host code)."""
     import tfhe_amd
