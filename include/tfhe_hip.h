@@ -188,9 +188,7 @@ int tfhe_hip_load_keys_device(tfhe_ctx* ctx, const uint64_t* d_bsk, size_t bsk_l
  * count = 0 disables).  Before each blind rotation the ciphertext gets the one zero whose
  * measure |E[err]| + r_sigma * sd(err) of the switch to 2N is best (tfhe-rs 1.x
  * improve_lwe_ciphertext_modulus_switch_noise_for_binary_key; exact rule in oracle/tfhe_oracle.h).
- * EUNSUPPORTED for order 0 parameter sets.  Each device keeps the zeros twice: the rows and an
- * element-major transpose the one-wave-per-ciphertext scan reads 64 zeros per load from
- * (2 x count x (n+1) x 8 bytes, 21.6 MB at P-FHEVM). */
+ * EUNSUPPORTED for order 0 parameter sets. */
 int tfhe_hip_load_ms_key(tfhe_ctx* ctx, const uint64_t* zeros, uint32_t count, double bound, double r_sigma,
                          double input_variance);
 /* Stage-level: the reduction alone on B small-key ciphertexts (B x (n+1)); picks (nullable, B
