@@ -84,6 +84,9 @@ __device__ __forceinline__ void load_ta(double2* ta, const double2* __restrict__
 #ifndef F1_ROT_UNIFORM
 #define F1_ROT_UNIFORM 1
 #endif
+#ifndef F1_ROT_FOLD
+#define F1_ROT_FOLD 1
+#endif
 // F1_Y32 1 (round 5): the keys' spectra carry 2^-32 (scale 2^-42 at conversion), so the inverse transform returns
 // y = x * 2^-32 bit for bit and the accumulator update starts at floor(y) (fft512.h: torus_acc_add_wide_y)
 #ifndef F1_Y32
@@ -118,10 +121,16 @@ __device__ __forceinline__ void rotate_digits(const u64 (&v)[32], int a, int lan
     asm("s_bfe_i32 %0, %1, %2" : "=s"(m32) : "s"(mbits), "i"(e | (1 << 16)));
     const u64 M = (u64)(long long)m32;
     const u64 x = ((const lds_u64*)(uintptr_t)(rb + (__builtin_amdgcn_ubfe(wmask, e, 1) << 14)))[64 * e];
+#if F1_NEGDIG && F1_ROT_FOLD
+    // 255 - hi(y) = hi(~y) + 256 = hi((v + M + 2^40 - 1) - (x ^ M)): the offset rides in the scalar M, so the negated
+    // digit is one arithmetic shift of the high word (one VALU fewer per coefficient, the same value)
+    const u64 Mz = M + ((1ull << 40) - 1);
+    const double d = (double)((int)(u32)(((v[e] + Mz) - (x ^ M)) >> 32) >> 9);
+#elif F1_NEGDIG
     const u64 y = (x ^ M) - (v[e] + M);
-#if F1_NEGDIG
     const double d = (double)dig23_neg((u32)(y >> 32));
 #else
+    const u64 y = (x ^ M) - (v[e] + M);
     const double d = (double)dig23((u32)(y >> 32));
 #endif
     if (e < 16) xr[e] = d;
