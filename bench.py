@@ -58,6 +58,7 @@ PBS_BYTES_PER_PBS = 103_303_024                           # whole PBS incl. KSK 
 # P-FHEVM blind rotate: BSK 918 x 2 x 2 x 2048 x 8 + small LWE in 919 x 8 + LUT 2048 x 8 + big LWE out 2049 x 8
 BR_BYTES_PER_PBS_FHEVM = 60_162_048 + 7_352 + 16_384 + 16_392
 FHEVM_MM = 16                                            # message 2 bits x carry 2 bits
+C3_MASK = 0b10110010                                     # --config c3: bits bootstrapped with the NOT LUT
 HBM_PEAK_GBS = 8000.0
 
 
@@ -165,7 +166,7 @@ def host_cores() -> tuple:
 
 
 def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int, preset: int = 0,
-                 lut_host: np.ndarray = None):
+                 lut_host: np.ndarray = None, lut_idx: np.ndarray = None):
     """Oracle PBS on host cores over `sample` ciphertexts of the same batch (same keys)."""
     from oracle import oracle as O
     prm = O.params(preset)
@@ -176,14 +177,16 @@ def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int
     else:
         keys.bsk_ntt
     log(f"oracle keys in {time.time() - t:.1f}s")
-    lut = O.lut_constant(1024, O.MU)[None] if lut_host is None else lut_host[None]
+    lut = O.lut_constant(1024, O.MU)[None] if lut_host is None else lut_host.reshape(-1, prm.N)
     sel = cts[:sample]
-    O.pbs_batch(prm, keys, sel[: max(1, threads // 4)], lut, threads=threads)  # warm tables
+    idx = lut_idx[:sample] if lut_idx is not None else None
+    w = max(1, threads // 4)
+    O.pbs_batch(prm, keys, sel[:w], lut, idx[:w] if idx is not None else None, threads=threads)  # warm tables
     t = time.time()
-    O.pbs_batch(prm, keys, sel[:1], lut, threads=1)  # single-thread latency of one PBS
+    O.pbs_batch(prm, keys, sel[:1], lut, idx[:1] if idx is not None else None, threads=1)  # one PBS, one thread
     lat_ms = (time.time() - t) * 1e3
     t = time.time()
-    ref = O.pbs_batch(prm, keys, sel, lut, threads=threads)
+    ref = O.pbs_batch(prm, keys, sel, lut, idx, threads=threads)
     dt = time.time() - t
     exact = bool(np.array_equal(ref, gpu_out[:sample]))
     digest = {"bitexact_pbs": sample, "gpu_sha256": hashlib.sha256(np.ascontiguousarray(gpu_out[:sample])).hexdigest(),
@@ -218,6 +221,10 @@ def main() -> int:
                     help="gate_fft (default) = the BASELINE metric on the FFT64 transform (P-GATE, tfhe-rs's f64-FFT "
                          "external product over the native torus); gate = P-GATE on the Goldilocks NTT transform; "
                          "fhevm / fhevm_fft = production fhEVM parameters on the NTT / FFT64 transform (secondary line)")
+    ap.add_argument("--config", choices=["metric", "c3"], default="metric",
+                    help="metric (default) = BASELINE.json's headline PBS line; c3 = BASELINE.json configs[2]: --batch "
+                         "FheUint8 ciphertexts, each bit bootstrapped with its own LUT (lut_index = bit position): "
+                         "8 x batch PBS in ONE multi-LUT launch per step (P-GATE presets only)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses device 0 (with --dist-backend gloo)")
     args = ap.parse_args()
@@ -234,7 +241,10 @@ def main() -> int:
     torch.cuda.set_device(dev)
     # a process group whenever a launcher set one up: N > 1, or torch.distributed.run with one rank (the 1-GPU
     # rehearsal of the RCCL path: key broadcast, barriers and the max-over-ranks all_reduce on a world-1 communicator)
-    dist_on = world > 1 or ("RANK" in os.environ and "MASTER_ADDR" in os.environ)
+    # (a launcher = torchrun's env: WORLD_SIZE plus LOCAL_RANK or TORCHELASTIC_RUN_ID; a scheduler that only exports
+    # RANK / MASTER_ADDR does not turn a plain single-GPU run into an env:// rendezvous -- ADVICE r5)
+    launched = "WORLD_SIZE" in os.environ and ("LOCAL_RANK" in os.environ or "TORCHELASTIC_RUN_ID" in os.environ)
+    dist_on = world > 1 or launched
     if dist_on:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -243,6 +253,11 @@ def main() -> int:
 
     fhevm = args.preset in ("fhevm", "fhevm_fft")
     fft = args.preset in ("gate_fft", "fhevm_fft")
+    c3 = args.config == "c3"
+    if c3 and fhevm:
+        ap.error("--config c3 is the P-GATE FheUint8 workload (BASELINE.json configs[2]); use --preset gate_fft or gate")
+    if c3 and args.global_batch:
+        ap.error("--config c3 runs weak scaling only (--batch FheUint8 per GPU)")
     preset_id = {"gate": tfhe_amd.PRESET_GATE, "gate_fft": tfhe_amd.PRESET_GATE_FFT, "fhevm": tfhe_amd.PRESET_FHEVM,
                  "fhevm_fft": tfhe_amd.PRESET_FHEVM_FFT}[args.preset]
     params = tfhe_amd.Params.preset(preset_id)
@@ -253,6 +268,9 @@ def main() -> int:
         B = hi - lo
     else:
         lo, B = rank * args.batch, args.batch
+    n_ct = B                 # ciphertexts of the workload (FheUint8 values under --config c3)
+    if c3:                   # 8 bit-ciphertexts per FheUint8: the PBS batch of the one launch
+        lo, B = 8 * lo, 8 * B
 
     # ---- key set: generated on rank 0, broadcast once over RCCL ---------------------------------
     t = time.time()
@@ -289,17 +307,28 @@ def main() -> int:
         msgs = (gm if strong else rng.integers(0, FHEVM_MM, B)).astype(np.uint64)
         cts = ck.encrypt(msgs, FHEVM_MM, seed=INPUT_SEED + 1, stream0=lo)
         lut_host = eng.generate_accumulator(lambda m: m, FHEVM_MM)
+    elif c3:
+        # n_ct FheUint8 values, LSB first; bit j bootstrapped with LUT j (gate LUT or its negation, per C3_MASK):
+        # the FheUint8.map_bits workload of tests/test_gpu_configs.py::test_c3_fheuint8_lut_eval_4096
+        vals = (gm if strong else rng.integers(0, 256, n_ct)).astype(np.uint64)
+        bits = ((vals[:, None] >> np.arange(8, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool).reshape(-1)
+        cts = ck.encrypt_bool(bits, seed=INPUT_SEED + 1, stream0=lo)
+        gate = eng.gate_lut()
+        inv = (np.uint64(0) - gate.astype(np.uint64)) % np.uint64(0xFFFFFFFF00000001)   # -1/8: NOT
+        lut_host = np.stack([inv if (C3_MASK >> j) & 1 else gate for j in range(8)])
+        lut_idx = np.tile(np.arange(8, dtype=np.uint32), n_ct)
     else:
         bits = (gm if strong else rng.integers(0, 2, B)).astype(bool)
         cts = ck.encrypt_bool(bits, seed=INPUT_SEED + 1, stream0=lo)
         lut_host = eng.gate_lut()
     d_in = torch.from_numpy(cts.view(np.int64)).to(dev)
-    d_lut = torch.from_numpy(lut_host.view(np.int64)).to(dev)
+    d_lut = torch.from_numpy(np.ascontiguousarray(lut_host).view(np.int64)).to(dev)
+    d_idx = torch.from_numpy(lut_idx.view(np.int32)).to(dev) if c3 else None
     d_out = torch.empty_like(d_in)
     stream = torch.cuda.current_stream(dev)
 
     for _ in range(args.warmup):
-        eng.pbs_async(d_in, d_lut, d_out, stream=stream)
+        eng.pbs_async(d_in, d_lut, d_out, d_idx, stream=stream)
     torch.cuda.synchronize()
 
     eng.timing(True)
@@ -309,7 +338,7 @@ def main() -> int:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.pbs_async(d_in, d_lut, d_out, stream=stream)
+        eng.pbs_async(d_in, d_lut, d_out, d_idx, stream=stream)
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
@@ -327,6 +356,9 @@ def main() -> int:
     out = d_out.cpu().numpy().view(np.uint64)
     if fhevm:
         correct = bool(np.array_equal(ck.decrypt(out, FHEVM_MM), msgs))
+    elif c3:
+        got = ck.decrypt_bool(out).reshape(-1, 8).astype(np.uint64)
+        correct = bool(np.array_equal((got << np.arange(8, dtype=np.uint64)[None, :]).sum(axis=1), vals ^ np.uint64(C3_MASK)))
     else:
         correct = bool(np.array_equal(ck.decrypt_bool(out), bits))
     ok = torch.tensor([1 if correct else 0], dtype=torch.int32, device=dev)
@@ -344,7 +376,46 @@ def main() -> int:
     # ciphertexts in + out: small LWEs at P-GATE (PBS -> KS), big LWEs at P-FHEVM (KS -> PBS)
     io_bytes = 16 * ((pd["n"] + 1) if pd["order"] == 0 else (pd["k"] * pd["N"] + 1))
     result = None
-    if rank == 0:
+    if rank == 0 and c3:
+        result = {
+            "metric": f"FheUint8 LUT evals/sec (8 PBS per ciphertext, one multi-LUT launch), batch={n_ct}",
+            "value": round(world * n_ct * args.steps / elapsed_max, 1),
+            "unit": "FheUint8/s",
+            "pbs_per_s": round(value, 1),
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "strong" if strong else "weak",
+            "vs_baseline": None,
+            "dtype": "f64" if fft else "u64",
+            "data": "synthetic: uniform bytes, 8 ChaCha20-seeded gate-encoded bit LWEs each (key seed 0x7F4E0001); "
+                    f"LUT j = NOT if bit j of {C3_MASK:#04x} else identity gate LUT (lut_index = bit position)",
+            "config": {
+                "workload": f"BASELINE.json configs[2]: FheUint8 LUT eval, {n_ct} FheUint8 x 8 per-bit LUTs = {B} P-GATE "
+                            "PBS (blind rotate + sample extract + keyswitch) per GPU in one launch"
+                            + (", FFT64 transform" if fft else ", NTT transform"),
+                "batch_per_gpu": n_ct, "pbs_per_gpu": B, "params": params.as_dict(),
+                "parallelism": f"batch-sharded x{world}",
+            },
+            "roofline": dict(roofline(args.preset, br_kernel, B, br_avg, br_bytes,
+                                      bsk_bytes + B * 8 * ((pd["n"] + 1) + (pd["k"] * pd["N"] + 1))), launches=br_n),
+            "keyswitch_ms": round(ks_ms / max(ks_n, 1), 3),
+            "decrypt_ok": bool(ok.item()),
+        }
+        if world == 1 and not args.no_cpu:
+            threads, how = host_cores()
+            log(f"cpu baseline on {threads} host cores ({how})")
+            sample = args.cpu_sample or (256 * threads if fft else 40 * threads)   # whole FheUint8 values: x 8
+            sample = min(sample - sample % 8, B)
+            cb, exact, digest = cpu_baseline(cts, out, sample, threads, preset_id, lut_host, lut_idx)
+            cb["value_fheuint8_per_s"] = round(cb["value"] / 8, 3)
+            result["cpu_baseline"] = cb
+            result["sample_bitexact"] = exact
+            result["bitexact_check"] = digest
+        print(json.dumps(result), flush=True)
+    elif rank == 0:
         result = {
             "metric": METRIC if not fhevm else f"PBS/sec at P-FHEVM (N=2048, KS->PBS), batch={B}",
             "value": round(value, 1),
@@ -389,6 +460,7 @@ def main() -> int:
             "keyswitch_ms": round(ks_ms / max(ks_n, 1), 3),
             "ms_noise_reduction_ms": round(msr_ms / msr_n, 3) if msr_n else None,
             "key_broadcast_ms": round(bcast_ms, 3),
+            "dist": {"backend": dist.get_backend() if dist_on else None, "world_size": world},
             "decrypt_ok": bool(ok.item()),
         }
         if world == 1 and not args.no_cpu:

@@ -122,6 +122,7 @@ export class LuxFHELocalClient {
   /** requests submitted concurrently share PBS launches (lockstep circuit levels) */
   evaluate(req: EvaluateRequest): Promise<Uint8Array>;
   decrypt(ct: Uint8Array): Promise<bigint>;
-  unseal(address: string, ct: Uint8Array): Promise<bigint>;
+  decryptSync(ct: Uint8Array): bigint;
+  unseal(address: string, sealedData: Uint8Array | string): bigint;
   close(): void;
 }

@@ -437,8 +437,8 @@ class LuxFHELocalClient {
     this.busy = false;
     this._pump();
   }
-  /** -> bigint (first value of the ciphertext) */
-  async decrypt(bytes) {
+  /** -> bigint (first value of the ciphertext); decryption is host-side, so this is synchronous */
+  decryptSync(bytes) {
     const ct = parseCiphertext(bytes);
     const c = { dim: ct.lweDim + 1 };
     if (ct.kind >= KIND.RADIX_UINT) {
@@ -448,7 +448,19 @@ class LuxFHELocalClient {
     const vec = integer.FheUintVec.fromValueMajor(c, ct.words, ct.count, ct.width);
     return integer.decryptColumns(this.clientKey, vec.cols, ct.count)[0];
   }
-  async unseal(_addr, data) { return this.decrypt(data); }
+  async decrypt(bytes) { return this.decryptSync(bytes); }
+  /**
+   * luxfhejs unseal(contractAddress, sealedData): bigint -- synchronous like the reference
+   * (packages/luxfhejs/src/index.ts:146); sealedData as bytes or a hex string ("0x..." or bare hex)
+   */
+  unseal(_addr, data) {
+    if (typeof data === 'string') {
+      const h = data.startsWith('0x') || data.startsWith('0X') ? data.slice(2) : data;
+      if (h.length % 2 !== 0 || /[^0-9a-fA-F]/.test(h)) throw new Error('unseal: sealedData is not a hex string');
+      data = Uint8Array.from(Buffer.from(h, 'hex'));
+    }
+    return this.decryptSync(data);
+  }
   close() { if (this.engine && this.engine.destroy) this.engine.destroy(); }
 }
 

@@ -28,4 +28,13 @@ out.entropy_cts_differ = h(e1) !== h(e2) && ck1.decryptBool(e1)[0] && ck1.decryp
 try { new t.LuxFHELocalClient({ seed: 1n }); out.seed_refused = false; } catch (e) { out.seed_refused = /dev: true/.test(e.message); }
 out.seed_dev_ok = new t.LuxFHELocalClient({ seed: 1n, dev: true }).seed === 1n;
 out.default_params = new t.LuxFHELocalClient().params.transform;
+// unseal(contractAddress, sealedData): bigint, synchronous like luxfhejs (index.ts:146); the client key is host-side
+{
+  const cl = new t.LuxFHELocalClient({ seed: 7n, dev: true, params: p });
+  [cl.clientKey] = t.genKeys(cl.params, 7n);
+  const sealed = cl.encryptValue(0xA5, 8);
+  const u = cl.unseal('0x00000000000000000000000000000000000000aa', sealed);
+  out.unseal_sync = typeof u === 'bigint' && u === 0xA5n
+    && cl.unseal('0xaa', '0x' + Buffer.from(sealed).toString('hex')) === 0xA5n;
+}
 console.log(JSON.stringify(out));

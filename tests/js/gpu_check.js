@@ -59,6 +59,11 @@ const t = require('../../js');
   const l = await cl.encrypt_uint8(0b10110011), r = await cl.encrypt_uint8(0b01100110);
   const x = await cl.evaluate({ op: 'xor', left: l, right: r, bitWidth: 8 });
   assert.strictEqual(await cl.decrypt(x, 8), BigInt(0b10110011 ^ 0b01100110));
+  // unseal is synchronous like the reference's (luxfhejs index.ts:146): a bigint, not a Promise; bytes or hex
+  const u = cl.unseal('0x00000000000000000000000000000000000000aa', x);
+  assert.strictEqual(typeof u, 'bigint');
+  assert.strictEqual(u, BigInt(0b10110011 ^ 0b01100110));
+  assert.strictEqual(cl.unseal('0xaa', '0x' + Buffer.from(x).toString('hex')), u);
   cl.close();
   console.log(JSON.stringify({ ok: true }));
 })().catch((e) => { console.error(e); process.exit(1); });

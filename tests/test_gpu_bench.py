@@ -47,3 +47,18 @@ def test_bench_strong_scaling_mode():
     d = json.loads([l for l in r.stdout.splitlines() if l.strip().startswith("{")][0])
     assert d["scaling"] == "strong" and d["config"]["global_batch"] == 1024 and d["config"]["batch_per_gpu"] == 1024
     assert d["decrypt_ok"] is True
+
+
+def test_bench_c3_config():
+    """--config c3 (BASELINE.json configs[2]): FheUint8 values x 8 per-bit LUTs in one multi-LUT launch; every byte
+    decrypted, the CPU sample (whole FheUint8 values, lut_index included) bit-exact against the oracle."""
+    r = subprocess.run([sys.executable, "bench.py", "--config", "c3", "--steps", "2", "--warmup", "1", "--batch", "128",
+                        "--cpu-sample", "64"], cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.strip().startswith("{")][0])
+    assert d["unit"] == "FheUint8/s" and d["config"]["batch_per_gpu"] == 128 and d["config"]["pbs_per_gpu"] == 1024
+    assert abs(d["pbs_per_s"] - 8 * d["value"]) < 1e-6 * d["pbs_per_s"] + 1
+    assert d["decrypt_ok"] is True and d["sample_bitexact"] is True
+    assert d["roofline"]["launches"] == 2 and d["roofline"]["kernel_ms"] > 0
+    bx = d["bitexact_check"]
+    assert bx["bitexact_pbs"] == 64 and bx["gpu_sha256"] == bx["oracle_sha256"]

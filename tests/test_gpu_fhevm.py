@@ -167,3 +167,18 @@ def test_ms_key_refused_for_pbs_ks_order(engine):
     z = np.zeros((4, 631), dtype=np.uint64)
     with pytest.raises(tfhe_amd.TfheError, match="EUNSUPPORTED"):
         engine.load_ms_key(z)
+
+
+def test_ms_key_refuses_keys_beyond_the_scan_window(fengine, fkeys):
+    """The scan reads the key's element-major transpose through a buffer resource with 32-bit offsets: a key with
+    (n + 1) x pitch x 8 >= 2^31 bytes is refused up front, not scanned with silently zeroed loads.
+    Called through the C ABI with a one-row buffer: the size check comes before anything is read."""
+    import ctypes
+    import tfhe_amd
+    one = np.zeros(919, dtype=np.uint64)
+    big = (2**31 // (919 * 8)) // 64 * 64 + 64           # the first 64-multiple past the window at n = 918
+    rc = tfhe_amd.lib().tfhe_hip_load_ms_key(fengine._h, one.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                              big, 2.0**58, 13.18, 2.63e-7)
+    assert rc == -1                                      # TFHE_HIP_EINVAL
+    assert "2 GiB scan window" in tfhe_amd.lib().tfhe_hip_last_error().decode()
+    fengine.load_ms_key(fkeys[1].ms_zeros)                 # the real key still loads afterwards

@@ -49,6 +49,7 @@ def test_js_addon_cpu(product_keys):
     assert out["entropy_keys_differ"] and out["entropy_cts_differ"]
     assert out["seed_refused"] and out["seed_dev_ok"]
     assert out["default_params"] == 1  # LuxFHELocalClient defaults to the FFT64 engine
+    assert out["unseal_sync"] is True  # a bigint, not a Promise (luxfhejs index.ts:146)
     if out["engine"] != "created":  # no GPU here: a clean error, not an abort
         assert out["engine"] in ("-1", "-3")
 

@@ -891,6 +891,12 @@ int tfhe_hip_load_ms_key(tfhe_ctx* c, const uint64_t* zeros, uint32_t count, dou
                                        "(KS -> PBS parameter sets only)");
   if (count > 0x7FFFFFFF || !(bound >= 0) || !(r_sigma >= 0) || !(input_variance >= 0))
     return fail(TFHE_HIP_EINVAL, "load_ms_key: count %u / bound / r_sigma / variance out of range", count);
+  // the scan addresses the element-major transpose through a buffer resource with 32-bit byte offsets
+  // (ms_reduce.hip): (n + 1) x pitch x 8 must stay below 2^31, or raw loads past num_records would read zeros
+  // silently.  n = 918 allows ~292 k zeros; the reference's key carries 1449.
+  if ((double)(c->p.n + 1) * (double)tfhe::ms_zeros_pitch(count) * 8.0 >= 0x1p31)
+    return fail(TFHE_HIP_EINVAL, "load_ms_key: %u zeros x %u elements exceed the 2 GiB scan window", count,
+                (unsigned)(c->p.n + 1));
   std::lock_guard<std::mutex> lk(c->mu);
   c->ms_count = 0;
   // two layouts in one allocation: rows [count][n+1] (the add of the chosen zero) then the element-major

@@ -446,6 +446,77 @@ __device__ __forceinline__ void dft512_inv_rb(double (&xr)[8], double (&xi)[8], 
   dft8<true>(xr, xi);
 }
 
+// Round 6 (three waves per SIMD): every twiddle read from LDS, pass B's from the COMPACT table.  TW_B[e][L] =
+// w512^(8 (L & 7) e) depends on L & 7 only, so the 64 distinct values sit in 1 KB as [e][L & 7]: a lane reads
+// twBc[8 e] from its base twBc + (L & 7) (8 distinct addresses per instruction, broadcast, conflict-free), the same
+// bits as the 8 KB table.  twAl = TW_A + L (pass A, slot 0 included: the merged twist), twIl = TW_I + L.
+template <bool TWIN = false, int BSTR = 8>
+__device__ __forceinline__ void dft512_fwd_c(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
+                                             const double2* twAl, const double2* twBc) {
+  if constexpr (TWIN) twist_dft8_fwd(xr, xi);
+  else dft8<false>(xr, xi);
+#pragma unroll
+  for (int e = 0; e < 8; e++) cmul<false>(xr[e], xi[e], twAl[64 * e]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[lane + S1 * e] = make_double2(xr[e], xi[e]);
+  lds_order();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[tb.b1 + 8 * e];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  lds_order();
+  dft8<false>(xr, xi);
+#pragma unroll
+  for (int e = 1; e < 8; e++) cmul<false>(xr[e], xi[e], twBc[BSTR * e]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[lane + S2 * e] = make_double2(xr[e], xi[e]);
+  lds_order();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[tb.b2 + e];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  lds_order();
+  dft8<false>(xr, xi);
+}
+
+// the matching inverse: pass C' conjugates the compact pass B table, pass B' reads twIl[64 e]
+// (BSTR: the pass B table's slot stride, 8 for the compact table, 64 for the full one)
+template <int BSTR = 8>
+__device__ __forceinline__ void dft512_inv_c(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
+                                             const double2* twBc, const double2* twIl) {
+  dft8<true>(xr, xi);
+#pragma unroll
+  for (int e = 1; e < 8; e++) cmul<true>(xr[e], xi[e], twBc[BSTR * e]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[tb.b2 + e] = make_double2(xr[e], xi[e]);
+  lds_order();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[lane + S2 * e];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  lds_order();
+  dft8<true>(xr, xi);
+#pragma unroll
+  for (int e = 0; e < 8; e++) cmul<true>(xr[e], xi[e], twIl[64 * e]);
+#pragma unroll
+  for (int e = 0; e < 8; e++) T[tb.b1 + 8 * e] = make_double2(xr[e], xi[e]);
+  lds_order();
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const double2 v = T[lane + S1 * e];
+    xr[e] = v.x;
+    xi[e] = v.y;
+  }
+  lds_order();
+  dft8<true>(xr, xi);
+}
+
 template <bool TW0 = false, bool TWIN = false>
 __device__ __forceinline__ void dft512_fwd(double (&xr)[8], double (&xi)[8], double2* T, int lane, TBase tb,
                                            const double2* tw) {
@@ -631,10 +702,13 @@ __device__ __forceinline__ u64 add_hi_word(u64 acc, double d) {
   const u32x2v w = __builtin_bit_cast(u32x2v, d);
   return __builtin_bit_cast(u64, (u32x2v){a.x, a.y + w.x});
 }
-// N = 1024 keeps the rint form (FFT_TORUS_NORINT_1K 0): the rint-free one measured 0.3 % slower on the P-GATE pair kernel
-// (24.19 vs 24.14 ms, profiles/r05f_ab_norint.txt) while it gains 0.3 % at N = 2048
+// Used only by FFT_Y32 = 0 A/B builds of the N = 1024 kernels (the default FFT_Y32 = 1 updates through torus_acc_add_y
+// below).  The oracle restates the rint-free update (or_f64_to_torus_dev) at both N, so this function takes the rint-free
+// form too (FFT_TORUS_NORINT_1K 1, round 6): the rint form differs from it for tiny negative x and would make
+// such a build fail bit-exact parity.  (Round 5 measured the two forms within 0.3 % of each other on the pair kernel,
+// profiles/r05f_ab_norint.txt.)
 #ifndef FFT_TORUS_NORINT_1K
-#define FFT_TORUS_NORINT_1K 0
+#define FFT_TORUS_NORINT_1K 1
 #endif
 __device__ __forceinline__ u64 torus_acc_add(u64 acc, double x) {
 #if FFT_TORUS_NORINT && FFT_TORUS_NORINT_1K

@@ -156,6 +156,8 @@ hipError_t launch_ms_reduce(u64* lwe, size_t B, int n, const u64* zeros, int cou
   if (shift < 33 || shift > 58 || n < 1 || (double)(n + 1) * std::ldexp(1.0, 2 * (shift - 26)) >= 0x1p64 ||
       (double)(n + 1) * std::ldexp(1.0, shift) >= 0x1p64)
     return hipErrorInvalidValue;
+  // the kernel's buffer-resource offsets are 32-bit (tfhe_hip_load_ms_key refuses larger keys first)
+  if (count < 0 || (double)(n + 1) * (double)ms_zeros_pitch((size_t)count) * 8.0 >= 0x1p31) return hipErrorInvalidValue;
   const int zp = (int)ms_zeros_pitch((size_t)count);
   const u64* zt = zeros + (size_t)count * (n + 1);
   const unsigned grid = (unsigned)((B + MS_WAVES - 1) / MS_WAVES);

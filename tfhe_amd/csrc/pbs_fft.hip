@@ -567,6 +567,198 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
 }
 
 // ---------------------------------------------------------------------------------------------
+// Three waves per SIMD (round 6, FFT_G3): ONE workgroup per CU of G3_CTS = 6 ciphertexts x 2 component waves (768
+// threads, <= 168 VGPRs).  The per-wave program is the pair kernel's -- rotate + decompose acc_c, three level steps
+// (digits, DFT, MAC into both outputs' partial sums), the partial-sum exchange, one inverse -- with the same
+// operation order (the oracle is unchanged), but
+//   * every twiddle comes from LDS (pass A and the inverse's pass B' from their 8 KB tables, pass B / C' from the
+//     1 KB compact table, fft512.h dft512_fwd_c), which frees the 60 registers the pair kernel keeps them in;
+//   * one 32 KB level-step chunk serves 6 ciphertexts instead of 2: a third of the LDS-DMA bytes and of the BSK
+//     stream per ciphertext;
+//   * the batch is spread over rounds of one workgroup per CU with the ciphertext counts balanced (4096 on 256 CUs:
+//     3 rounds, 16 ciphertexts per CU as 6 + 5 + 5) instead of a fixed 6 per workgroup (2.67 rounds).  Pairs beyond a
+//     workgroup's count skip all compute but keep the barrier sequence.
+// LDS: TW_A 8 KB | TW_I 8 KB | TW_B compact 1 KB | one 32 KB level step | 12 x 9 KB transpose areas = 160,768 B.
+#ifndef FFT_G3
+#define FFT_G3 0
+#endif
+#ifndef G3_TW_GLOBAL
+#define G3_TW_GLOBAL 0
+#endif
+constexpr int G3_CTS = 6;
+constexpr int G3_NW = 2 * G3_CTS;
+struct G3Shared {
+  double2 twA[M];
+  double2 twI[M];
+  double2 twB[64];                                 // [e][L & 7]
+  double2 K[STEP_C64];
+  double2 T[G3_NW][T_C64];
+};
+static_assert(sizeof(G3Shared) <= 163840, "G3 LDS");
+
+template <bool WRITE_ACC, bool WRITE_BIG>
+__global__ __launch_bounds__(64 * G3_NW, 1) void blind_rotate_fft_g3_kernel(
+    const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
+    int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tw_g, u64* __restrict__ out_big,
+    u64* __restrict__ out_acc) {
+  __shared__ __attribute__((aligned(16))) G3Shared sh;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = wave & 1;
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const int c_s = wave_s & 1;
+  // balanced split: workgroup w takes B / G or B / G + 1 ciphertexts (G = gridDim.x)
+  const size_t G = gridDim.x, w = blockIdx.x;
+  const size_t per = B / G, extra = B % G;
+  const size_t cnt = per + (w < extra ? 1 : 0);
+  const size_t b0 = w * per + (w < extra ? w : extra);
+  const int p = wave_s >> 1;
+  const bool live = (size_t)p < cnt;
+  const size_t b = live ? b0 + p : b0;
+  const u64* ct = lwe_in + b * (size_t)(n + 1);
+  double2* T = sh.T[wave];
+  const double2* Tp = sh.T[wave ^ 1];
+  const int n_steps = 3 * n;
+  (void)n_steps;
+
+  const __amdgpu_buffer_rsrc_t bsr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)bsk, (short)0, n * 6 * 2 * M * (int)sizeof(double2), 0x00020000);
+  const int voff = lane * 16;
+  for (int q = threadIdx.x; q < M; q += 64 * G3_NW) {
+    sh.twA[q] = tw_g[TW_A + q];
+    sh.twI[q] = tw_g[TW_I + q];
+  }
+  if (threadIdx.x < 64) sh.twB[threadIdx.x] = tw_g[TW_B + 64 * (threadIdx.x >> 3) + (threadIdx.x & 7)];
+
+  u64 acc[16];
+  {
+    int li = lut_index ? (int)lut_index[b] : 0;
+    li = (li < 0 || li >= n_lut) ? 0 : li;
+    const u64* lut = luts + (size_t)li * N1K;
+    const int s = (2048 - ms2048(ct[n])) & 2047;
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      int d = 64 * e + lane - s;
+      bool neg = false;
+      if (d < 0) { d += N1K; neg = !neg; }
+      if (d < 0) { d += N1K; neg = !neg; }
+      const u64 v = gl_to_torus(lut[d]);
+      acc[e] = c ? (neg ? 0 - v : v) : 0;
+    }
+  }
+  __syncthreads();
+  const TBase tb(lane);
+#if G3_TW_GLOBAL
+  // A/B: the twiddles straight from the global tables (L1 / L2 hits) instead of LDS
+  const double2* twAl = tw_g + TW_A + lane;
+  const double2* twIl = tw_g + TW_I + lane;
+  const double2* twBc = tw_g + TW_B + (lane & 7);  // the full table at stride 64
+  constexpr int BSTR = 64;
+#else
+  const double2* twAl = sh.twA + lane;
+  const double2* twIl = sh.twI + lane;
+  const double2* twBc = sh.twB + (lane & 7);
+  constexpr int BSTR = 8;
+#endif
+
+  for (int i = 0; i < n; i++) {
+    u32 st[16];
+    if (live) rotate_states(acc, ms2048(ct[i]), lane, T, st);
+    double o0r[8], o0i[8], o1r[8], o1i[8];
+    auto level = [&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      const int g = 3 * i + q;
+#if FFT_MACPRIO
+      if (q > 0) __builtin_amdgcn_s_setprio(0);
+#endif
+      if (q > 0) __syncthreads();  // every wave is done with step g - 1's chunk (the exchange's barriers order q = 0)
+      {
+        const int ii = g / 3;
+        for (int blk = wave_s; blk < 32; blk += G3_NW) {
+          const int cc = blk >> 4;
+          const int soff = ((ii * 6 + cc * 3 + q) * (2 * M)) * (int)sizeof(double2) + (blk & 15) * 1024;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              bsr, (__attribute__((address_space(3))) void*)((char*)sh.K + blk * 1024), 16, voff, soff, 0, 0);
+        }
+      }
+      double xr[8], xi[8];
+      if (live) {
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          if constexpr (q == 2) {
+            xr[e] = (double)decomp_top(st[e]);
+            xi[e] = (double)decomp_top(st[e + 8]);
+          } else {
+            xr[e] = (double)decomp_step(st[e], 1u);
+            xi[e] = (double)decomp_step(st[e + 8], 1u);
+          }
+        }
+        dft512_fwd_c<true, BSTR>(xr, xi, T, lane, tb, twAl, twBc);
+      }
+      glds_barrier();  // step g's chunk has landed
+      if (live) {
+#if FFT_MACPRIO
+        __builtin_amdgcn_s_setprio(3);
+#endif
+        const double2* k0 = sh.K + c * (2 * M) + lane;
+        const double2* k1 = k0 + M;
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          const double2 u = k0[64 * e], v = k1[64 * e];
+          if constexpr (q == 0) {
+            mac_first(o0r[e], o0i[e], xr[e], xi[e], u);
+            mac_first(o1r[e], o1i[e], xr[e], xi[e], v);
+          } else {
+            mac_next(o0r[e], o0i[e], xr[e], xi[e], u);
+            mac_next(o1r[e], o1i[e], xr[e], xi[e], v);
+          }
+        }
+      }
+    };
+    level(std::integral_constant<int, 0>{});
+    level(std::integral_constant<int, 1>{});
+    level(std::integral_constant<int, 2>{});
+#if FFT_MACPRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+    double xr[8], xi[8];
+    if (live) {
+      if (c_s) exchange_partials<1>(o0r, o0i, o1r, o1i, xr, xi, T, Tp, lane);
+      else exchange_partials<0>(o0r, o0i, o1r, o1i, xr, xi, T, Tp, lane);
+      dft512_inv_c<BSTR>(xr, xi, T, lane, tb, twBc, twIl);
+      twist_slots<true>(xr, xi);
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        acc[e] = ACC_ADD(acc[e], xr[e]);
+        acc[e + 8] = ACC_ADD(acc[e + 8], xi[e]);
+      }
+    } else {
+      __syncthreads();  // the exchange's two barriers
+      __syncthreads();
+    }
+  }
+
+  if (!live) return;
+  if (WRITE_ACC) {
+    u64* oa = out_acc + b * 2048 + c * N1K;
+#pragma unroll
+    for (int e = 0; e < 16; e++) oa[64 * e + lane] = acc[e];
+  }
+  if (WRITE_BIG) {
+    u64* ob = out_big + b * (size_t)(N1K + 1);
+    if (c == 0) {
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        const int idx = 64 * e + lane;
+        if (idx == 0) ob[0] = acc[e];
+        else ob[N1K - idx] = 0 - acc[e];
+      }
+    } else if (lane == 0) {
+      ob[N1K] = acc[0];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Latency-mode blind rotation (small batches): ONE ciphertext per workgroup of 8 waves.  Per CMUX:
 //   A  waves 0..5: wave r = chain position (c, q) (c = r / 3; q = 0, 1, 2: levels least significant
 //      first) rotates + decomposes accumulator polynomial c, keeps step q's digits and transforms
@@ -840,6 +1032,28 @@ hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64
                          n_lut, bk, t, out_big, out_acc);
     return hipGetLastError();
   }
+#if FFT_G3
+  {
+    // rounds of one workgroup per CU, at most G3_CTS ciphertexts each, counts balanced over the whole grid
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+    const size_t rounds = (B + (size_t)G3_CTS * cus - 1) / ((size_t)G3_CTS * cus);
+    size_t nwg = rounds * (size_t)cus;
+    if (nwg > B) nwg = B;
+    dim3 grid((unsigned)nwg), block(64 * G3_NW);
+    if (out_acc && out_big)
+      hipLaunchKernelGGL((blind_rotate_fft_g3_kernel<true, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                         n_lut, bk, t, out_big, out_acc);
+    else if (out_acc)
+      hipLaunchKernelGGL((blind_rotate_fft_g3_kernel<true, false>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                         n_lut, bk, t, out_big, out_acc);
+    else
+      hipLaunchKernelGGL((blind_rotate_fft_g3_kernel<false, true>), grid, block, 0, s, lwe_in, n, B, luts, lut_index,
+                         n_lut, bk, t, out_big, out_acc);
+    return hipGetLastError();
+  }
+#endif
   constexpr int CTS = FFT_PAIR_CTS;
   dim3 grid((unsigned)((B + CTS - 1) / CTS)), block(128 * CTS);
   if (out_acc && out_big)

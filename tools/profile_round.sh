@@ -6,13 +6,15 @@
 # profiles/ only while its source_id matches its own).  Each GPU step has its own time
 # limit; the script stops at the first failure.
 #   TAG=r02_fft1 PRESET=gate_fft tools/profile_round.sh
+#   TAG=r06_c3 PRESET=gate_fft ARGS="--config c3" BATCH=32768 tools/profile_round.sh   (BASELINE configs[2]: the
+#   summary's batch is the launch's PBS count, 8 x 4096)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r02}
 PRESET=${PRESET:-gate_fft}
-B="--preset $PRESET"
+B="--preset $PRESET ${ARGS:-}"
 BENCH=${BENCH:-1}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python3 bench.py $B --no-cpu > gpurun_out/prof_${TAG}.log 2>&1 || { echo "rocprof stats failed"; tail -30 gpurun_out/prof_${TAG}.log; exit 1; }
 find gpurun_out/prof_${TAG} -name '*kernel_stats.csv' -exec cp {} gpurun_out/${TAG}_kernel_stats.csv \;
