@@ -171,11 +171,19 @@ __global__ __launch_bounds__(64) void fft_inv_kernel(const double2* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
-// FFT_PRIO: s_setprio 1 for waves 4-7 (the second-dispatched wave of each SIMD pair) for the whole
-// CMUX loop (round 1, measured on the 8-ciphertext kernel 29.36 -> 29.25 ms per 4096: both waves of a SIMD run the
-// same lockstep program, the younger one otherwise loses VALU arbitration after every barrier).
+// FFT_PRIO: the waves' base priority (what FFT_MACPRIO drops back to after each MAC phase).
+//   3 (default since round 6): the workgroups with bit 8 of blockIdx set -- on 256 CUs the second workgroup each CU
+//     receives, then every other dispatch half-round -- at base priority 1.  The hardware arbitrates oldest-first, so
+//     of the two workgroups that share a CU the older always ran ahead: in a 4096 launch one slot of every CU
+//     finished its four workgroups 2.4 ms before the other and idled (profiles/r06d_wgt_4096.json, per-workgroup
+//     s_memrealtime stamps, tools/wg_timeline.py).  With the alternation the two slots end 0.33 ms apart and the
+//     CU-slot busy fraction rises 0.945 -> 0.980: 24.04 -> 23.04 ms per 4096, C2 6.45 -> 6.24 ms (same box, three
+//     boxes; profiles/r06e_ab_prio.txt).  Round 4 had measured this scheme "neutral" -- with a C-level branch around
+//     s_setprio that made hipcc spill (below).
+//   1: s_setprio 1 for waves 4-7 of an 8-wave workgroup (round 1; no effect on the 4-wave CTS = 2 workgroup)
+//   4 / 5: A/B forms (the last FFT_TAILWG workgroups high; bit 8 xor bit 9)
 #ifndef FFT_PRIO
-#define FFT_PRIO 1
+#define FFT_PRIO 3
 #endif
 
 // Component-pair batch kernel (round 3, the default above the latency range): workgroup = CTS ciphertexts x 2
@@ -209,17 +217,22 @@ constexpr int STEP_C64 = 4 * M;                    // rows (0, q), (1, q), j = 0
 // workgroups drift apart and one's LDS phases overlap the other's VALU phases on every SIMD: 27.01 -> 26.63 ms per
 // 4096 on the same box (profiles/r04a_cts_ab.txt, two rounds).  4 (FFT_PAIR_CTS=4): 8 waves, one workgroup per CU,
 // all tables in LDS, level steps double-buffered (the round-3 kernel).
-template <int CTS>
+// FFT_PAIR_LDSTW: the round-3 layout (all tables in LDS, level steps double-buffered) for CTS = 4; 0 (round 6 A/B):
+// CTS = 4 with the CTS = 2 program (passes A / B in registers, one level-step buffer): 8 waves, one workgroup per CU
+#ifndef FFT_PAIR_LDSTW
+#define FFT_PAIR_LDSTW 1
+#endif
+template <int CTS, bool LDS_TW = (CTS == 4 && FFT_PAIR_LDSTW)>
 struct FpShared {
   double2 tw[3 * M];                               // TW_A | TW_B | TW_I of the global table (no twist table)
   double2 T[2 * CTS][T_C64];                       // after the tables: T - 8 KB is still inside the block
   double2 K[2][STEP_C64];
 };
-template <>
-struct FpShared<2> {
+template <int CTS>
+struct FpShared<CTS, false> {
   double2 twI[M];                                  // TW_I only (passes A, B: registers, loaded from global)
   double2 K[1][STEP_C64];
-  double2 T[4][T_C64];
+  double2 T[2 * CTS][T_C64];
 };
 #ifndef FFT_PAIR_CTS
 #define FFT_PAIR_CTS 2
@@ -230,6 +243,12 @@ struct FpShared<2> {
 // 160.4k PBS/s (profiles/r04k_pgate_macprio_ab.txt)
 #ifndef FFT_MACPRIO
 #define FFT_MACPRIO 1
+#endif
+#ifndef FFT_STAGGER
+#define FFT_STAGGER 1
+#endif
+#ifndef FFT_TAILWG
+#define FFT_TAILWG 256
 #endif
 typedef __attribute__((address_space(3))) u64 lds_u64;
 
@@ -370,14 +389,24 @@ __device__ __forceinline__ void load_step_buf(__amdgpu_buffer_rsrc_t bsr, int g,
   }
 }
 
+#ifndef FFT_WGTIME
+#define FFT_WGTIME 0
+#endif
+#if FFT_WGTIME
+// diagnostic build only: per-workgroup start / end (s_memrealtime, 100 MHz), HW_ID and XCC_ID of the last launch
+__device__ unsigned long long g_wgt[4 * 16384];
+#endif
 template <int CTS, bool WRITE_ACC, bool WRITE_BIG>
 __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kernel(
     const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
     int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tw_g, u64* __restrict__ out_big,
     u64* __restrict__ out_acc) {
   constexpr int NW = 2 * CTS;
-  constexpr bool LDS_TW = CTS == 4;
+  constexpr bool LDS_TW = CTS == 4 && FFT_PAIR_LDSTW;
   __shared__ __attribute__((aligned(16))) FpShared<CTS> sh;
+#if FFT_WGTIME
+  const unsigned long long wg_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int c = wave & 1;
   const size_t b_raw = (size_t)blockIdx.x * CTS + (wave >> 1);
@@ -447,17 +476,44 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
 #if FFT_PRIO == 1
   const bool prio_hi = NW > 4 && wave_s >= 4;  // the 4-wave CTS = 2 workgroup has no second wave per SIMD
 #elif FFT_PRIO == 3
-  // A/B: with two workgroups per CU, one of them (by dispatch round) at the higher priority.  Bit 8 of the
+  // with two workgroups per CU, one of them (by dispatch half-round) at the higher priority.  Bit 8 of the
   // workgroup index is the second dispatch half on a 256-CU part (MI355X only; other CU counts just alternate)
   const bool prio_hi = (blockIdx.x >> 8) & 1;
+#elif FFT_PRIO == 5
+  // A/B: bit 8 xor bit 9 of the workgroup index (the alternation flips every other dispatch round)
+  const bool prio_hi = ((blockIdx.x >> 8) ^ (blockIdx.x >> 9)) & 1;
+#elif FFT_PRIO == 4
+  // A/B (round 6): the workgroups of the final dispatch half-round (the last FFT_TAILWG of the grid; on 256 CUs these
+  // take the slot of each CU that frees last) at the higher base priority, against the hardware's oldest-first
+  // arbitration, so the two final workgroups of a CU end closer together (profiles/r06d_wgt_*: without it one slot
+  // of every CU idles ~2.4 ms at the end of a 4096 launch)
+  const bool prio_hi = blockIdx.x + FFT_TAILWG >= gridDim.x;
 #else
   constexpr bool prio_hi = false;
 #endif
+#if FFT_PRIO == 1 || FFT_PRIO == 0
   auto base_prio = [&]() {
     if (prio_hi) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
   };
-  if (prio_hi) __builtin_amdgcn_s_setprio(1);
+#else
+  // a runtime (wave-uniform) priority as ONE asm block with its own scalar branch: a C-level branch around the two
+  // s_setprio forms splits every level step into basic blocks and hipcc then spills ~195 VGPRs (measured 71 ms)
+  const unsigned prio_flag = __builtin_amdgcn_readfirstlane(prio_hi ? 1u : 0u);
+  auto base_prio = [&]() {
+    asm volatile(
+        "s_cmp_lg_u32 %0, 0\n\ts_cbranch_scc0 .Lbp0_%=\n\ts_setprio 1\n\ts_branch .Lbp1_%=\n"
+        ".Lbp0_%=:\n\ts_setprio 0\n.Lbp1_%=:" ::"s"(prio_flag) : "scc");
+  };
+#endif
+  base_prio();
+#if FFT_STAGGER
+  // round 6 (default 1): the second workgroup of each CU in the first dispatch round (blockIdx bit 8 on 256 CUs) starts
+  // FFT_STAGGER x ~3.4 us late, so the two workgroups of a CU do not run their phases in lockstep from the start
+  // (with FFT_PRIO 3: 23.04 -> 22.97 ms per 4096, C2 6.24 -> 6.19 ms; alone 24.04 -> 23.87 ms; 2 and 4 x 3.4 us: neutral)
+  if (blockIdx.x < 512 && ((blockIdx.x >> 8) & 1))
+    for (int k = 0; k < FFT_STAGGER; k++) __builtin_amdgcn_s_sleep(127);
+#endif
   for (int i = 0; i < n; i++) {
     // (X^a acc_c - acc_c), decomposed: the rotation image in this wave's own transpose area (its previous
     // user, the last inverse, is this wave: DS operations of a wave run in order)
@@ -543,6 +599,15 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
       acc[e + 8] = ACC_ADD(acc[e + 8], xi[e]);
     }
   }
+#if FFT_WGTIME
+  if (threadIdx.x == 0 && blockIdx.x < 16384) {
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    g_wgt[4 * blockIdx.x] = wg_t0;
+    g_wgt[4 * blockIdx.x + 1] = t1;
+    g_wgt[4 * blockIdx.x + 2] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_ID
+    g_wgt[4 * blockIdx.x + 3] = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // XCC_ID
+  }
+#endif
 
   if (!live) return;
   if (WRITE_ACC) {
@@ -1067,6 +1132,13 @@ hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64
                        lut_index, n_lut, bk, t, out_big, out_acc);
   return hipGetLastError();
 }
+
+#if FFT_WGTIME
+extern "C" int tfhe_hip_debug_wgtimes(unsigned long long* out, size_t n) {
+  if (n > 4 * 16384) n = 4 * 16384;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(fftk::g_wgt), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t launch_sample_extract_torus(const u64* acc, size_t B, u64* out, hipStream_t s) {
   if (B == 0) return hipSuccess;

@@ -65,6 +65,12 @@ typedef __attribute__((address_space(3))) u64 lds_u64;
 #ifndef F1_MACPRIO
 #define F1_MACPRIO 1
 #endif
+#ifndef F1_PRIO_ASM
+#define F1_PRIO_ASM 0
+#endif
+#ifndef F1_STAGGER
+#define F1_STAGGER 0
+#endif
 
 template <int CTS>
 struct F1Shared {
@@ -203,6 +209,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
   constexpr int SPW = 16 / NW;  // MAC slots per wave
   static_assert(NW == 8 || NW == 2 * CTS, "waves: 8, or one per polynomial");
   const int s0 = SPW * wave_s;  // MAC slots s0 .. s0 + SPW - 1
+#if F1_PRIO_ASM
+  const unsigned prio_flag = __builtin_amdgcn_readfirstlane(
+      (F1_PRIO == 3 && NW == 2 * CTS && ((blockIdx.x >> 8) & 1)) || (F1_PRIO == 1 && wave_s >= 4) ? 1u : 0u);
+#endif
+#if F1_STAGGER
+  // A/B (round 6, as pbs_fft.hip FFT_STAGGER): the second workgroup of each CU in the first dispatch round starts late
+  if (blockIdx.x < 512 && ((blockIdx.x >> 8) & 1))
+    for (int k = 0; k < F1_STAGGER; k++) __builtin_amdgcn_s_sleep(127);
+#endif
 #if F1_PRIO == 1
   if (wave_s >= 4) __builtin_amdgcn_s_setprio(1);
 #elif F1_PRIO == 3
@@ -267,9 +282,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
     }
     __syncthreads();
 #if F1_MACPRIO  // back to the workgroup's level (F1_PRIO)
+#if F1_PRIO_ASM
+    // one asm block with its own scalar branch (as pbs_fft.hip's base_prio): no C-level branch in the CMUX loop
+    asm volatile(
+        "s_cmp_lg_u32 %0, 0\n\ts_cbranch_scc0 .Lfp0_%=\n\ts_setprio 1\n\ts_branch .Lfp1_%=\n"
+        ".Lfp0_%=:\n\ts_setprio 0\n.Lfp1_%=:" ::"s"(prio_flag) : "scc");
+#else
     if (F1_PRIO == 3 && NW == 2 * CTS && ((blockIdx.x >> 8) & 1)) __builtin_amdgcn_s_setprio(1);
     else if (F1_PRIO == 1 && wave_s >= 4) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
+#endif
 #endif
     if (tw_wave) {
       double xr[16], xi[16];
