@@ -250,6 +250,9 @@ struct FpShared<CTS, false> {
 #ifndef FFT_TAILWG
 #define FFT_TAILWG 256
 #endif
+#ifndef FFT_PRIO_SH
+#define FFT_PRIO_SH 0
+#endif
 typedef __attribute__((address_space(3))) u64 lds_u64;
 
 // FFT_ROT_UNIFORM 1 (default since round 5): the rotation split so that every per-slot decision is wave-uniform.
@@ -479,6 +482,8 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
   // with two workgroups per CU, one of them (by dispatch half-round) at the higher priority.  Bit 8 of the
   // workgroup index is the second dispatch half on a 256-CU part (MI355X only; other CU counts just alternate)
   const bool prio_hi = (blockIdx.x >> 8) & 1;
+#elif FFT_PRIO == 6
+  [[maybe_unused]] constexpr bool prio_hi = false;  // the per-CMUX alternation below
 #elif FFT_PRIO == 5
   // A/B: bit 8 xor bit 9 of the workgroup index (the alternation flips every other dispatch round)
   const bool prio_hi = ((blockIdx.x >> 8) ^ (blockIdx.x >> 9)) & 1;
@@ -499,7 +504,14 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
 #else
   // a runtime (wave-uniform) priority as ONE asm block with its own scalar branch: a C-level branch around the two
   // s_setprio forms splits every level step into basic blocks and hipcc then spills ~195 VGPRs (measured 71 ms)
+#if FFT_PRIO == 6
+  // A/B (round 6): the base priority alternates every 2^FFT_PRIO_SH CMUXes, in opposite phase for the two dispatch
+  // halves (blockIdx bit 8), so the two workgroups of a CU take turns instead of the older one always winning
+  const unsigned prio_ph = __builtin_amdgcn_readfirstlane((blockIdx.x >> 8) & 1);
+  unsigned prio_flag = prio_ph;
+#else
   const unsigned prio_flag = __builtin_amdgcn_readfirstlane(prio_hi ? 1u : 0u);
+#endif
   auto base_prio = [&]() {
     asm volatile(
         "s_cmp_lg_u32 %0, 0\n\ts_cbranch_scc0 .Lbp0_%=\n\ts_setprio 1\n\ts_branch .Lbp1_%=\n"
@@ -515,6 +527,10 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
     for (int k = 0; k < FFT_STAGGER; k++) __builtin_amdgcn_s_sleep(127);
 #endif
   for (int i = 0; i < n; i++) {
+#if FFT_PRIO == 6
+    prio_flag = ((unsigned)i >> FFT_PRIO_SH ^ prio_ph) & 1u;
+    base_prio();
+#endif
     // (X^a acc_c - acc_c), decomposed: the rotation image in this wave's own transpose area (its previous
     // user, the last inverse, is this wave: DS operations of a wave run in order)
     u32 st[16];

@@ -71,6 +71,12 @@ typedef __attribute__((address_space(3))) u64 lds_u64;
 #ifndef F1_STAGGER
 #define F1_STAGGER 0
 #endif
+#ifndef F1_PRIO_SH
+#define F1_PRIO_SH 0
+#endif
+#ifndef F1_TAILWG
+#define F1_TAILWG 512
+#endif
 
 template <int CTS>
 struct F1Shared {
@@ -168,12 +174,22 @@ __device__ __forceinline__ void rotate_digits(const u64 (&v)[32], int a, int lan
 
 // NW waves per workgroup: 8 (the MAC spread over 8 waves, 2 slots each) or 2 CTS (every wave a transform wave,
 // 16 / NW slots each; with CTS = 2 and 16 KB areas two workgroups share a CU)
+#ifndef FFT_WGTIME
+#define FFT_WGTIME 0
+#endif
+#if FFT_WGTIME
+// diagnostic build only (as pbs_fft.hip): per-workgroup start / end, HW_ID, XCC_ID of the last launch
+__device__ unsigned long long g_wgt2k[4 * 16384];
+#endif
 template <int CTS, int NW, bool WRITE_ACC, bool WRITE_BIG>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
     const u64* __restrict__ lwe_in, int n, size_t B, const u64* __restrict__ luts, const u32* __restrict__ lut_index,
     int n_lut, const double2* __restrict__ bsk, const double2* __restrict__ tg, u64* __restrict__ out_big,
     u64* __restrict__ out_acc) {
   __shared__ __attribute__((aligned(16))) F1Shared<CTS> sh;
+#if FFT_WGTIME
+  const unsigned long long wg_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wave_s = __builtin_amdgcn_readfirstlane(wave);
   const bool tw_wave = wave_s < 2 * CTS;
@@ -210,8 +226,22 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
   static_assert(NW == 8 || NW == 2 * CTS, "waves: 8, or one per polynomial");
   const int s0 = SPW * wave_s;  // MAC slots s0 .. s0 + SPW - 1
 #if F1_PRIO_ASM
+#if F1_PRIO == 6
+  // A/B (round 6, as pbs_fft.hip FFT_PRIO 6): the base priority alternates every 2^F1_PRIO_SH CMUXes, in opposite
+  // phase for the two dispatch halves
+  const unsigned prio_ph = __builtin_amdgcn_readfirstlane((blockIdx.x >> 8) & 1);
+  unsigned prio_flag = prio_ph;
+#elif F1_PRIO == 7
+  // A/B (round 6): F1_PRIO 3's dispatch-half alternation, except the last F1_TAILWG workgroups of the grid run at
+  // the base level, so the two final workgroups of a CU fall back to oldest-first arbitration (the one that started
+  // earlier finishes first) instead of the alternation's fast / slow pair (profiles/r06g_wgt_f2k_4096.json: the two
+  // slots of a CU end 1.9 ms apart)
+  const unsigned prio_flag = __builtin_amdgcn_readfirstlane(
+      (((blockIdx.x >> 8) & 1) && blockIdx.x + F1_TAILWG < gridDim.x) ? 1u : 0u);
+#else
   const unsigned prio_flag = __builtin_amdgcn_readfirstlane(
       (F1_PRIO == 3 && NW == 2 * CTS && ((blockIdx.x >> 8) & 1)) || (F1_PRIO == 1 && wave_s >= 4) ? 1u : 0u);
+#endif
 #endif
 #if F1_STAGGER
   // A/B (round 6, as pbs_fft.hip FFT_STAGGER): the second workgroup of each CU in the first dispatch round starts late
@@ -225,6 +255,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
   // the two workgroups of a CU just get an arbitrary split)
   if constexpr (NW == 2 * CTS)
     if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_setprio(1);
+#elif F1_PRIO == 7 && F1_PRIO_ASM
+  asm volatile(
+      "s_cmp_lg_u32 %0, 0\n\ts_cbranch_scc0 .Lfi0_%=\n\ts_setprio 1\n\ts_branch .Lfi1_%=\n"
+      ".Lfi0_%=:\n\ts_setprio 0\n.Lfi1_%=:" ::"s"(prio_flag) : "scc");
 #endif
   // key words of CMUX i for the MAC phase: kv[t][cc][j] = K_{cc,j}[slot s0 + t][lane].  The first KPRE slots are
   // requested at the CMUX start (their latency hides behind the forward transform); with 4 slots per wave the
@@ -240,6 +274,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
           for (int j = 0; j < 2; j++) kv[t][cc][j] = bsk[((size_t)(i * 2 + cc) * 2 + j) * M1 + 64 * (s0 + t) + lane];
   };
   auto cmux = [&](int i, double2 (&kv)[SPW][2][2]) {
+#if F1_PRIO_ASM && F1_PRIO == 6
+    prio_flag = ((unsigned)i >> F1_PRIO_SH ^ prio_ph) & 1u;
+    asm volatile(
+        "s_cmp_lg_u32 %0, 0\n\ts_cbranch_scc0 .Lfq0_%=\n\ts_setprio 1\n\ts_branch .Lfq1_%=\n"
+        ".Lfq0_%=:\n\ts_setprio 0\n.Lfq1_%=:" ::"s"(prio_flag) : "scc");
+#endif
     const int a = a_next;
     if (tw_wave && i + 1 < n) a_next = ms4096(ct[i + 1]);
     if (tw_wave) {
@@ -331,6 +371,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
     cmux(i, kv);
   }
 #endif
+#if FFT_WGTIME
+  if (threadIdx.x == 0 && blockIdx.x < 16384) {
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    g_wgt2k[4 * blockIdx.x] = wg_t0;
+    g_wgt2k[4 * blockIdx.x + 1] = t1;
+    g_wgt2k[4 * blockIdx.x + 2] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+    g_wgt2k[4 * blockIdx.x + 3] = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11));
+  }
+#endif
 
   if (!live) return;
   if (WRITE_ACC) {
@@ -413,6 +462,13 @@ __global__ void sample_extract_torus2k_kernel(const u64* __restrict__ acc, size_
 }
 
 }  // namespace fft1k
+
+#if FFT_WGTIME
+extern "C" int tfhe_hip_debug_wgtimes2k(unsigned long long* out, size_t n) {
+  if (n > 4 * 16384) n = 4 * 16384;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(fft1k::g_wgt2k), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t launch_sample_extract_torus2k(const u64* acc, size_t B, u64* out, hipStream_t s) {
   if (B == 0) return hipSuccess;

@@ -1,10 +1,11 @@
-"""Per-workgroup timeline of one P-GATE batch blind rotation (diagnostic build only: tools/ab_build.sh wgtime
--DFFT_WGTIME=1, run with TFHE_HIP_LIB=build_ab/wgtime/libtfhe_hip.so on the GPU box).
+"""Per-workgroup timeline of one batch blind rotation, P-GATE or P-FHEVM (diagnostic build only:
+make -C tfhe_amd B=../build_diag/wgt/obj LIB=../build_diag/wgt/libtfhe_hip.so EXTRA=-DFFT_WGTIME=1, run with
+TFHE_HIP_LIB=build_diag/wgt/libtfhe_hip.so on the GPU box).
 
 Reads each workgroup's start / end (s_memrealtime, 100 MHz), HW_ID and XCC_ID of the last launch and prints where the
 launch's time goes: workgroup durations, the dispatch rounds, and the drain (CU-slot time left idle after a slot's
 last workgroup while the launch is still running).
-  python tools/wg_timeline.py [--batch 4096] [--out gpurun_out/wg_timeline.json]"""
+  python tools/wg_timeline.py [--preset gate_fft|fhevm_fft] [--batch 4096] [--out gpurun_out/wg_timeline.json]"""
 import argparse
 import ctypes
 import json
@@ -21,17 +22,25 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--out", default="gpurun_out/wg_timeline.json")
+    ap.add_argument("--preset", choices=["gate_fft", "fhevm_fft"], default="gate_fft")
     a = ap.parse_args()
     import torch
-    params = tfhe_amd.Params.preset(tfhe_amd.PRESET_GATE_FFT)
+    fhevm = a.preset == "fhevm_fft"
+    params = tfhe_amd.Params.preset(tfhe_amd.PRESET_FHEVM_FFT if fhevm else tfhe_amd.PRESET_GATE_FFT)
     ck, sk = tfhe_amd.gen_keys(params, 0x7F4E0001)
     eng = tfhe_amd.Engine(params, 0).load_keys(sk)
     B = a.batch
-    bits = np.random.default_rng(1).integers(0, 2, B).astype(bool)
-    cts = ck.encrypt_bool(bits, seed=0xC0FFEE01)
+    if fhevm:
+        eng.load_ms_key(tfhe_amd.ms_zeros_keygen(params, 0x7F4E0001, ck.lwe_key))
+        cts = ck.encrypt((np.arange(B) % 16).astype(np.uint64), 16, seed=0xC0FFEE01)
+        lut = eng.generate_accumulator(lambda m: m, 16)
+    else:
+        bits = np.random.default_rng(1).integers(0, 2, B).astype(bool)
+        cts = ck.encrypt_bool(bits, seed=0xC0FFEE01)
+        lut = eng.gate_lut()
     dev = torch.device("cuda:0")
     d_in = torch.from_numpy(cts.view(np.int64)).to(dev)
-    d_lut = torch.from_numpy(eng.gate_lut().view(np.int64)).to(dev)
+    d_lut = torch.from_numpy(lut.view(np.int64)).to(dev)
     d_out = torch.empty_like(d_in)
     for _ in range(4):
         eng.pbs_async(d_in, d_lut, d_out)
@@ -39,8 +48,9 @@ def main():
     L = tfhe_amd.lib()
     nwg = (B + 1) // 2
     buf = np.zeros(4 * 16384, dtype=np.uint64)
-    L.tfhe_hip_debug_wgtimes.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
-    assert L.tfhe_hip_debug_wgtimes(buf.ctypes.data, buf.size) == 0
+    fn = L.tfhe_hip_debug_wgtimes2k if fhevm else L.tfhe_hip_debug_wgtimes
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    assert fn(buf.ctypes.data, buf.size) == 0
     t = buf[: 4 * nwg].reshape(nwg, 4)
     t0, t1 = t[:, 0].astype(np.int64), t[:, 1].astype(np.int64)
     base = t0.min()
@@ -77,6 +87,22 @@ def main():
     res["start_quantiles_us"] = [round(float(np.percentile(s_us, q)), 1) for q in (0, 25, 50, 75, 100)]
     res["per_xcc_span_us"] = {int(x): round(float(e_us[xcc == x].max()), 1) for x in np.unique(xcc)}
     res["per_xcc_mean_dur_us"] = {int(x): round(float(dur[xcc == x].mean()), 1) for x in np.unique(xcc)}
+    # the two workgroup slots of each CU (a workgroup takes the slot whose previous workgroup ended closest to its
+    # start): how far apart the slots' last workgroups end
+    by_cu = {}
+    for i, k in enumerate(slot_key):
+        by_cu.setdefault(int(k), []).append((s_us[i], e_us[i]))
+    diffs = []
+    for v in by_cu.values():
+        v.sort()
+        if len(v) < 2:
+            continue
+        ends = [v[0][1], v[1][1]]
+        for st, en in v[2:]:
+            j = 0 if abs(ends[0] - st) < abs(ends[1] - st) else 1
+            ends[j] = en
+        diffs.append(abs(ends[0] - ends[1]))
+    res["slot_end_diff_us"] = {"mean": round(float(np.mean(diffs)), 1), "max": round(float(np.max(diffs)), 1)}
     res["wg0_16"] = [[int(slot_key[i]), round(float(s_us[i]), 1), round(float(e_us[i]), 1)] for i in range(16)]
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     json.dump(res, open(a.out, "w"), indent=1)
