@@ -238,6 +238,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
   // slots of a CU end 1.9 ms apart)
   const unsigned prio_flag = __builtin_amdgcn_readfirstlane(
       (((blockIdx.x >> 8) & 1) && blockIdx.x + F1_TAILWG < gridDim.x) ? 1u : 0u);
+#elif F1_PRIO == 8
+  // A/B: the dispatch-half alternation inverted for the last F1_TAILWG workgroups
+  const unsigned prio_flag = __builtin_amdgcn_readfirstlane(
+      ((((blockIdx.x >> 8) & 1) != 0) != (blockIdx.x + F1_TAILWG >= gridDim.x)) ? 1u : 0u);
 #else
   const unsigned prio_flag = __builtin_amdgcn_readfirstlane(
       (F1_PRIO == 3 && NW == 2 * CTS && ((blockIdx.x >> 8) & 1)) || (F1_PRIO == 1 && wave_s >= 4) ? 1u : 0u);
@@ -255,7 +259,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
   // the two workgroups of a CU just get an arbitrary split)
   if constexpr (NW == 2 * CTS)
     if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_setprio(1);
-#elif F1_PRIO == 7 && F1_PRIO_ASM
+#elif (F1_PRIO == 7 || F1_PRIO == 8) && F1_PRIO_ASM
   asm volatile(
       "s_cmp_lg_u32 %0, 0\n\ts_cbranch_scc0 .Lfi0_%=\n\ts_setprio 1\n\ts_branch .Lfi1_%=\n"
       ".Lfi0_%=:\n\ts_setprio 0\n.Lfi1_%=:" ::"s"(prio_flag) : "scc");

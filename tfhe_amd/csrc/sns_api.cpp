@@ -55,13 +55,15 @@ struct DevGuard {
   }
 };
 
-// ciphertexts per pass (acc 96 KB + digit spectra 147 KB + MAC products 246 KB each);
-// TFHE_HIP_SNS_CHUNK overrides
+// ciphertexts per pass (acc 96 KB + digit spectra 147 KB + MAC products 246 KB each); TFHE_HIP_SNS_CHUNK overrides.
+// 512 since round 6: a 1024 batch as two 512 chunks measured 4,819 vs 4,556 squashes/s (256: 4,455) on one box
+// (profiles/r06c_sns_chunk.txt; round 5: 4,687 vs 4,568): the inverse gains more from the smaller per-CMUX working set
+// than the MAC and step 1 lose to the half-size grids
 size_t sns_chunk() {
   static const size_t v = [] {
     const char* e = getenv("TFHE_HIP_SNS_CHUNK");
     const long x = e ? atol(e) : 0;
-    return x > 0 ? (size_t)x : (size_t)1024;
+    return x > 0 ? (size_t)x : (size_t)512;
   }();
   return v;
 }
