@@ -253,6 +253,12 @@ struct FpShared<CTS, false> {
 #ifndef FFT_PRIO_SH
 #define FFT_PRIO_SH 0
 #endif
+#ifndef FFT_ROTPRIO
+#define FFT_ROTPRIO 0
+#endif
+#ifndef FFT_XCHPRIO
+#define FFT_XCHPRIO 0
+#endif
 typedef __attribute__((address_space(3))) u64 lds_u64;
 
 // FFT_ROT_UNIFORM 1 (default since round 5): the rotation split so that every per-slot decision is wave-uniform.
@@ -534,6 +540,9 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
     // (X^a acc_c - acc_c), decomposed: the rotation image in this wave's own transpose area (its previous
     // user, the last inverse, is this wave: DS operations of a wave run in order)
     u32 st[16];
+#if FFT_ROTPRIO
+    __builtin_amdgcn_s_setprio(FFT_ROTPRIO);  // A/B: the rotation phase at a raised priority
+#endif
     rotate_states(acc, ms2048(ct[i]), lane, T, st);
     double o0r[8], o0i[8], o1r[8], o1i[8];
     // level steps q = 0, 1, 2 (least significant first), each specialised at compile time: q = 0 starts the two
@@ -542,7 +551,7 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
       constexpr int q = decltype(qc)::value;
       const int g = 3 * i + q;
 #if FFT_MACPRIO
-      if (q > 0) base_prio();
+      if (q > 0 || FFT_ROTPRIO) base_prio();
 #endif
       if constexpr (LDS_TW) {
         glds_barrier();  // step g's chunk is in K[g & 1]; every wave is done with K[(g + 1) & 1]
@@ -596,13 +605,16 @@ __global__ __launch_bounds__(128 * CTS, 4 / CTS) void blind_rotate_fft_pair_kern
     level(std::integral_constant<int, 0>{});
     level(std::integral_constant<int, 1>{});
     level(std::integral_constant<int, 2>{});
-#if FFT_MACPRIO
+#if FFT_MACPRIO && !FFT_XCHPRIO
     base_prio();
 #endif
     // exchange the partial sums: publish O_(1-c)^c, take O_c^(1-c) (c wave-uniform: a scalar branch, no selects)
     double xr[8], xi[8];
     if (c_s) exchange_partials<1>(o0r, o0i, o1r, o1i, xr, xi, T, Tp, lane);
     else exchange_partials<0>(o0r, o0i, o1r, o1i, xr, xi, T, Tp, lane);
+#if FFT_MACPRIO && FFT_XCHPRIO
+    base_prio();  // A/B: the partial-sum exchange still at the MAC's priority
+#endif
 #if FFT_PAIR_TWREG >= 2
     dft512_inv_rb(xr, xi, T, lane, tb, wb, twI);
 #else
