@@ -272,6 +272,29 @@ __device__ __forceinline__ void fft_inv_reg(const cd* __restrict__ o, cd* buf, c
   snsf::r4_dit(y[0], y[1], y[2], y[3], t, T);  // dit_stage(s = 0): base t, q 256, e = t
 }
 
+#ifndef SNS_INV_V2
+#define SNS_INV_V2 1
+#endif
+#if SNS_INV_V2
+// Default since round 6 (+2 %: 234.4 -> 229.8 ms per 1024 squashes on one box, 4,369 -> 4,457/s, the squash tests
+// bit-exact; profiles/r06i_sns_inv2_ab.txt): the same inverse (every butterfly, twiddle and rounding identical) with
+//   * the thread's 12 stage twiddles and 4 untwist factors read once per workgroup into registers (the limbs share them),
+//   * LDS-only barriers (s_waitcnt lgkmcnt(0) + s_barrier: __syncthreads also drains vmcnt),
+//   * the next limb's 4 points requested before this limb's stages, so their global latency overlaps them.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void r4_dit_w(cd& y0, cd& y1, cd& y2, cd& y3, cd w1, cd w2, cd w3) {
+  y1 = snsf::cmulc(y1, w1);
+  y2 = snsf::cmulc(y2, w2);
+  y3 = snsf::cmulc(y3, w3);
+  const cd b0 = snsf::cadd(y0, y2), b1 = snsf::csub(y0, y2), b2 = snsf::cadd(y1, y3), d = snsf::csub(y1, y3);
+  const cd b3 = {d.y, -d.x};
+  y0 = snsf::cadd(b0, b2);
+  y1 = snsf::cadd(b1, b3);
+  y2 = snsf::csub(b0, b2);
+  y3 = snsf::csub(b1, b3);
+}
+#endif
+
 // (ciphertext, output j): the 5 inverse transforms one after another by all 256 threads, top limb first;
 // each thread untwists and rounds its 8 coefficients (limbs 4..1: |c| < 2^53, exact) and folds them into u128
 // Horner sums h = (h << 16) + c, then h = (h << 48) + c_0 for the low limb (|c_0| < 2^85, converted from the
@@ -319,6 +342,85 @@ __global__ void __launch_bounds__(ST, SNS_INV_OCC) sns_inv_kernel(const cd* __re
       st128(a, x, ld128(a, x) + (h[2 * u + hh] << 16));
     }
 }
+
+#if SNS_INV_V2
+__global__ void __launch_bounds__(ST, SNS_INV_OCC) sns_inv2_kernel(const cd* __restrict__ O, u64* __restrict__ acc,
+                                                         const SnsFftConst* __restrict__ Fc) {
+  __shared__ cd buf[SF_M];
+  const int j = blockIdx.x % (SK + 1), ct = blockIdx.x / (SK + 1);
+  const SnsFftConst& F = *Fc;
+  const int t = threadIdx.x;
+  const cd* ob = O + ((size_t)ct * MAC_JT + j * SF_LIMBS) * SF_M;
+  cd nx[4];  // the next limb's points 4t .. 4t + 3
+#pragma unroll
+  for (int k = 0; k < 4; k++) nx[k] = ob[(size_t)(SF_LIMBS - 1) * SF_M + 4 * t + k];
+  // stage twiddles (dit_stage s = 3, 2, 1: e = (t & (q - 1)) << 2s; stage 0: e = t) and the untwist factors
+  cd w[4][3], pu[4];
+#pragma unroll
+  for (int s = 3; s >= 1; s--) {
+    const int lq = 8 - 2 * s, e = (t & ((1 << lq) - 1)) << (2 * s);
+    w[s][0] = F.T[e];
+    w[s][1] = F.T[2 * e];
+    w[s][2] = F.T[3 * e];
+  }
+  const cd w4 = F.T[0];
+  w[0][0] = F.T[t];
+  w[0][1] = F.T[2 * t];
+  w[0][2] = F.T[3 * t];
+#pragma unroll
+  for (int u = 0; u < 4; u++) pu[u] = F.P[t + 256 * u];
+  u128 h[8];
+#pragma unroll
+  for (int e = 0; e < 8; e++) h[e] = 0;
+#pragma unroll 1
+  for (int l = SF_LIMBS - 1; l >= 0; l--) {
+    cd y[4] = {nx[0], nx[1], nx[2], nx[3]};
+    if (l > 0) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) nx[k] = ob[(size_t)(l - 1) * SF_M + 4 * t + k];
+    }
+    r4_dit_w(y[0], y[1], y[2], y[3], w4, w4, w4);  // stage 4: e = 0, the shipped kernel's multiplies by T[0] kept
+#pragma unroll
+    for (int k = 0; k < 4; k++) buf[4 * t + k] = y[k];
+    lds_barrier();
+#pragma unroll
+    for (int s = 3; s >= 1; s--) {
+      const int lq = 8 - 2 * s;
+      const int q = 1 << lq, jj = t & (q - 1), base = ((t >> lq) << (lq + 2)) + jj;
+      cd z0 = buf[base], z1 = buf[base + q], z2 = buf[base + 2 * q], z3 = buf[base + 3 * q];
+      r4_dit_w(z0, z1, z2, z3, w[s][0], w[s][1], w[s][2]);
+      buf[base] = z0;
+      buf[base + q] = z1;
+      buf[base + 2 * q] = z2;
+      buf[base + 3 * q] = z3;
+      lds_barrier();
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) y[k] = buf[t + 256 * k];
+    r4_dit_w(y[0], y[1], y[2], y[3], w[0][0], w[0][1], w[0][2]);
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const cd yy = snsf::cmulc(y[u], pu[u]);
+      if (l > 0) {
+        h[2 * u] = snsf::horner16(h[2 * u], __builtin_rint(yy.x));
+        h[2 * u + 1] = snsf::horner16(h[2 * u + 1], __builtin_rint(yy.y));
+      } else {
+        h[2 * u] = snsf::horner_low(h[2 * u], __builtin_rint(yy.x));
+        h[2 * u + 1] = snsf::horner_low(h[2 * u + 1], __builtin_rint(yy.y));
+      }
+    }
+    lds_barrier();
+  }
+  u64* a = acc + ((size_t)ct * (SK + 1) + j) * 2 * SN;
+#pragma unroll
+  for (int u = 0; u < 4; u++)
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++) {
+      const int x = threadIdx.x + 256 * u + SF_M * hh;
+      st128(a, x, ld128(a, x) + (h[2 * u + hh] << 16));
+    }
+}
+#endif
 
 // acc -> LWE over Z_2^128 (dim k N, + body), (lo, hi) pairs: a'_(cN) = A_c[0], a'_(cN + t) = -A_c[N - t]
 __global__ void sns_extract_kernel(const u64* __restrict__ acc, u64* __restrict__ out) {
@@ -373,7 +475,11 @@ hipError_t launch_sns_blind_rotate(const u64* lwe, size_t B, int n, const u64* l
   for (int i = 0; i < n; i++) {
     sns_step1f_kernel<<<g3, ST, 0, s>>>(lwe, n, i, acc, (cd*)D, F);
     sns_mac_kernel<<<mac_grid, ST, 0, s>>>((const cd*)D, (const cd*)bsk_fft + per_i * i, (cd*)Oprod, (int)B);
+#if SNS_INV_V2
+    sns_inv2_kernel<<<g3, ST, 0, s>>>((const cd*)Oprod, acc, F);
+#else
     sns_inv_kernel<<<g3, ST, 0, s>>>((const cd*)Oprod, acc, F);
+#endif
   }
   return hipGetLastError();
 }

@@ -1,5 +1,6 @@
 #!/bin/bash
-# End-of-round evidence on the final tree: the whole -m gpu suite (SUITE), the profile set of both FFT64 presets
+# End-of-round evidence on the final tree: the whole -m gpu suite (SUITE), the profile set of both FFT64 presets and of
+# C3 (C3=1: bench.py --config c3, 32,768 PBS per launch)
 # (PROFILES; tools/profile_round.sh: rocprofv3 kernel stats, SQ / FETCH / WRITE / mix counter passes -> <TAG>_roofline.json
 # tagged with this tree's source_id, then the bench line with the CPU baseline reading it), and EXTRA: C2, the squash
 # profile (tools/gpu_sns_prof.sh) and C5 (tools/c5_bench.py).  Stops at the first failure.  Split over two calls to stay
@@ -19,6 +20,10 @@ if [ "${PROFILES:-1}" = "1" ]; then
   tail -3 gpurun_out/${TAG}_prof.log
   TAG=${TAG}_fhevm PRESET=fhevm_fft bash tools/profile_round.sh > gpurun_out/${TAG}_fhevm_prof.log 2>&1 || { echo "fhevm profile failed"; tail -20 gpurun_out/${TAG}_fhevm_prof.log; exit 1; }
   tail -3 gpurun_out/${TAG}_fhevm_prof.log
+fi
+if [ "${C3:-1}" = "1" ]; then  # BASELINE configs[2]: 4096 FheUint8 x 8 LUTs = 32,768 PBS per launch (bench.py --config c3)
+  TAG=${TAG}_c3 PRESET=gate_fft ARGS="--config c3" BATCH=32768 MIX=0 bash tools/profile_round.sh > gpurun_out/${TAG}_c3_prof.log 2>&1 || { echo "c3 profile failed"; tail -20 gpurun_out/${TAG}_c3_prof.log; exit 1; }
+  tail -3 gpurun_out/${TAG}_c3_prof.log
 fi
 if [ "${EXTRA:-1}" = "1" ]; then  # C2 (batch 1024), the squash bench + kernel stats, C5 timed
   timeout -k 10 300 python -u bench.py --batch 1024 --steps 10 --warmup 3 --no-cpu > gpurun_out/${TAG}_c2_bench.json 2> gpurun_out/${TAG}_c2_bench.err || { echo "C2 bench failed"; tail gpurun_out/${TAG}_c2_bench.err; exit 1; }
