@@ -596,6 +596,12 @@ static void monomial_torus(uint64_t* out, const uint64_t* in, uint32_t N, uint32
   }
 }
 
+/* the N = 2048 MAC order: 0 = one fma chain over every (c, l) from zero (pbs_fft2k.hip's slot-owned MAC), 1 = the
+ * split order of N = 1024 (per-component products, then one add: pbs_fft2k.hip F1_PAIRMAC).  A/B switch, set through
+ * or_set_fft2k_mac_split (oracle.py: ORACLE_FFT2K_SPLIT=1) */
+int or_fft2k_mac_split = 0;
+void or_set_fft2k_mac_split(int v) { or_fft2k_mac_split = v != 0; }
+
 /* trace (nullable): (n + 1) x (k+1)N words, the accumulator before CMUX 0 and after every CMUX i (skipped CMUXes
  * included), so tests can hand each state to the exact arbiter (exact_oracle.c) */
 static void blind_rotate_fft_impl(const or_params* p, const or_c64* bsk_f, const uint64_t* lwe_in, const uint64_t* lut,
@@ -613,7 +619,7 @@ static void blind_rotate_fft_impl(const or_params* p, const or_c64* bsk_f, const
   /* MAC order.  N = 1024 (pbs_fft.hip: component-pair and latency kernels): one fma chain per component,
    * O_j = O_j^0 + O_j^1 with O_j^c = chain over the levels of D_(c,l) (.) BSK_i[(c, l)][j] from zero.
    * N = 2048 (pbs_fft2k.hip): one chain over every (c, l) from zero. */
-  const int split = N == 2 * FFT_M;
+  const int split = N == 2 * FFT_M || or_fft2k_mac_split;
   double res[4 * FFT_M];
   int64_t d[64];
   const size_t row = (size_t)(k + 1) * N;

@@ -78,6 +78,8 @@ def lib():
         L.or_f64_to_torus.argtypes = [ctypes.c_double]
         L.or_f64_to_torus_dev.restype = ctypes.c_uint64
         L.or_f64_to_torus_dev.argtypes = [ctypes.c_double]
+        if os.environ.get("ORACLE_FFT2K_SPLIT") == "1":  # A/B of the N = 2048 MAC order (fft_oracle.c)
+            L.or_set_fft2k_mac_split(1)
         _LIB = L
     return _LIB
 

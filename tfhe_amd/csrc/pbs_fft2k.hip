@@ -77,6 +77,12 @@ typedef __attribute__((address_space(3))) u64 lds_u64;
 #ifndef F1_TAILWG
 #define F1_TAILWG 512
 #endif
+#ifndef F1_PAIRMAC
+#define F1_PAIRMAC 0
+#endif
+#ifndef F1_PAIRMAC_KG
+#define F1_PAIRMAC_KG 2
+#endif
 
 template <int CTS>
 struct F1Shared {
@@ -194,6 +200,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
   const int wave_s = __builtin_amdgcn_readfirstlane(wave);
   const bool tw_wave = wave_s < 2 * CTS;
   const int c = wave & 1, p = tw_wave ? wave >> 1 : 0;
+  [[maybe_unused]] const int c_u = wave_s & 1;  // wave-uniform c (scalar branches)
   const size_t b_raw = (size_t)blockIdx.x * CTS + p;
   const bool live = tw_wave && b_raw < B;
   const size_t b = b_raw < B ? b_raw : B - 1;  // padding waves run a copy of the last ciphertext, store nothing
@@ -310,6 +317,18 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
 #pragma unroll
         for (int j = 0; j < 2; j++) {
           const double2 k0 = kv[t][0][j], k1 = kv[t][1][j];
+#if F1_PAIRMAC
+          // the split order (oracle: per-component products, then one add -- as the P-GATE kernels)
+          double r0 = d0.x * k0.x;
+          r0 = __builtin_fma(-d0.y, k0.y, r0);
+          double i0 = d0.x * k0.y;
+          i0 = __builtin_fma(d0.y, k0.x, i0);
+          double r1 = d1.x * k1.x;
+          r1 = __builtin_fma(-d1.y, k1.y, r1);
+          double i1 = d1.x * k1.y;
+          i1 = __builtin_fma(d1.y, k1.x, i1);
+          o[j] = make_double2(r0 + r1, i0 + i1);
+#else
           double re = __builtin_fma(d0.x, k0.x, 0.0);
           re = __builtin_fma(-d0.y, k0.y, re);
           double im = __builtin_fma(d0.x, k0.y, 0.0);
@@ -319,6 +338,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
           im = __builtin_fma(d1.x, k1.y, im);
           im = __builtin_fma(d1.y, k1.x, im);
           o[j] = make_double2(re, im);
+#endif
         }
         sh.area[2 * q][idx] = o[0];
         sh.area[2 * q + 1][idx] = o[1];
@@ -358,6 +378,90 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
       }
     }
   };
+#if F1_PAIRMAC
+  // A/B (round 6): the batch form with the P-GATE kernel's MAC.  Wave (p, c) multiplies its own spectrum D_c by both
+  // key polynomials of component c (read from L2, four slots ahead), publishes the product for the other output
+  // (D_c (.) K_(c, 1-c)) in its area and keeps D_c (.) K_(c, c) in registers; after one barrier it adds the partner's
+  // D_(1-c) (.) K_(1-c, c): O_c = O_c^0 + O_c^1, the oracle's split order.  Against the slot-owned MAC: no spectrum
+  // store, no MAC-phase reads / writes of both spectra (16 b128 LDS writes and 16 reads fewer per wave and CMUX), twice
+  // the key words per wave from L2 (32 instead of 16 b128 loads), one barrier pair as before.
+  if constexpr (NW == 2 * CTS) {
+    const double2* Tp = sh.area[wave ^ 1];
+    for (int i = 0; i < n; i++) {
+      const int a = a_next;
+      if (i + 1 < n) a_next = ms4096(ct[i + 1]);
+      const double2* kc = bsk + (size_t)(i * 2 + c) * 2 * M1 + lane;  // K_(c, j)[s] = kc[j M1 + 64 s]
+      constexpr int KG = F1_PAIRMAC_KG;  // key slots per prefetch group
+      double2 kv[KG][2];
+#pragma unroll
+      for (int t = 0; t < KG; t++) {
+        kv[t][0] = kc[64 * t];
+        kv[t][1] = kc[M1 + 64 * t];
+      }
+      double xr[16], xi[16];
+      rotate_digits(acc, a, lane, area, xr, xi);
+      fft1k_fwd(xr, xi, area, lane, sh.ta, tb);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int g = 0; g < 16 / KG; g++) {
+        __builtin_amdgcn_sched_barrier(0);  // keep each group's key loads in their group (no hoisting of all 32)
+        double2 kn[KG][2];
+        if (g + 1 < 16 / KG) {
+#pragma unroll
+          for (int t = 0; t < KG; t++) {
+            kn[t][0] = kc[64 * (KG * (g + 1) + t)];
+            kn[t][1] = kc[M1 + 64 * (KG * (g + 1) + t)];
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < KG; t++) {
+          const int sl = KG * g + t;
+          const double dr = xr[sl], di = xi[sl];
+          double pr[2], pi[2];
+#pragma unroll
+          for (int j = 0; j < 2; j++) {
+            const double2 k = kv[t][j];
+            pr[j] = dr * k.x;
+            pr[j] = __builtin_fma(-di, k.y, pr[j]);
+            pi[j] = dr * k.y;
+            pi[j] = __builtin_fma(di, k.x, pi[j]);
+          }
+          // c wave-uniform: the own output c stays, output 1 - c goes to the area
+          if (c_u) {
+            area[64 * sl + lane] = make_double2(pr[0], pi[0]);
+            xr[sl] = pr[1];
+            xi[sl] = pi[1];
+          } else {
+            area[64 * sl + lane] = make_double2(pr[1], pi[1]);
+            xr[sl] = pr[0];
+            xi[sl] = pi[0];
+          }
+        }
+        if (g + 1 < 16 / KG) {
+#pragma unroll
+          for (int t = 0; t < KG; t++) {
+            kv[t][0] = kn[t][0];
+            kv[t][1] = kn[t][1];
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int sl = 0; sl < 16; sl++) {
+        const double2 v = Tp[64 * sl + lane];
+        xr[sl] = xr[sl] + v.x;
+        xi[sl] = xi[sl] + v.y;
+      }
+      __syncthreads();  // the partner has read this wave's area before the inverse overwrites it
+      fft1k_inv(xr, xi, area, lane, sh.ta, tb);
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        acc[e] = torus_acc_add_wide_y(acc[e], xr[e]);
+        acc[e + 16] = torus_acc_add_wide_y(acc[e + 16], xi[e]);
+      }
+    }
+  } else
+#endif
 #if F1_KPF
   double2 kva[SPW][2][2], kvb[SPW][2][2];  // one CMUX ahead
   load_key(0, kva, false);
