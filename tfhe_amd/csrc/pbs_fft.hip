@@ -884,9 +884,45 @@ __device__ __forceinline__ void lat_load_key(const double2* __restrict__ bsk, in
     for (int t = 0; t < 2; t++) kv[r][t] = bsk[((size_t)(i * 6 + r) * 2 + j) * M + 64 * (s0 + t) + lane];
 }
 
+// FFT_LAT_LDSBAR 1 (round 6): the latency kernel's three barriers per CMUX wait for LDS only (s_waitcnt lgkmcnt(0) +
+// s_barrier).  Every cross-wave exchange of the kernel goes through LDS; __syncthreads also drains vmcnt, which made
+// the first barrier of CMUX i wait for the key words of CMUX i + 1 that FFT_LAT_PREFETCH had just requested (an L2 /
+// HBM round trip on the critical path of every CMUX) -- with LDS-only barriers they stay in flight for a whole CMUX.
+#ifndef FFT_LAT_LDSBAR
+#define FFT_LAT_LDSBAR 1
+#endif
+__device__ __forceinline__ void lat_barrier() {
+#if FFT_LAT_LDSBAR
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+  __syncthreads();
+#endif
+}
+
 // one CMUX of the latency kernel (phases A, B, C and their three barriers)
+#ifndef FFT_LATSTAMP
+#define FFT_LATSTAMP 0
+#endif
+#if FFT_LATSTAMP
+// diagnostic build only: per-CMUX phase times of the latency kernel (s_memrealtime, 100 MHz), summed per wave:
+// [0] CMUX start -> this wave done with phase A (before barrier 1), [1] -> past barrier 1, [2] -> done with phase B,
+// [3] -> past barrier 2, [4] -> done with phase C, [5] -> past barrier 3
+struct LatStamp {
+  unsigned long long acc[6] = {0, 0, 0, 0, 0, 0}, t0 = 0;
+  __device__ __forceinline__ void start() { t0 = __builtin_amdgcn_s_memrealtime(); }
+  __device__ __forceinline__ void mark(int k) { acc[k] += __builtin_amdgcn_s_memrealtime() - t0; }
+};
+__device__ unsigned long long g_latst[8 * 8 * 6];  // workgroup 0..7 x wave x phase mark
+#define LS_START(st) st.start()
+#define LS_MARK(st, k) st.mark(k)
+#else
+struct LatStamp {};
+#define LS_START(st)
+#define LS_MARK(st, k)
+#endif
 __device__ __forceinline__ void lat_cmux(FftLatShared& sh, const u64* __restrict__ ct, int i, int wave, int lane,
-                                         TBase tb, int j, int s0, const double2 (&kv)[6][2]) {
+                                         TBase tb, int j, int s0, const double2 (&kv)[6][2], LatStamp& ls) {
+  LS_START(ls);
   const int a = i < FL_MAXN ? (int)sh.ab[i] : ms2048(ct[i]);
   if (wave < 6) {  // phase A
     const int c = wave / 3, q = wave % 3;
@@ -915,7 +951,9 @@ __device__ __forceinline__ void lat_cmux(FftLatShared& sh, const u64* __restrict
 #pragma unroll
     for (int e = 0; e < 8; e++) sh.F[wave][64 * e + lane] = make_double2(xr[e], xi[e]);
   }
-  __syncthreads();
+  LS_MARK(ls, 0);
+  lat_barrier();
+  LS_MARK(ls, 1);
   {  // phase B
     double2* O = sh.T[2 + j];
 #pragma unroll
@@ -932,7 +970,9 @@ __device__ __forceinline__ void lat_cmux(FftLatShared& sh, const u64* __restrict
       O[64 * e + lane] = make_double2(re[0] + re[1], im[0] + im[1]);
     }
   }
-  __syncthreads();
+  LS_MARK(ls, 2);
+  lat_barrier();
+  LS_MARK(ls, 3);
   if (wave < 2) {  // phase C
     const double2* O = sh.T[2 + wave];
     double xr[8], xi[8];
@@ -950,7 +990,9 @@ __device__ __forceinline__ void lat_cmux(FftLatShared& sh, const u64* __restrict
       acc[64 * (e + 8) + lane] = ACC_ADD(acc[64 * (e + 8) + lane], xi[e]);
     }
   }
-  __syncthreads();
+  LS_MARK(ls, 4);
+  lat_barrier();
+  LS_MARK(ls, 5);
 }
 
 template <bool WRITE_ACC, bool WRITE_BIG>
@@ -984,6 +1026,7 @@ __global__ __launch_bounds__(FL_THREADS, 1) void blind_rotate_fft_lat_kernel(
   __syncthreads();
 
   const int j = wave >> 2, s0 = (wave & 3) * 2;  // phase B: output j, slots s0, s0 + 1
+  LatStamp ls;
 #if FFT_LAT_PREFETCH
   // key words one CMUX ahead (two register sets, the loop unrolled by two): a CMUX's row arrives while the
   // previous CMUX runs instead of behind this CMUX's phase A
@@ -991,19 +1034,23 @@ __global__ __launch_bounds__(FL_THREADS, 1) void blind_rotate_fft_lat_kernel(
   lat_load_key(bsk, 0, j, s0, lane, kva);
   for (int i = 0; i < n; i += 2) {
     if (i + 1 < n) lat_load_key(bsk, i + 1, j, s0, lane, kvb);
-    lat_cmux(sh, ct, i, wave, lane, tb, j, s0, kva);
+    lat_cmux(sh, ct, i, wave, lane, tb, j, s0, kva, ls);
     if (i + 1 >= n) break;
     if (i + 2 < n) lat_load_key(bsk, i + 2, j, s0, lane, kva);
-    lat_cmux(sh, ct, i + 1, wave, lane, tb, j, s0, kvb);
+    lat_cmux(sh, ct, i + 1, wave, lane, tb, j, s0, kvb, ls);
   }
 #else
   for (int i = 0; i < n; i++) {
     double2 kv[6][2];  // phase-B key words of this CMUX, requested now, consumed after phase A
     lat_load_key(bsk, i, j, s0, lane, kv);
-    lat_cmux(sh, ct, i, wave, lane, tb, j, s0, kv);
+    lat_cmux(sh, ct, i, wave, lane, tb, j, s0, kv, ls);
   }
 #endif
 
+#if FFT_LATSTAMP
+  if (lane == 0 && b < 8)
+    for (int k = 0; k < 6; k++) g_latst[(b * 8 + wave) * 6 + k] = ls.acc[k];
+#endif
   if (WRITE_ACC) {
     u64* oa = out_acc + b * 2048;
     for (int q = threadIdx.x; q < 2 * N1K; q += FL_THREADS) oa[q] = sh.A[q >> 10][q & (N1K - 1)];
@@ -1161,6 +1208,12 @@ hipError_t launch_blind_rotate_fft(const u64* lwe_in, size_t B, int n, const u64
   return hipGetLastError();
 }
 
+#if FFT_LATSTAMP
+extern "C" int tfhe_hip_debug_latstamps(unsigned long long* out, size_t n) {
+  if (n > 8 * 8 * 6) n = 8 * 8 * 6;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(fftk::g_latst), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 #if FFT_WGTIME
 extern "C" int tfhe_hip_debug_wgtimes(unsigned long long* out, size_t n) {
   if (n > 4 * 16384) n = 4 * 16384;

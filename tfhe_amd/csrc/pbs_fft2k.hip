@@ -84,6 +84,19 @@ typedef __attribute__((address_space(3))) u64 lds_u64;
 #define F1_PAIRMAC_KG 2
 #endif
 
+// F1_LDSBAR (A/B, round 6): the CMUX's two barriers wait for LDS only (s_waitcnt lgkmcnt(0) + s_barrier) instead of
+// __syncthreads' vmcnt(0) as well, so key words requested ahead (F1_KPF) stay in flight across them
+#ifndef F1_LDSBAR
+#define F1_LDSBAR 0
+#endif
+__device__ __forceinline__ void f1_barrier() {
+#if F1_LDSBAR
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+  __syncthreads();
+#endif
+}
+
 template <int CTS>
 struct F1Shared {
   double2 ta[M1];                 // pass A table (K_TA)
@@ -303,7 +316,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
     // the other key slots: requested before the barrier (the transform's registers are free by now), so their
     // latency overlaps the wait (+0.3-0.5 %, profiles/r04i_fhevm_2wg_ab.txt)
     if constexpr (SPW > KPRE) load_key(i, kv, true);
-    __syncthreads();
+    f1_barrier();
 #if F1_MACPRIO
     __builtin_amdgcn_s_setprio(3);  // the short MAC phase ahead of the other workgroup's transforms
 #endif
@@ -344,7 +357,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void blind_rotate_fft2k_kernel(
         sh.area[2 * q + 1][idx] = o[1];
       }
     }
-    __syncthreads();
+    f1_barrier();
 #if F1_MACPRIO  // back to the workgroup's level (F1_PRIO)
 #if F1_PRIO_ASM
     // one asm block with its own scalar branch (as pbs_fft.hip's base_prio): no C-level branch in the CMUX loop
