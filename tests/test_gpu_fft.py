@@ -106,15 +106,17 @@ def test_batch_4096_decrypts_and_sampled_bitexact(fft_engine, fft_keys, oracle_m
     cts = ck.encrypt_bool(bits, seed=0xC0FFEE03)
     out = fft_engine.pbs(cts, fft_engine.gate_lut())
     assert np.array_equal(ck.decrypt_bool(out), bits)
-    sample = np.r_[0:16, 4080:4096]
+    # ends of the batch, plus the workgroup boundaries where the pair kernel's wave priority (blockIdx bit 8) and
+    # its start stagger (workgroups 256..511) switch: 2 ciphertexts per workgroup, so ciphertexts 512, 1024, 2048
+    sample = np.r_[0:16, 510:514, 1022:1026, 2046:2050, 4080:4096]
     ref = oracle_mod.pbs_batch_fft(fft_params, fft_okeys, cts[sample], oracle_mod.lut_constant(N, 1 << 61)[None])
     assert np.array_equal(out[sample], ref)
 
 
 def test_batch_kernel_ragged_workgroups_agree(fft_engine, fft_keys):
-    """The component-pair batch kernel runs 4 ciphertexts per workgroup at any batch size above the latency
-    range: a ragged batch (1025 = 256 full workgroups + one with three padding pairs) gives every ciphertext the
-    same output as its first 1024 alone, and every output decrypts."""
+    """The component-pair batch kernel runs 2 ciphertexts x 2 component waves per workgroup at any batch size above
+    the latency range: a ragged batch (1025 = 512 full workgroups + one with a padding ciphertext) gives every
+    ciphertext the same output as its first 1024 alone, and every output decrypts."""
     ck, _ = fft_keys
     bits = np.random.default_rng(0x4A8).integers(0, 2, 1025).astype(bool)
     cts = ck.encrypt_bool(bits, seed=0xC0FFEE4A)
@@ -128,7 +130,7 @@ def test_batch_kernel_ragged_workgroups_agree(fft_engine, fft_keys):
 @pytest.mark.parametrize("B", [1, 9, 300])
 def test_latency_and_batch_kernels_agree(fft_engine, fft_keys, oracle_mod, fft_params, fft_okeys, B):
     """The latency-mode kernel (one ciphertext per workgroup, 6 transforms in parallel) and the component-pair
-    batch kernel (4 ciphertexts x 2 waves per workgroup) produce identical accumulators and PBS outputs."""
+    batch kernel (2 ciphertexts x 2 component waves per workgroup) produce identical accumulators and PBS outputs."""
     ck, _ = fft_keys
     rng = np.random.default_rng(B + 1024)
     msgs = rng.integers(0, 8, B).astype(np.uint64) * np.uint64((1 << 63) // 8)

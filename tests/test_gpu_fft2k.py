@@ -98,7 +98,9 @@ def test_pbs2k_batch_4096_decrypts_and_sampled_bitexact(f2_engine, f2_keys, orac
     cts = ck.encrypt(msgs, MM, seed=0xC0FFEE80)
     out = f2_engine.pbs(cts, acc)
     assert np.array_equal(ck.decrypt(out, MM), np.array([f(int(m)) for m in msgs], dtype=np.uint64))
-    sample = np.r_[0:8, 4088:4096]
+    # batch ends plus the workgroup boundaries where the wave priority (blockIdx bit 8, 2 ciphertexts per workgroup)
+    # switches: ciphertexts 512 and 1024
+    sample = np.r_[0:8, 510:514, 1022:1026, 4088:4096]
     assert np.array_equal(out[sample], oracle_mod.pbs_batch_fft(f2_prm, f2_okeys, cts[sample], acc[None]))
     out2 = f2_engine.pbs(out[:512], acc)  # chained: f(f(m))
     assert np.array_equal(ck.decrypt(out2, MM), np.array([f(f(int(m))) for m in msgs[:512]], dtype=np.uint64))
