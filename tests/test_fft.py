@@ -185,6 +185,31 @@ def test_oracle_pbs_decrypts(oracle_mod, fft_keys):
     assert max(abs(e) for e in err) < 2**60  # 1/16 of the torus: inside the 1/8 gate margin
 
 
+@pytest.mark.parametrize("lanes", [4, 8])
+def test_simd_port_equals_scalar_restatement(oracle_mod, fft_keys, monkeypatch, lanes):
+    """oracle/fft_batch.c (the CPU port bench.py times) runs fft_oracle.c's operations on 4 (AVX2) or 8 (AVX-512F)
+    ciphertexts per vector: every output word equals the scalar restatement's, over a ragged group, two LUTs by
+    lut_index, skipped CMUXes (mask words that switch to 0) and the rotation's wrapped half (a >= N)."""
+    if lanes == 4:
+        monkeypatch.setenv("ORACLE_SIMD_LANES", "4")
+    elif oracle_mod.simd_lanes() != 8:
+        pytest.skip("no AVX-512F on this CPU")
+    assert oracle_mod.simd_lanes() == lanes
+    prm = oracle_mod.params(2)
+    rng = np.random.default_rng(40 + lanes)
+    B = lanes + 3
+    cts = rng.integers(0, 2**64, (B, prm.n + 1), dtype=np.uint64)
+    cts[1, : prm.n : 3] = 0
+    cts[2, : prm.n : 2] = np.uint64(3 << 62)  # switches to a = 1536 >= N
+    luts = np.stack([oracle_mod.lut_constant(N, oracle_mod.MU),
+                     oracle_mod.lut_from_table(N, 8, [(5 * m + 2) % 8 for m in range(8)], (1 << 63) // 8)])
+    idx = rng.integers(0, 2, B).astype(np.uint32)
+    ref = oracle_mod.pbs_batch_fft(prm, fft_keys, cts, luts, idx)
+    assert np.array_equal(oracle_mod.pbs_batch_fft_simd(prm, fft_keys, cts, luts, idx, threads=2), ref)
+    with pytest.raises(ValueError):
+        oracle_mod.pbs_batch_fft_simd(oracle_mod.params(3), fft_keys, cts, luts, idx)
+
+
 def test_oracle_blind_rotate_lut_table(oracle_mod, fft_keys):
     """decrypt(BR(m)) == f(m) for every message of an 8-valued table (biometrics main.rs:65-77)."""
     prm = oracle_mod.params(2)
