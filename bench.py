@@ -185,10 +185,10 @@ def cpu_baseline(cts: np.ndarray, gpu_out: np.ndarray, sample: int, threads: int
     t = time.time()
     O.pbs_batch(prm, keys, sel[:1], lut, idx[:1] if idx is not None else None, threads=1)  # one PBS, one thread
     lat_ms = (time.time() - t) * 1e3
-    # P-GATE FFT64: the timed leg is the SIMD port (oracle/fft_batch.c: the scalar restatement's operations on 8
+    # FFT64 presets: the timed leg is the SIMD port (oracle/fft_batch.c: the scalar restatement's operations on 8
     # AVX-512 or 4 AVX2 lanes, bit-identical to it -- tests/test_fft.py), the fairer CPU figure; one SIMD group on
-    # one thread gives its per-PBS latency.  Other presets: the scalar restatement, one PBS per thread.
-    simd = prm.transform == 1 and prm.N == 1024 and prm.order == 0
+    # one thread gives its per-PBS latency.  NTT presets: the scalar restatement, one PBS per thread.
+    simd = prm.transform == 1
     simd_lat = None
     if simd:
         lanes = O.simd_lanes()

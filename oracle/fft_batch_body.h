@@ -21,6 +21,15 @@ typedef struct {
   or_c64 twIm[8][64];  /* zeta^{(n0 + 8 e)(4 k0 + 1)}, L = n0 + 8 k0 */
 } or_fftb_tab;
 const or_fftb_tab* or_fftb_tables(void);
+/* fft_oracle.c's fft1k_tab (N = 2048) */
+typedef struct {
+  or_c64 slot[16];    /* zeta^{64 e}, zeta = e^{2 pi i / 4096} */
+  or_c64 ta[16][64];  /* zeta^{L (1 + 4 k)} */
+  or_c64 tb[4][16];   /* e^{2 pi i l0 m / 64} */
+} or_fftb_tab1k;
+const or_fftb_tab1k* or_fftb_tables1k(void);
+/* or_mod_switch(x, 4096) */
+static inline uint32_t ms4096(uint64_t x) { return (uint32_t)((((x >> 51) + 1) >> 1) & 4095u); }
 
 /* or_mod_switch(x, 2048) */
 static inline uint32_t ms2048(uint64_t x) { return (uint32_t)((((x >> 52) + 1) >> 1) & 2047u); }
@@ -257,4 +266,214 @@ void BR_SIMD(const or_params* p, const or_c64* bsk_f, const uint64_t* const* lwe
   free(acc); free(rot); free(dig); free(res); free(D); free(O); free(Oc);
 }
 
+
+/* ---- N = 2048 (P-FHEVM): fft_oracle.c fft1k_fwd / fft1k_inv, dft16, radix-4, operation for operation ---- */
+#define C16 0.92387953251128675613
+#define S16 0.38268343236508977173
+static inline void radix4(CX* x, int i0, int st, int inv) {
+  const CX a = x[i0], b = x[i0 + st], c = x[i0 + 2 * st], d = x[i0 + 3 * st];
+  const CX t0 = cadd(a, c), t1 = csub(a, c), t2 = cadd(b, d), t3 = csub(b, d);
+  x[i0] = cadd(t0, t2);
+  x[i0 + 2 * st] = csub(t0, t2);
+  const CX p = {t1.re - t3.im, t1.im + t3.re}, q = {t1.re + t3.im, t1.im - t3.re};
+  x[i0 + st] = inv ? q : p;
+  x[i0 + 3 * st] = inv ? p : q;
+}
+/* t * W16^k (inv: conj) for the k dft16 uses: 1, 3, 9 as cmul, 4 = i */
+static inline CX w16(CX t, int k, int inv) {
+  switch (k) {
+    case 1: return inv ? cmul(t, C16, -S16) : cmul(t, C16, S16);
+    case 3: return inv ? cmul(t, S16, -C16) : cmul(t, S16, C16);
+    case 9: return inv ? cmul(t, -C16, S16) : cmul(t, -C16, -S16);
+    default: {
+      CX r;
+      if (!inv) { r.re = -t.im; r.im = t.re; } else { r.re = t.im; r.im = -t.re; }
+      return r;
+    }
+  }
+}
+static inline CX w8u(CX t, int j, int inv) {
+  const VD p = t.re, q = t.im;
+  CX r;
+  if (j == 1) {
+    if (!inv) { r.re = p - q; r.im = p + q; } else { r.re = p + q; r.im = q - p; }
+  } else {
+    if (!inv) { r.re = -(p + q); r.im = p - q; } else { r.re = q - p; r.im = -(p + q); }
+  }
+  return r;
+}
+static inline void radix4_s(CX* x, int i0, int cs, int inv) {
+  const CX a = x[i0], b = x[i0 + 1], c = x[i0 + 2], d = x[i0 + 3];
+  const VD s = BC(SQRT1_2), ns = BC(-SQRT1_2);
+  CX t0, t1, A, C, p, q;
+  if (cs) {
+    t0.re = VF(s, c.re, a.re); t0.im = VF(s, c.im, a.im);
+    t1.re = VF(ns, c.re, a.re); t1.im = VF(ns, c.im, a.im);
+    const CX t2 = cadd(b, d), t3 = csub(b, d);
+    A = cadd(t0, t2);
+    C = csub(t0, t2);
+    p.re = t1.re - t3.im; p.im = t1.im + t3.re;
+    q.re = t1.re + t3.im; q.im = t1.im - t3.re;
+  } else {
+    t0 = cadd(a, c);
+    t1 = csub(a, c);
+    const CX t2 = cadd(b, d), t3 = csub(b, d);
+    A.re = VF(s, t2.re, t0.re); A.im = VF(s, t2.im, t0.im);
+    C.re = VF(ns, t2.re, t0.re); C.im = VF(ns, t2.im, t0.im);
+    p.re = VF(ns, t3.im, t1.re); p.im = VF(s, t3.re, t1.im);
+    q.re = VF(s, t3.im, t1.re); q.im = VF(ns, t3.re, t1.im);
+  }
+  x[i0] = A;
+  x[i0 + 2] = C;
+  x[i0 + 1] = inv ? q : p;
+  x[i0 + 3] = inv ? p : q;
+}
+static inline void dft16(CX x[16], int inv) {
+  for (int n0 = 0; n0 < 4; n0++) radix4(x, n0, 4, inv);
+  radix4(x, 0, 1, inv);
+  x[5] = w16(x[5], 1, inv);
+  x[6] = w8u(x[6], 1, inv);
+  x[7] = w16(x[7], 3, inv);
+  radix4_s(x, 4, 1, inv);
+  x[9] = w8u(x[9], 1, inv);
+  x[10] = w16(x[10], 4, inv);
+  x[11] = w8u(x[11], 3, inv);
+  radix4_s(x, 8, 0, inv);
+  x[13] = w16(x[13], 3, inv);
+  x[14] = w8u(x[14], 3, inv);
+  x[15] = w16(x[15], 9, inv);
+  radix4_s(x, 12, 1, inv);
+  CX y[16];
+  for (int k0 = 0; k0 < 4; k0++)
+    for (int k1 = 0; k1 < 4; k1++) y[k0 + 4 * k1] = x[4 * k0 + k1];
+  memcpy(x, y, sizeof(y));
+}
+/* X, Y, Z: 64 x 16 workspaces each */
+static void fwd2k(const VD* a, CX* out, const or_fftb_tab1k* T, CX (*X)[16], CX (*Y)[16]) {
+  for (int L = 0; L < 64; L++) {
+    CX* x = X[L];
+    for (int e = 0; e < 16; e++) {
+      const CX v = {a[L + 64 * e], a[L + 64 * e + 1024]};
+      x[e] = e ? cmul(v, T->slot[e].re, T->slot[e].im) : v;
+    }
+    dft16(x, 0);
+    for (int k = 0; k < 16; k++) x[k] = cmul(x[k], T->ta[k][L].re, T->ta[k][L].im);
+  }
+  for (int Lp = 0; Lp < 64; Lp++)
+    for (int sp = 0; sp < 16; sp++) Y[Lp][sp] = X[(Lp & 15) | ((sp >> 2) << 4)][(sp & 3) | ((Lp >> 4) << 2)];
+  for (int Lp = 0; Lp < 64; Lp++) {
+    CX* y = Y[Lp];
+    for (int g = 0; g < 4; g++) {
+      radix4(y, g, 4, 0);
+      for (int m = 1; m < 4; m++) y[g + 4 * m] = cmul(y[g + 4 * m], T->tb[m][Lp & 15].re, T->tb[m][Lp & 15].im);
+    }
+  }
+  for (int Lpp = 0; Lpp < 64; Lpp++) {
+    CX z[16];
+    for (int r = 0; r < 16; r++) z[r] = Y[r + 16 * (Lpp >> 4)][Lpp & 15];
+    dft16(z, 0);
+    for (int m = 0; m < 16; m++) out[Lpp + 64 * m] = z[m];
+  }
+}
+static void inv2k(const CX* in, VD* a, const or_fftb_tab1k* T, CX (*X)[16], CX (*Y)[16], CX (*Z)[16]) {
+  for (int Lpp = 0; Lpp < 64; Lpp++) {
+    for (int m = 0; m < 16; m++) Z[Lpp][m] = in[Lpp + 64 * m];
+    dft16(Z[Lpp], 1);
+  }
+  for (int Lp = 0; Lp < 64; Lp++) {
+    CX* y = Y[Lp];
+    for (int sp = 0; sp < 16; sp++) y[sp] = Z[sp + 16 * (Lp >> 4)][Lp & 15];
+    for (int g = 0; g < 4; g++) {
+      for (int m = 1; m < 4; m++) y[g + 4 * m] = cmul(y[g + 4 * m], T->tb[m][Lp & 15].re, -T->tb[m][Lp & 15].im);
+      radix4(y, g, 4, 1);
+    }
+  }
+  for (int L = 0; L < 64; L++) {
+    CX* x = X[L];
+    for (int k = 0; k < 16; k++)
+      x[k] = cmul(Y[(L & 15) | ((k >> 2) << 4)][(k & 3) | ((L >> 4) << 2)], T->ta[k][L].re, -T->ta[k][L].im);
+    dft16(x, 1);
+    for (int e = 0; e < 16; e++) {
+      const CX v = e ? cmul(x[e], T->slot[e].re, -T->slot[e].im) : x[e];
+      a[L + 64 * e] = v.re;
+      a[L + 64 * e + 1024] = v.im;
+    }
+  }
+}
+
+/* or_decompose at base_log 23 x 1 level (digits up to 2^22: exact through the same 1.5 2^52 bias) */
+static inline VD decompose_23x1(VU x) {
+  const VU one = BCU(1), m23 = BCU(0x7FFFFF);
+  const VU res = (((x >> 40) + one) >> 1) & m23;
+  const VU carry = (((res - one) & res) >> 22) & one;
+  return (VD)((res - (carry << 23)) + BCU(0x4338000000000000ull)) - BC(0x1.8p52);
+}
+
+/* blind rotation of BW ciphertexts at N = 2048, k = 1, 2^23 x 1 (fft_oracle.c blind_rotate_fft_impl: ONE fma chain
+ * per output over (c, l) from zero) */
+void BR_SIMD_2K(const or_params* p, const or_c64* bsk_f, const uint64_t* const* lwe, const uint64_t* const* lut,
+                uint64_t* const* acc_out) {
+  enum { N2 = 2048, M2 = 1024 };
+  const or_fftb_tab1k* T = or_fftb_tables1k();
+  const uint32_t n = p->n;
+  const size_t per_i = (size_t)2 * 1 * 2 * M2;
+  VU* acc = (VU*)aligned_alloc(64, sizeof(VU) * 2 * N2);
+  VU* rot = (VU*)aligned_alloc(64, sizeof(VU) * N2);
+  VD* dig = (VD*)aligned_alloc(64, sizeof(VD) * N2);
+  VD* res = (VD*)aligned_alloc(64, sizeof(VD) * N2);
+  CX* D = (CX*)aligned_alloc(64, sizeof(CX) * M2);
+  CX* O = (CX*)aligned_alloc(64, sizeof(CX) * 2 * M2);
+  CX(*X)[16] = (CX(*)[16])aligned_alloc(64, sizeof(CX) * 64 * 16);
+  CX(*Y)[16] = (CX(*)[16])aligned_alloc(64, sizeof(CX) * 64 * 16);
+  CX(*Z)[16] = (CX(*)[16])aligned_alloc(64, sizeof(CX) * 64 * 16);
+  for (int q = 0; q < BW; q++) {
+    const uint32_t bt = ms4096(lwe[q][n]), t = (2 * N2 - bt) % (2 * N2);
+    for (uint32_t j = 0; j < N2; j++) {
+      int64_t d = (int64_t)j - (int64_t)t;
+      int neg = 0;
+      while (d < 0) { d += N2; neg ^= 1; }
+      const uint64_t v = or_p_to_tor(lut[q][d]);
+      acc[j][q] = 0;
+      acc[N2 + j][q] = neg ? 0 - v : v;
+    }
+  }
+  const VD zero = BC(0.0);
+  for (uint32_t i = 0; i < n; i++) {
+    uint32_t a[BW];
+    for (int q = 0; q < BW; q++) a[q] = ms4096(lwe[q][i]);
+    const double* Kb = (const double*)(bsk_f + per_i * i);
+    for (uint32_t f = 0; f < 2 * M2; f++) { O[f].re = zero; O[f].im = zero; }
+    for (uint32_t c = 0; c < 2; c++) {
+      const VU* ac = acc + (size_t)c * N2;
+      for (int q = 0; q < BW; q++) {
+        const uint32_t r = a[q] & (N2 - 1);
+        const uint64_t s0 = a[q] >= N2 ? ~0ull : 0, s1 = ~s0;
+        for (uint32_t j = 0; j < r; j++) rot[j][q] = (ac[j + N2 - r][q] ^ s1) - s1;
+        for (uint32_t j = r; j < N2; j++) rot[j][q] = (ac[j - r][q] ^ s0) - s0;
+      }
+      for (uint32_t j = 0; j < N2; j++) dig[j] = decompose_23x1(rot[j] - ac[j]);
+      fwd2k(dig, D, T, X, Y);
+      const double* row = Kb + 2 * ((size_t)c * 2 * M2);
+      for (uint32_t j = 0; j < 2; j++) {
+        const double* K = row + 2 * (size_t)j * M2;
+        CX* A = O + (size_t)j * M2;
+        for (uint32_t f = 0; f < M2; f++) {
+          const VD kr = BC(K[2 * f]), ki = BC(K[2 * f + 1]);
+          A[f].re = VF(D[f].re, kr, A[f].re);
+          A[f].re = VF(-D[f].im, ki, A[f].re);
+          A[f].im = VF(D[f].re, ki, A[f].im);
+          A[f].im = VF(D[f].im, kr, A[f].im);
+        }
+      }
+    }
+    for (uint32_t j = 0; j < 2; j++) {
+      inv2k(O + (size_t)j * M2, res, T, X, Y, Z);
+      VU* aj = acc + (size_t)j * N2;
+      for (uint32_t f = 0; f < N2; f++) aj[f] = aj[f] + torus_dev(res[f]);
+    }
+  }
+  for (int q = 0; q < BW; q++)
+    for (uint32_t j = 0; j < 2 * N2; j++) acc_out[q][j] = acc[j][q];
+  free(acc); free(rot); free(dig); free(res); free(D); free(O); free(X); free(Y); free(Z);
+}
 #endif /* BW */

@@ -364,19 +364,23 @@ def pbs_batch_fft(prm: Params, keys: Keys, lwe_in: np.ndarray, luts: np.ndarray,
 
 
 def pbs_batch_fft_simd(prm: Params, keys: Keys, lwe_in: np.ndarray, luts: np.ndarray, lut_index=None,
-                       threads: int = 0) -> np.ndarray:
-    """P-GATE FFT64 PBS with 8 (AVX-512) or 4 (AVX2) ciphertexts per vector (fft_batch.c): bit-identical to
-    pbs_batch_fft, the CPU port bench.py times.  Other parameter sets raise ValueError."""
+                       threads: int = 0, ms: bool = True) -> np.ndarray:
+    """FFT64 PBS with 8 (AVX-512) or 4 (AVX2) ciphertexts per vector (fft_batch.c): bit-identical to pbs_batch_fft
+    at P-GATE (BR -> SE -> KS) and P-FHEVM (KS -> MS -> BR -> SE); the CPU port bench.py times.  Other parameter sets
+    raise ValueError."""
     lwe_in = np.ascontiguousarray(lwe_in, dtype=np.uint64)
     luts = np.ascontiguousarray(luts, dtype=np.uint64).reshape(-1, prm.N)
     B = lwe_in.shape[0]
-    out = np.zeros((B, prm.n + 1), dtype=np.uint64)
+    dout = (prm.n if prm.order == 0 else prm.k * prm.N) + 1
+    out = np.zeros((B, dout), dtype=np.uint64)
     li = np.ascontiguousarray(lut_index, dtype=np.uint32) if lut_index is not None else None
-    rc = lib().or_pbs_batch_fft_simd(ctypes.byref(prm), _p(keys.bsk_fourier, ctypes.c_void_p), _p(keys.ksk),
-                                     _p(lwe_in), ctypes.c_size_t(B), _p(luts), ctypes.c_size_t(luts.shape[0]),
-                                     _p(li, U32P) if li is not None else None, _p(out), ctypes.c_int(threads))
+    msk = keys.ms_key(ms)
+    rc = lib().or_pbs_batch_fft_simd_ex(ctypes.byref(prm), _p(keys.bsk_fourier, ctypes.c_void_p), _p(keys.ksk),
+                                        ctypes.byref(msk) if msk else None, _p(lwe_in), ctypes.c_size_t(B), _p(luts),
+                                        ctypes.c_size_t(luts.shape[0]), _p(li, U32P) if li is not None else None,
+                                        _p(out), ctypes.c_int(threads))
     if rc != 0:
-        raise ValueError("or_pbs_batch_fft_simd: P-GATE FFT64 parameters only")
+        raise ValueError("or_pbs_batch_fft_simd_ex: the FFT64 presets (P-GATE, P-FHEVM) only")
     return out
 
 

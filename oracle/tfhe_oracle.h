@@ -258,10 +258,13 @@ void or_pbs_batch_fft(const or_params* p, const or_c64* bsk_f, const uint64_t* k
 void or_pbs_batch_fft_ex(const or_params* p, const or_c64* bsk_f, const uint64_t* ksk, const or_ms_key* ms,
                          const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
                          const uint32_t* lut_index, uint64_t* lwe_out, int threads);
-/* fft_batch.c: or_pbs_batch_fft for P-GATE FFT64 (N = 1024, k = 1, order 0) with 8 (AVX-512) or 4 (AVX2) ciphertexts per vector,
+/* fft_batch.c: or_pbs_batch_fft(_ex) for the FFT64 presets (P-GATE, P-FHEVM) with 8 (AVX-512) or 4 (AVX2) ciphertexts per vector,
  * the same operations in the same order (bit-identical outputs); -1 for any other parameter set */
 int or_pbs_batch_fft_simd(const or_params* p, const or_c64* bsk_f, const uint64_t* ksk, const uint64_t* lwe_in, size_t B,
                           const uint64_t* luts, size_t n_lut, const uint32_t* lut_index, uint64_t* lwe_out, int threads);
+int or_pbs_batch_fft_simd_ex(const or_params* p, const or_c64* bsk_f, const uint64_t* ksk, const or_ms_key* ms,
+                             const uint64_t* lwe_in, size_t B, const uint64_t* luts, size_t n_lut,
+                             const uint32_t* lut_index, uint64_t* lwe_out, int threads); /* + P-FHEVM FFT64 (order 1) */
 int or_fft_batch_lanes(void); /* 8 (AVX-512F) or 4 (AVX2, or ORACLE_SIMD_LANES=4) */
 /* exact negacyclic product over Z_2^64 (wrapping): the independent arbiter of the FFT's rounding */
 void or_poly_mul_torus_schoolbook(uint64_t* out, const int64_t* a, const uint64_t* b, uint32_t N);

@@ -207,7 +207,28 @@ def test_simd_port_equals_scalar_restatement(oracle_mod, fft_keys, monkeypatch, 
     ref = oracle_mod.pbs_batch_fft(prm, fft_keys, cts, luts, idx)
     assert np.array_equal(oracle_mod.pbs_batch_fft_simd(prm, fft_keys, cts, luts, idx, threads=2), ref)
     with pytest.raises(ValueError):
-        oracle_mod.pbs_batch_fft_simd(oracle_mod.params(3), fft_keys, cts, luts, idx)
+        oracle_mod.pbs_batch_fft_simd(oracle_mod.params(0), fft_keys, cts, luts, idx)
+
+
+@pytest.mark.parametrize("lanes", [4, 8])
+def test_simd_port_equals_scalar_restatement_fhevm(oracle_mod, monkeypatch, lanes):
+    """The same at P-FHEVM (N = 2048, 2^23 x 1, KS -> MS noise reduction -> BR -> SE): the 1024-point transforms, the
+    one-chain MAC from zero and the grouped keyswitch on the lanes equal the scalar restatement word for word, with
+    and without the noise reduction, over a ragged group and two LUTs."""
+    if lanes == 4:
+        monkeypatch.setenv("ORACLE_SIMD_LANES", "4")
+    elif oracle_mod.simd_lanes() != 8:
+        pytest.skip("no AVX-512F on this CPU")
+    prm = oracle_mod.params(3)
+    keys = oracle_mod.Keys(prm, KEY_SEED)
+    rng = np.random.default_rng(50 + lanes)
+    B = lanes + 2
+    cts = rng.integers(0, 2**64, (B, prm.k * prm.N + 1), dtype=np.uint64)
+    luts = np.stack([oracle_mod.lut_constant(prm.N, 1 << 59), oracle_mod.lut_constant(prm.N, 3 << 59)])
+    idx = rng.integers(0, 2, B).astype(np.uint32)
+    for ms in (True, False):
+        ref = oracle_mod.pbs_batch_fft(prm, keys, cts, luts, idx, ms=ms)
+        assert np.array_equal(oracle_mod.pbs_batch_fft_simd(prm, keys, cts, luts, idx, threads=2, ms=ms), ref)
 
 
 def test_oracle_blind_rotate_lut_table(oracle_mod, fft_keys):
