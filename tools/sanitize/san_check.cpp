@@ -72,6 +72,16 @@ static void run_preset(int preset) {
     or_bsk_to_fourier(&q, bsk.data(), bf.data());
     or_pbs_batch_fft_ex(&q, bf.data(), ksk.data(), p.order == 1 ? &ms : nullptr, cts.data(), B, lut.data(), 1,
                         nullptr, out.data(), 1);
+    // the SIMD port (fft_batch.c) on the same inputs at both widths: bit-identical outputs
+    for (const char* lanes : {"4", "8"}) {
+      setenv("ORACLE_SIMD_LANES", lanes, 1);
+      if (lanes[0] == '8' && or_fft_batch_lanes() != 8) continue;
+      std::vector<uint64_t> out2(out.size());
+      CHECK(or_pbs_batch_fft_simd_ex(&q, bf.data(), ksk.data(), p.order == 1 ? &ms : nullptr, cts.data(), B,
+                                     lut.data(), 1, nullptr, out2.data(), 2) == 0);
+      CHECK(out2 == out);
+    }
+    unsetenv("ORACLE_SIMD_LANES");
   } else {
     std::vector<uint64_t> bn(bl);
     or_bsk_to_ntt(&q, bsk.data(), bn.data());
